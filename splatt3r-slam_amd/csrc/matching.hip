@@ -1,0 +1,335 @@
+// Dense correspondence kernels behind include/s3m.h.
+//
+// Restates splatt3r_slam/backend/src/matching_kernels.cu (iter_proj
+// :118-274, refine_matches :24-80) and the torch glue of
+// splatt3r_slam/matching.py:25-90 / image.py:5-38 as wave64 kernels:
+// 256-thread blocks (4 waves) instead of the reference's 16-thread blocks
+// (a quarter wave), one query point per lane.  This file is compiled with
+// -ffp-contract=off so that the arithmetic is the strict evaluation of the
+// reference source text (see s3m.h).
+#include "common.hpp"
+#include "s3m.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ float clampf(float x, float lo, float hi) {
+  return fminf(fmaxf(x, lo), hi);
+}
+
+// Bilinear sample of channels [c0, c0+3) of the 9-channel ray image at
+// (u, v); weights exactly as matching_kernels.cu:150-180 ("pixels are
+// opposite the area calc").
+struct Taps {
+  const float* r11;  // (v11+1, u11+1)
+  const float* r12;  // (v11+1, u11)
+  const float* r21;  // (v11,   u11+1)
+  const float* r22;  // (v11,   u11)
+  float w11, w12, w21, w22;
+};
+
+__device__ __forceinline__ Taps make_taps(const float* img, int w, float u, float v) {
+  Taps t;
+  int u11 = (int)floorf(u);
+  int v11 = (int)floorf(v);
+  float du = u - (float)u11;
+  float dv = v - (float)v11;
+  t.w11 = du * dv;
+  t.w12 = (float)((1.0 - (double)du) * (double)dv);
+  t.w21 = (float)((double)du * (1.0 - (double)dv));
+  t.w22 = (float)((1.0 - (double)du) * (1.0 - (double)dv));
+  t.r11 = img + ((int64_t)(v11 + 1) * w + (u11 + 1)) * 9;
+  t.r12 = img + ((int64_t)(v11 + 1) * w + u11) * 9;
+  t.r21 = img + ((int64_t)v11 * w + (u11 + 1)) * 9;
+  t.r22 = img + ((int64_t)v11 * w + u11) * 9;
+  return t;
+}
+
+__device__ __forceinline__ float lerp_ch(const Taps& t, int c) {
+  return t.w11 * t.r11[c] + t.w12 * t.r12[c] + t.w21 * t.r21[c] + t.w22 * t.r22[c];
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_iter_proj(const float* __restrict__ rays_img, const float* __restrict__ pts,
+            const float* __restrict__ p_init, float* __restrict__ p_new,
+            uint8_t* __restrict__ converged_out, int h, int w, int n,
+            int max_iter, float lambda_init, float cost_thresh) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (i >= n) return;
+  const float* img = rays_img + b * (int64_t)h * w * 9;
+  const int64_t pi = b * (int64_t)n + i;
+  float u = clampf(p_init[pi * 2 + 0], 1.0f, (float)(w - 2));
+  float v = clampf(p_init[pi * 2 + 1], 1.0f, (float)(h - 2));
+  const float p0 = pts[pi * 3 + 0], p1 = pts[pi * 3 + 1], p2 = pts[pi * 3 + 2];
+
+  float lambda = lambda_init;
+  bool converged = false;
+  for (int it = 0; it < max_iter; ++it) {
+    Taps t = make_taps(img, w, u, v);
+    float r0 = lerp_ch(t, 0), r1 = lerp_ch(t, 1), r2 = lerp_ch(t, 2);
+    float gx0 = lerp_ch(t, 3), gx1 = lerp_ch(t, 4), gx2 = lerp_ch(t, 5);
+    float gy0 = lerp_ch(t, 6), gy1 = lerp_ch(t, 7), gy2 = lerp_ch(t, 8);
+    float r_norm = sqrtf(r0 * r0 + r1 * r1 + r2 * r2);
+    float r_norm_inv = (float)(1.0 / (double)r_norm);
+    r0 *= r_norm_inv; r1 *= r_norm_inv; r2 *= r_norm_inv;
+    float e0 = r0 - p0, e1 = r1 - p1, e2 = r2 - p2;
+    float cost = e0 * e0 + e1 * e1 + e2 * e2;
+
+    float A00 = gx0 * gx0 + gx1 * gx1 + gx2 * gx2;
+    float A01 = gx0 * gy0 + gx1 * gy1 + gx2 * gy2;
+    float A11 = gy0 * gy0 + gy1 * gy1 + gy2 * gy2;
+    float b0 = -(e0 * gx0 + e1 * gx1 + e2 * gx2);
+    float b1 = -(e0 * gy0 + e1 * gy1 + e2 * gy2);
+    A00 += lambda;
+    A11 += lambda;
+    float det_inv = (float)(1.0 / (double)(A00 * A11 - A01 * A01));
+    float delta_u = det_inv * (A11 * b0 - A01 * b1);
+    float delta_v = det_inv * (-A01 * b0 + A00 * b1);
+
+    float u_new = clampf(u + delta_u, 1.0f, (float)(w - 2));
+    float v_new = clampf(v + delta_v, 1.0f, (float)(h - 2));
+
+    Taps t2 = make_taps(img, w, u_new, v_new);
+    float q0 = lerp_ch(t2, 0), q1 = lerp_ch(t2, 1), q2 = lerp_ch(t2, 2);
+    float q_norm = sqrtf(q0 * q0 + q1 * q1 + q2 * q2);
+    float q_norm_inv = (float)(1.0 / (double)q_norm);
+    q0 *= q_norm_inv; q1 *= q_norm_inv; q2 *= q_norm_inv;
+    float f0 = q0 - p0, f1 = q1 - p1, f2 = q2 - p2;
+    float new_cost = f0 * f0 + f1 * f1 + f2 * f2;
+
+    if (new_cost < cost) {
+      u = u_new;
+      v = v_new;
+      lambda = (float)((double)lambda * 0.1);
+      converged = new_cost < cost_thresh;
+    } else {
+      lambda = (float)((double)lambda * 10.0);
+      converged = cost < cost_thresh;
+    }
+  }
+  p_new[pi * 2 + 0] = u;
+  p_new[pi * 2 + 1] = v;
+  converged_out[pi] = converged ? 1 : 0;
+}
+
+// c10::Half dot product: every product and partial sum rounded to fp16.
+// Initial best score: cuda::std::numeric_limits<c10::Half>::min() in the
+// reference (:46).  c10::Half has no cuda::std specialisation, so the
+// primary template returns Half() == 0; see DESIGN.md "refine_matches".
+template <int F>
+__global__ void __launch_bounds__(kBlock)
+k_refine(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
+         const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h,
+         int w, int n, int fdim_rt, int radius, int dilation_max) {
+  const int fdim = F > 0 ? F : fdim_rt;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (i >= n) return;
+  const int64_t pi = b * (int64_t)n + i;
+  const _Float16* d21 = D21 + pi * fdim;
+  const _Float16* d11 = D11 + b * (int64_t)h * w * fdim;
+
+  float q[F > 0 ? F : 1];
+  if constexpr (F > 0) {
+#pragma unroll
+    for (int k = 0; k < F; ++k) q[k] = (float)d21[k];
+  }
+
+  int64_t u0 = p1[pi * 2 + 0];
+  int64_t v0 = p1[pi * 2 + 1];
+  _Float16 max_score = (_Float16)0.0f;
+  int64_t u_new = u0, v_new = v0;
+  for (int d = dilation_max; d > 0; --d) {
+    const int rd = radius * d;
+    const int diam = 2 * rd + 1;
+    for (int ii = 0; ii < diam; ii += d) {
+      for (int jj = 0; jj < diam; jj += d) {
+        const int64_t u = u0 - rd + ii;
+        const int64_t v = v0 - rd + jj;
+        if (v >= 0 && v < h && u >= 0 && u < w) {
+          const _Float16* row = d11 + (v * w + u) * fdim;
+          _Float16 score = (_Float16)0.0f;
+          if constexpr (F > 0) {
+#pragma unroll
+            for (int k = 0; k < F; ++k) {
+              _Float16 prod = (_Float16)(q[k] * (float)row[k]);
+              score = (_Float16)((float)score + (float)prod);
+            }
+          } else {
+            for (int k = 0; k < fdim; ++k) {
+              _Float16 prod = (_Float16)((float)d21[k] * (float)row[k]);
+              score = (_Float16)((float)score + (float)prod);
+            }
+          }
+          if ((float)score > (float)max_score) {
+            max_score = score;
+            u_new = u;
+            v_new = v;
+          }
+        }
+      }
+    }
+    u0 = u_new;
+    v0 = v_new;
+  }
+  p1_new[pi * 2 + 0] = u_new;
+  p1_new[pi * 2 + 1] = v_new;
+}
+
+// |x| / max(||x||, 1e-12) (F.normalize), strict order ((x0^2+x1^2)+x2^2).
+__device__ __forceinline__ void normalize3(const float* x, float* o) {
+  float nrm = sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+  float d = fmaxf(nrm, 1e-12f);
+  o[0] = x[0] / d; o[1] = x[1] / d; o[2] = x[2] / d;
+}
+
+__device__ __forceinline__ int reflect(int i, int n) {
+  return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
+}
+
+// prep_for_iter_proj: one thread per pixel of X11 / X21.
+__global__ void __launch_bounds__(kBlock)
+k_prep(const float* __restrict__ X11, const float* __restrict__ X21,
+       const int64_t* __restrict__ idx_init, float* __restrict__ rays_out,
+       float* __restrict__ pts_out, float* __restrict__ p_init, int h, int w) {
+  const int64_t hw = (int64_t)h * w;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (i >= hw) return;
+  const int y = (int)(i / w), x = (int)(i % w);
+  const float* X = X11 + b * hw * 3;
+  float r[3][3][3];
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      int yy = reflect(y + dy - 1, h), xx = reflect(x + dx - 1, w);
+      normalize3(X + ((int64_t)yy * w + xx) * 3, r[dy][dx]);
+    }
+  float* o = rays_out + (b * hw + i) * 9;
+  const float k3 = 3.0f / 32.0f, k10 = 10.0f / 32.0f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    o[c] = r[1][1][c];
+    // Scharr x: [[-3,0,3],[-10,0,10],[-3,0,3]]/32, row-major tap order.
+    float gx = -k3 * r[0][0][c] + k3 * r[0][2][c] - k10 * r[1][0][c] +
+               k10 * r[1][2][c] - k3 * r[2][0][c] + k3 * r[2][2][c];
+    // Scharr y: [[-3,-10,-3],[0,0,0],[3,10,3]]/32.
+    float gy = -k3 * r[0][0][c] - k10 * r[0][1][c] - k3 * r[0][2][c] +
+               k3 * r[2][0][c] + k10 * r[2][1][c] + k3 * r[2][2][c];
+    o[3 + c] = gx;
+    o[6 + c] = gy;
+  }
+  float pn[3];
+  normalize3(X21 + (b * hw + i) * 3, pn);
+  pts_out[(b * hw + i) * 3 + 0] = pn[0];
+  pts_out[(b * hw + i) * 3 + 1] = pn[1];
+  pts_out[(b * hw + i) * 3 + 2] = pn[2];
+  int64_t lin = idx_init ? idx_init[b * hw + i] : i;
+  p_init[(b * hw + i) * 2 + 0] = (float)(lin % w);
+  p_init[(b * hw + i) * 2 + 1] = (float)(lin / w);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_occlusion(const float* __restrict__ p, const uint8_t* __restrict__ conv,
+            const float* __restrict__ X11, const float* __restrict__ X21,
+            int64_t* __restrict__ p1, uint8_t* __restrict__ valid, int h, int w,
+            float dist_thresh) {
+  const int64_t hw = (int64_t)h * w;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (i >= hw) return;
+  const int64_t pi = b * hw + i;
+  int64_t u = (int64_t)p[pi * 2 + 0];
+  int64_t v = (int64_t)p[pi * 2 + 1];
+  p1[pi * 2 + 0] = u;
+  p1[pi * 2 + 1] = v;
+  const float* a = X11 + (b * hw + v * w + u) * 3;
+  const float* c = X21 + pi * 3;
+  float d0 = a[0] - c[0], d1 = a[1] - c[1], d2 = a[2] - c[2];
+  float dist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+  valid[pi] = (conv[pi] && dist < dist_thresh) ? 1 : 0;
+}
+
+__global__ void k_pixel_to_lin(const int64_t* __restrict__ p1, int64_t* __restrict__ idx,
+                               int64_t count, int w) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  idx[i] = p1[i * 2 + 0] + (int64_t)w * p1[i * 2 + 1];
+}
+
+}  // namespace
+
+extern "C" {
+
+int s3m_iter_proj(const float* rays_img_with_grad, const float* pts_3d_norm,
+                  const float* p_init, float* p_new, uint8_t* converged, int b,
+                  int h, int w, int n, int max_iter, float lambda_init,
+                  float cost_thresh, void* stream) {
+  S3_REQUIRE(b >= 0 && n >= 0 && h >= 3 && w >= 3 && max_iter >= 0,
+             "s3m_iter_proj: bad shape b=%d h=%d w=%d n=%d", b, h, w, n);
+  if (b == 0 || n == 0) return S3_OK;
+  dim3 grid((unsigned)s3::cdiv(n, kBlock), (unsigned)b);
+  k_iter_proj<<<grid, kBlock, 0, s3::as_stream(stream)>>>(
+      rays_img_with_grad, pts_3d_norm, p_init, p_new, converged, h, w, n,
+      max_iter, lambda_init, cost_thresh);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
+                       int64_t* p1_new, int b, int h, int w, int n, int fdim,
+                       int radius, int dilation_max, void* stream) {
+  S3_REQUIRE(b >= 0 && n >= 0 && h > 0 && w > 0 && fdim > 0 && radius >= 0 &&
+                 dilation_max >= 0,
+             "s3m_refine_matches: bad shape");
+  if (b == 0 || n == 0) return S3_OK;
+  dim3 grid((unsigned)s3::cdiv(n, kBlock), (unsigned)b);
+  auto d11 = reinterpret_cast<const _Float16*>(D11);
+  auto d21 = reinterpret_cast<const _Float16*>(D21);
+  if (fdim == 24)
+    k_refine<24><<<grid, kBlock, 0, s3::as_stream(stream)>>>(
+        d11, d21, p1, p1_new, h, w, n, fdim, radius, dilation_max);
+  else
+    k_refine<0><<<grid, kBlock, 0, s3::as_stream(stream)>>>(
+        d11, d21, p1, p1_new, h, w, n, fdim, radius, dilation_max);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+int s3m_prep_iter_proj(const float* X11, const float* X21, const int64_t* idx_init,
+                       float* rays_with_grad, float* pts_norm, float* p_init,
+                       int b, int h, int w, void* stream) {
+  S3_REQUIRE(b >= 0 && h >= 2 && w >= 2, "s3m_prep_iter_proj: bad shape");
+  if (b == 0) return S3_OK;
+  dim3 grid((unsigned)s3::cdiv((int64_t)h * w, kBlock), (unsigned)b);
+  k_prep<<<grid, kBlock, 0, s3::as_stream(stream)>>>(X11, X21, idx_init, rays_with_grad,
+                                                    pts_norm, p_init, h, w);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+int s3m_occlusion(const float* p, const uint8_t* converged, const float* X11,
+                  const float* X21, int64_t* p1, uint8_t* valid, int b, int h,
+                  int w, float dist_thresh, void* stream) {
+  S3_REQUIRE(b >= 0 && h > 0 && w > 0, "s3m_occlusion: bad shape");
+  if (b == 0) return S3_OK;
+  dim3 grid((unsigned)s3::cdiv((int64_t)h * w, kBlock), (unsigned)b);
+  k_occlusion<<<grid, kBlock, 0, s3::as_stream(stream)>>>(p, converged, X11, X21, p1, valid,
+                                                         h, w, dist_thresh);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+int s3m_pixel_to_lin(const int64_t* p1, int64_t* idx, int64_t count, int w, void* stream) {
+  S3_REQUIRE(count >= 0 && w > 0, "s3m_pixel_to_lin: bad shape");
+  if (count == 0) return S3_OK;
+  k_pixel_to_lin<<<(unsigned)s3::cdiv(count, kBlock), kBlock, 0, s3::as_stream(stream)>>>(
+      p1, idx, count, w);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+"""ctypes binding of libsplatt3r_hip.so (the C ABI declared in include/*.h).
+
+The product path always goes through this library; there is no Python or
+torch fallback for any kernel.  If the library is missing, `lib()` raises.
+torch is imported first so that the library binds to the HIP runtime torch
+already loaded (same SONAME libamdhip64.so.7): torch's streams and device
+pointers are then valid inside the library.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see above)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_native", "libsplatt3r_hip.so")
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes).  Kept in the order of include/*.h.
+SIGNATURES: dict[str, tuple] = {
+    # s3_common.h
+    "s3_last_error": (ctypes.c_char_p, []),
+    "s3_abi_version": (I32, []),
+    "s3_arch": (ctypes.c_char_p, []),
+    # s3lie.h
+    "s3lie_sim3_mul": (I32, [P, I64, P, I64, P, I64, P]),
+    "s3lie_sim3_inv": (I32, [P, P, I64, P]),
+    "s3lie_sim3_act": (I32, [P, I64, P, P, I64, P]),
+    "s3lie_sim3_exp": (I32, [P, P, I64, P]),
+    "s3lie_sim3_log": (I32, [P, P, I64, P]),
+    "s3lie_sim3_retr": (I32, [P, I64, P, I64, P, I64, P]),
+    "s3lie_sim3_matrix": (I32, [P, P, I64, P]),
+    "s3lie_se3_matrix": (I32, [P, P, I64, P]),
+    "s3lie_pose_retr": (I32, [P, P, I64, I64, P]),
+    "s3lie_sim3_retr_host": (None, [P, P, P]),
+    "s3lie_sim3_mul_host": (None, [P, P, P]),
+    "s3lie_sim3_inv_host": (None, [P, P]),
+    # s3m.h
+    "s3m_iter_proj": (I32, [P, P, P, P, P, I32, I32, I32, I32, I32, F32, F32, P]),
+    "s3m_refine_matches": (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P]),
+    "s3m_prep_iter_proj": (I32, [P, P, P, P, P, P, I32, I32, I32, P]),
+    "s3m_occlusion": (I32, [P, P, P, P, P, P, I32, I32, I32, F32, P]),
+    "s3m_pixel_to_lin": (I32, [P, P, I64, I32, P]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def register(sigs: dict) -> None:
+    """Add signatures (used by modules that own a header)."""
+    SIGNATURES.update(sigs)
+    if _lib is not None:
+        _bind(_lib, sigs)
+
+
+def _bind(l, sigs):
+    for name, (res, args) in sigs.items():
+        fn = getattr(l, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """Load (once) and return the bound library; raises if it is missing."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(
+                        f"splatt3r-slam_amd native library not built: {LIB_PATH} "
+                        "(run __graft_entry__.build() or "
+                        "python splatt3r-slam_amd/csrc/build.py)")
+                l = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+                _bind(l, SIGNATURES)
+                _lib = l
+    return _lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = lib().s3_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {status}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    """Call an s3_status-returning entry point and raise on failure."""
+    check(getattr(lib(), name)(*args), name)
+
+
+def stream(device: torch.device | None = None) -> int:
+    """Raw hipStream_t of torch's current stream (as int for ctypes)."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def require_cuda(*tensors: torch.Tensor) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                "splatt3r-slam_amd kernels run on the GPU only; got a CPU tensor "
+                f"of shape {tuple(t.shape)} (there is no CPU fallback)")
+
+
+def require_contig(name: str, *tensors: torch.Tensor) -> None:
+    # reference: CHECK_CONTIGUOUS in splatt3r_slam/backend/src/gn.cpp
+    for t in tensors:
+        if t is not None and not t.is_contiguous():
+            raise RuntimeError(f"{name}: input must be contiguous")

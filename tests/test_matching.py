@@ -1,0 +1,161 @@
+"""Dense matching (include/s3m.h) vs the oracle restatement of
+matching_kernels.cu / matching.py, pinned by the reference-importable
+img_gradient fixture and by known-answer cases."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import GOLDEN
+
+
+def smooth_pointmap(b, h, w, rng, z=2.0):
+    """A smooth surface seen by a pinhole camera (well-posed for iter_proj)."""
+    v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    f = max(h, w)
+    x = (u - w / 2) / f
+    y = (v - h / 2) / f
+    out = []
+    for _ in range(b):
+        a = rng.normal(size=3) * 0.2
+        depth = z + a[0] * np.sin(3 * x) + a[1] * np.cos(2 * y) + a[2] * x * y
+        out.append(np.stack([x * depth, y * depth, depth], -1))
+    return np.stack(out).astype(np.float32)
+
+
+def unit_desc(b, h, w, f, rng):
+    d = rng.normal(size=(b, h, w, f)).astype(np.float32)
+    return d / np.linalg.norm(d, axis=-1, keepdims=True)
+
+
+# ------------------------------------------------------------- CPU: oracle
+def test_oracle_prep_matches_reference_img_gradient():
+    g = np.load(os.path.join(GOLDEN, "matching_prep.npz"))
+    rays, pts, p_init = oracle.prep_iter_proj(g["X11"], g["X21"])
+    # reference uses torch conv2d (summation order unspecified): fp32 tolerance
+    np.testing.assert_allclose(rays, g["rays_with_grad"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(pts, g["pts3d_norm"], rtol=1e-6, atol=1e-7)
+    b, h, w, _ = g["X11"].shape
+    assert p_init[0, w + 3].tolist() == [3.0, 1.0]
+
+
+def test_oracle_self_match_is_identity():
+    rng = np.random.default_rng(0)
+    X = smooth_pointmap(1, 24, 32, rng)
+    D = unit_desc(1, 24, 32, 24, rng)
+    idx, valid = oracle.match(X, X, D, D)
+    # border pixels are clamped into [1, w-2] x [1, h-2] by iter_proj
+    # (matching_kernels.cu:141-142) and the greedy dilated search then drifts
+    # with random descriptors; interior pixels map to themselves except where
+    # the LM estimate lands a hair below the integer (x.9999983) and `.long()`
+    # (matching.py:68) truncates it, exactly as the reference does.
+    ys, xs = np.meshgrid(np.arange(24), np.arange(32), indexing="ij")
+    inner = ((ys > 0) & (ys < 23) & (xs > 0) & (xs < 31)).ravel()
+    assert (idx[0][inner] == np.arange(24 * 32)[inner]).mean() > 0.95
+    assert valid[0, inner, 0].mean() > 0.9
+
+
+def test_oracle_iter_proj_recovers_planted_shift():
+    rng = np.random.default_rng(1)
+    h, w = 24, 32
+    X11 = smooth_pointmap(1, h, w, rng)
+    X21 = np.roll(X11, shift=(2, -3), axis=(1, 2))  # pixel (y,x) sees X11[y-2, x+3]
+    rays, pts, p_init = oracle.prep_iter_proj(X11, X21)
+    p, conv = oracle.iter_proj(rays, pts, p_init, 10, 1e-8, 1e-6)
+    p = p.reshape(h, w, 2)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    inner = (ys >= 4) & (ys < h - 2) & (xs >= 2) & (xs < w - 5)
+    np.testing.assert_allclose(p[..., 0][inner], (xs + 3)[inner], atol=0.05)
+    np.testing.assert_allclose(p[..., 1][inner], (ys - 2)[inner], atol=0.05)
+
+
+def test_oracle_refine_finds_best_descriptor():
+    rng = np.random.default_rng(2)
+    h, w, f = 20, 20, 24
+    D11 = unit_desc(1, h, w, f, rng).astype(np.float16)
+    D21 = D11[:, 10:11, 13:14].reshape(1, 1, f)  # query = descriptor at (u=13, v=10)
+    p1 = np.array([[[11, 9]]], np.int64)          # start 2 px off
+    out = oracle.refine_matches(D11, D21, p1, 3, 5)
+    assert out[0, 0].tolist() == [13, 10]
+
+
+def test_oracle_refine_all_negative_scores_keep_start():
+    h, w, f = 10, 10, 4
+    D11 = np.full((1, h, w, f), 0.5, np.float16)
+    D21 = np.full((1, 1, f), -0.5, np.float16)
+    out = oracle.refine_matches(D11, D21, np.array([[[4, 5]]], np.int64), 3, 5)
+    assert out[0, 0].tolist() == [4, 5]
+
+
+# -------------------------------------------------------------- GPU: HIP
+def _to(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+@pytest.mark.gpu
+def test_hip_prep_bitexact_vs_oracle_and_golden():
+    from splatt3r_amd.matching import prep_for_iter_proj
+    g = np.load(os.path.join(GOLDEN, "matching_prep.npz"))
+    rays, pts, p_init = prep_for_iter_proj(_to(g["X11"]), _to(g["X21"]), None)
+    r_o, p_o, pi_o = oracle.prep_iter_proj(g["X11"], g["X21"])
+    np.testing.assert_array_equal(rays.cpu().numpy(), r_o)
+    np.testing.assert_array_equal(pts.cpu().numpy(), p_o)
+    np.testing.assert_array_equal(p_init.cpu().numpy(), pi_o)
+    np.testing.assert_allclose(rays.cpu().numpy(), g["rays_with_grad"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,h,w", [(1, 24, 32), (2, 48, 64), (1, 384, 512)])
+def test_hip_iter_proj_bitexact_vs_oracle(b, h, w):
+    import mast3r_slam_backends as be
+    rng = np.random.default_rng(h)
+    X11 = smooth_pointmap(b, h, w, rng)
+    X21 = smooth_pointmap(b, h, w, rng) + rng.normal(size=(b, h, w, 3)).astype(np.float32) * 1e-3
+    rays, pts, p_init = oracle.prep_iter_proj(X11, X21)
+    p_ref, c_ref = oracle.iter_proj(rays, pts, p_init, 10, 1e-8, 1e-6)
+    p, c = be.iter_proj(_to(rays), _to(pts), _to(p_init), 10, 1e-8, 1e-6)
+    np.testing.assert_array_equal(p.cpu().numpy(), p_ref)
+    np.testing.assert_array_equal(c.cpu().numpy(), c_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("f", [24, 16])
+def test_hip_refine_bitexact_vs_oracle(f):
+    import mast3r_slam_backends as be
+    rng = np.random.default_rng(f)
+    b, h, w = 2, 40, 56
+    D11 = unit_desc(b, h, w, f, rng).astype(np.float16)
+    D21 = unit_desc(b, h, w, f, rng).astype(np.float16).reshape(b, h * w, f)
+    p1 = np.stack([rng.integers(0, w, size=(b, h * w)), rng.integers(0, h, size=(b, h * w))], -1)
+    ref = oracle.refine_matches(D11, D21, p1, 3, 5)
+    (out,) = be.refine_matches(_to(D11), _to(D21), _to(p1.astype(np.int64)), 3, 5)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+def test_hip_match_end_to_end_vs_oracle():
+    from splatt3r_amd.matching import match
+    rng = np.random.default_rng(7)
+    b, h, w = 2, 48, 64
+    X11 = smooth_pointmap(b, h, w, rng)
+    X21 = np.roll(X11, 1, axis=2) + rng.normal(size=X11.shape).astype(np.float32) * 1e-3
+    D11 = unit_desc(b, h, w, 24, rng)
+    D21 = unit_desc(b, h, w, 24, rng)
+    init = rng.integers(0, h * w, size=(b, h * w)).astype(np.int64)
+    for idx_init in (None, init):
+        idx_ref, valid_ref = oracle.match(X11, X21, D11, D21, idx_init)
+        idx, valid = match(_to(X11), _to(X21), _to(D11), _to(D21),
+                           None if idx_init is None else _to(idx_init))
+        np.testing.assert_array_equal(idx.cpu().numpy(), idx_ref)
+        np.testing.assert_array_equal(valid.cpu().numpy(), valid_ref)
+
+
+@pytest.mark.gpu
+def test_backends_reject_non_contiguous():
+    import mast3r_slam_backends as be
+    rays = torch.zeros(1, 8, 8, 9, device="cuda")
+    pts = torch.zeros(1, 3, 64, device="cuda").transpose(1, 2)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        be.iter_proj(rays, pts, torch.zeros(1, 64, 2, device="cuda"), 10, 1e-8, 1e-6)
