@@ -178,3 +178,63 @@ def match(X11, X21, D11, D21, idx_init=None, cfg=MATCH_CFG):
         p1 = refine_matches(D11h, D21h, p1, cfg["radius"], cfg["dilation_max"])
     idx = p1[..., 0] + w * p1[..., 1]
     return idx, valid[..., None]
+
+
+# ---------------------------------------------------------- rasterizer ----
+class _OracleCam(ctypes.Structure):
+    _fields_ = [("H", ctypes.c_int), ("W", ctypes.c_int), ("tanfovx", ctypes.c_float),
+                ("tanfovy", ctypes.c_float), ("scale_modifier", ctypes.c_float),
+                ("D", ctypes.c_int), ("bg", ctypes.c_float * 3),
+                ("viewmatrix", ctypes.c_float * 16), ("projmatrix", ctypes.c_float * 16),
+                ("campos", ctypes.c_float * 3)]
+
+
+def raster(settings: dict, means3D, opacities, shs=None, colors_precomp=None, scales=None,
+           rotations=None, cov3D_precomp=None, dL_dout=None, nthreads=8):
+    """graphdeco forward (+ backward if dL_dout) on the CPU.
+
+    settings: dict with image_height, image_width, tanfovx, tanfovy, bg(3),
+    scale_modifier, viewmatrix(16, memory order of the torch arg),
+    projmatrix(16), sh_degree, campos(3).
+    Returns dict(color [3,H,W], radii [P], num_rendered, and grads if asked).
+    """
+    H, W = int(settings["image_height"]), int(settings["image_width"])
+    cam = _OracleCam()
+    cam.H, cam.W = H, W
+    cam.tanfovx, cam.tanfovy = float(settings["tanfovx"]), float(settings["tanfovy"])
+    cam.scale_modifier = float(settings.get("scale_modifier", 1.0))
+    cam.D = int(settings["sh_degree"])
+    for k, n in (("bg", 3), ("viewmatrix", 16), ("projmatrix", 16), ("campos", 3)):
+        vals = np.asarray(settings[k], np.float32).ravel()
+        arr = getattr(cam, k)
+        for i in range(n):
+            arr[i] = float(vals[i])
+    m = _c(means3D, np.float32).reshape(-1, 3)
+    P = m.shape[0]
+    op = _c(opacities, np.float32).reshape(-1)
+    sh = None if shs is None else _c(shs, np.float32).reshape(P, -1, 3)
+    M = 0 if sh is None else sh.shape[1]
+    col = None if colors_precomp is None else _c(colors_precomp, np.float32).reshape(P, 3)
+    sc = None if scales is None else _c(scales, np.float32).reshape(P, 3)
+    rot = None if rotations is None else _c(rotations, np.float32).reshape(P, 4)
+    cov = None if cov3D_precomp is None else _c(cov3D_precomp, np.float32).reshape(P, 6)
+    color = np.zeros((3, H, W), np.float32)
+    radii = np.zeros(P, np.int32)
+    out = dict(color=color, radii=radii)
+    g = None
+    if dL_dout is not None:
+        g = _c(dL_dout, np.float32).reshape(3, H, W)
+        out.update(dL_dmeans2D=np.zeros((P, 3), np.float32), dL_dconic=np.zeros((P, 4), np.float32),
+                   dL_dopacity=np.zeros(P, np.float32), dL_dcolors=np.zeros((P, 3), np.float32),
+                   dL_dmeans3D=np.zeros((P, 3), np.float32), dL_dcov3D=np.zeros((P, 6), np.float32),
+                   dL_dsh=np.zeros((P, max(M, 1), 3), np.float32))
+    q = lambda a: None if a is None else _p(a)
+    f = lib().oracle_raster
+    f.restype = ctypes.c_int64
+    gk = ("dL_dmeans2D", "dL_dconic", "dL_dopacity", "dL_dcolors", "dL_dmeans3D", "dL_dcov3D",
+          "dL_dsh")
+    R = f(ctypes.byref(cam), ctypes.c_int64(P), M, _p(m), q(sc), q(rot), q(cov), q(sh), q(col),
+          _p(op), _p(color), _p(radii), q(g),
+          *[q(out[k]) if g is not None else None for k in gk], nthreads)
+    out["num_rendered"] = int(R)
+    return out

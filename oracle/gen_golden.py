@@ -51,7 +51,109 @@ def gen_matching():
     print("wrote matching_prep.npz")
 
 
-SECTIONS = {"matching": gen_matching}
+def gen_render():
+    """Capture the rasterizer boundary of the reference splat-decoder glue.
+
+    A stub `diff_gaussian_rasterization` is injected into sys.modules; the
+    reference's decoder_splatting_cuda.py / cuda_splatting.py / projection.py
+    and utils/geometry.py + utils/sh_utils.py are imported from
+    /root/reference and driven exactly as splatt3r_slam/splatt3r_utils.py:332-432
+    (splatt3r_render) drives them.  Saved: the settings the glue builds and
+    the tensors it hands to GaussianRasterizer.
+    """
+    import types
+    captured = {}
+
+    class Settings(tuple):
+        def __new__(cls, **kw):
+            o = tuple.__new__(cls, tuple(kw.values()))
+            o.kw = kw
+            return o
+
+    class Rasterizer(torch.nn.Module):
+        def __init__(self, rs):
+            super().__init__()
+            self.rs = rs
+
+        def forward(self, **kw):
+            captured["settings"] = self.rs.kw
+            captured["inputs"] = kw
+            h, w = self.rs.kw["image_height"], self.rs.kw["image_width"]
+            return torch.zeros(3, h, w), torch.zeros(kw["means3D"].shape[0], dtype=torch.int32)
+
+    stub = types.ModuleType("diff_gaussian_rasterization")
+    stub.GaussianRasterizationSettings = Settings
+    stub.GaussianRasterizer = Rasterizer
+    sys.modules["diff_gaussian_rasterization"] = stub
+    core = os.path.join(REF, "splatt3r_core")
+    ps = os.path.join(core, "src", "pixelsplat_src")
+    for p in (ps, core):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    dec = _load_file("ref_decoder_splatting_cuda", os.path.join(ps, "decoder_splatting_cuda.py"))
+    geo = _load_file("ref_geometry", os.path.join(core, "utils", "geometry.py"))
+    shu = _load_file("ref_sh_utils", os.path.join(core, "utils", "sh_utils.py"))
+
+    g = torch.Generator().manual_seed(3)
+    h, w = 16, 24
+    out = {}
+
+    def head(seed_off):
+        means = torch.randn(1, h, w, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 2.0])
+        scales = torch.exp(torch.randn(1, h, w, 3, generator=g) * 0.3 - 4.0)
+        rot = torch.randn(1, h, w, 4, generator=g)
+        rot = rot / (rot.norm(dim=-1, keepdim=True) + 1e-8)
+        sh = torch.randn(1, h, w, 3, 1, generator=g) * 0.3
+        opac = torch.rand(1, h, w, 1, generator=g)
+        return means, scales, rot, sh, opac
+
+    m1, s1, r1, sh1, o1 = head(0)
+    m2, s2, r2, sh2, o2 = head(1)
+    img1 = torch.rand(1, 3, h, w, generator=g) * 2 - 1   # ImgNorm space
+    img2 = torch.rand(1, 3, h, w, generator=g) * 2 - 1
+
+    def hwc(img):  # splatt3r_utils.py:140-150 _get_original_img_hwc
+        return (img * 0.5 + 0.5).clamp(0, 1).permute(0, 2, 3, 1)
+
+    # splatt3r_utils.py:371-407
+    cov1 = geo.build_covariance(s1, r1)
+    cov2 = geo.build_covariance(s2, r2)
+    shr1 = torch.zeros_like(sh1); shr1[..., 0] = shu.RGB2SH(hwc(img1))
+    shr2 = torch.zeros_like(sh2); shr2[..., 0] = shu.RGB2SH(hwc(img2))
+    pred1 = {"means": m1, "covariances": cov1, "sh": sh1 + shr1, "opacities": o1}
+    pred2 = {"means_in_other_view": m2, "covariances": cov2, "sh": sh2 + shr2, "opacities": o2}
+    # a non-trivial Sim3 -> 4x4 target pose (splatt3r_utils.py:153-165) and K
+    ctx_pose = torch.eye(4)[None]
+    tgt = torch.eye(4)[None].clone()
+    ang = 0.1
+    tgt[0, :3, :3] = torch.tensor([[np.cos(ang), 0, np.sin(ang)], [0, 1, 0],
+                                   [-np.sin(ang), 0, np.cos(ang)]], dtype=torch.float32) * 1.1
+    tgt[0, :3, 3] = torch.tensor([0.05, -0.02, 0.1])
+    K = torch.tensor([[[30.0, 0, 12.0], [0, 30.0, 8.0], [0, 0, 1]]])
+    batch = {"context": [{"camera_pose": ctx_pose}],
+             "target": [{"camera_pose": tgt, "camera_intrinsics": K}]}
+    decoder = dec.DecoderSplattingCUDA(background_color=[0.0, 0.0, 0.0])
+    decoder(batch, pred1, pred2, (h, w))
+    st = captured["settings"]
+    ins = captured["inputs"]
+    for k in ("tanfovx", "tanfovy", "scale_modifier", "image_height", "image_width",
+              "sh_degree"):
+        out["settings_" + k] = np.asarray(st[k])
+    for k in ("bg", "viewmatrix", "projmatrix", "campos"):
+        out["settings_" + k] = st[k].detach().numpy()
+    for k in ("means3D", "shs", "opacities", "cov3D_precomp"):
+        out["in_" + k] = ins[k].detach().contiguous().numpy()
+    # head outputs (to drive our glue with the same data)
+    for name, t in dict(m1=m1, s1=s1, r1=r1, sh1=sh1, o1=o1, m2=m2, s2=s2, r2=r2, sh2=sh2,
+                        o2=o2, img1=img1, img2=img2, ctx_pose=ctx_pose, tgt_pose=tgt,
+                        K=K).items():
+        out["head_" + name] = t.numpy()
+    np.savez_compressed(os.path.join(GOLDEN, "render_boundary.npz"), **out)
+    del sys.modules["diff_gaussian_rasterization"]
+    print("wrote render_boundary.npz", {k: v.shape for k, v in out.items() if k.startswith("in_")})
+
+
+SECTIONS = {"matching": gen_matching, "render": gen_render}
 
 
 def main(argv):

@@ -36,6 +36,7 @@ SOURCES = {
     "matching.hip": STRICT,
     "tracker.hip": STRICT,
     "raster.hip": STRICT,
+    "splat_pack.hip": STRICT,
     "net_gemm.hip": FAST,
     "net_attn.hip": FAST,
     "net_ops.hip": FAST,

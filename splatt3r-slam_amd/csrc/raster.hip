@@ -1,0 +1,791 @@
+// Tile-binned Gaussian splat rasterizer (include/gsr.h), written for gfx950.
+//
+// Forward:  preprocess (1 lane / Gaussian) -> inclusive scan of tiles touched
+//           -> duplicate (tile<<32 | depth) keys -> radix sort (stable)
+//           -> tile ranges -> blend (one 256-lane workgroup per 16x16 tile,
+//           Gaussians staged through LDS in 256-record batches, block-wide
+//           early exit).
+// Backward: per-tile back-to-front replay; per-Gaussian gradients are
+//           reduced across the wave with DPP/shuffles before one lane issues
+//           the global atomics (64x fewer atomics than one per pixel), then a
+//           per-Gaussian pass for the EWA / projection / SH chain rule.
+// Tile blocks are remapped so that each XCD (private L2) receives a
+// contiguous band of tiles: neighbouring tiles share most of their splats.
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+#include "gsr.h"
+#include "raster_math.hpp"
+
+using namespace gsr;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr size_t kAlign = 256;
+
+inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  template <typename T>
+  T* take(size_t count) {
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += align_up(count * sizeof(T));
+    return p;
+  }
+};
+
+struct GeomState {
+  float* depth;
+  float4* rec0;  // x, y, conic.a, conic.b
+  float4* rec1;  // conic.c, opacity, -, -
+  float* rgb;    // [P,3]
+  float* cov3D;  // [P,6] (scale/rotation path)
+  uint8_t* clamped;  // [P,3]
+  uint32_t* tiles;
+  uint32_t* offsets;
+  void* scan_tmp;
+  size_t scan_bytes;
+};
+
+size_t scan_temp_bytes(int64_t P) {
+  size_t bytes = 0;
+  hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                   (int)P);
+  return bytes;
+}
+
+GeomState carve_geom(void* base, int64_t P) {
+  Carver c{static_cast<char*>(base)};
+  GeomState g;
+  g.depth = c.take<float>(P);
+  g.rec0 = c.take<float4>(P);
+  g.rec1 = c.take<float4>(P);
+  g.rgb = c.take<float>(P * 3);
+  g.cov3D = c.take<float>(P * 6);
+  g.clamped = c.take<uint8_t>(P * 3);
+  g.tiles = c.take<uint32_t>(P);
+  g.offsets = c.take<uint32_t>(P);
+  g.scan_bytes = scan_temp_bytes(P);
+  g.scan_tmp = c.take<char>(g.scan_bytes);
+  return g;
+}
+size_t geom_bytes(int64_t P) {
+  Carver c{nullptr};
+  c.take<float>(P); c.take<float4>(P); c.take<float4>(P); c.take<float>(P * 3);
+  c.take<float>(P * 6); c.take<uint8_t>(P * 3); c.take<uint32_t>(P); c.take<uint32_t>(P);
+  c.take<char>(scan_temp_bytes(P));
+  return c.off;
+}
+
+struct BinningState {
+  uint64_t* keys_unsorted;
+  uint64_t* keys;
+  uint32_t* vals_unsorted;
+  uint32_t* vals;  // point_list: Gaussian index per sorted instance
+  void* sort_tmp;
+  size_t sort_bytes;
+};
+
+size_t sort_temp_bytes(int64_t R) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                     (uint32_t*)nullptr, (uint32_t*)nullptr, (int)R);
+  return bytes;
+}
+
+BinningState carve_binning(void* base, int64_t R) {
+  Carver c{static_cast<char*>(base)};
+  BinningState b;
+  b.keys_unsorted = c.take<uint64_t>(R);
+  b.keys = c.take<uint64_t>(R);
+  b.vals_unsorted = c.take<uint32_t>(R);
+  b.vals = c.take<uint32_t>(R);
+  b.sort_bytes = sort_temp_bytes(R);
+  b.sort_tmp = c.take<char>(b.sort_bytes);
+  return b;
+}
+size_t binning_bytes(int64_t R) {
+  Carver c{nullptr};
+  c.take<uint64_t>(R); c.take<uint64_t>(R); c.take<uint32_t>(R); c.take<uint32_t>(R);
+  c.take<char>(sort_temp_bytes(R));
+  return c.off;
+}
+
+struct ImageState {
+  uint2* ranges;       // [tiles]
+  uint32_t* n_contrib; // [H*W]
+  float* final_T;      // [H*W]
+};
+ImageState carve_image(void* base, int H, int W) {
+  Carver c{static_cast<char*>(base)};
+  int tiles = ((W + BX - 1) / BX) * ((H + BY - 1) / BY);
+  ImageState s;
+  s.ranges = c.take<uint2>(tiles);
+  s.n_contrib = c.take<uint32_t>((size_t)H * W);
+  s.final_T = c.take<float>((size_t)H * W);
+  return s;
+}
+size_t image_bytes(int H, int W) {
+  Carver c{nullptr};
+  int tiles = ((W + BX - 1) / BX) * ((H + BY - 1) / BY);
+  c.take<uint2>(tiles); c.take<uint32_t>((size_t)H * W); c.take<float>((size_t)H * W);
+  return c.off;
+}
+
+int tile_bits(int tiles) {
+  int b = 0;
+  while ((1u << b) <= (unsigned)tiles) ++b;
+  return b;
+}
+
+// Bijective XCD-aware tile order: consecutive workgroup ids round-robin over
+// the 8 XCDs; give each XCD a contiguous run of tiles (guide §5, T1).
+__device__ __forceinline__ int xcd_tile(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, k = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+// ------------------------------------------------------------ preprocess --
+struct Cam {
+  int W, H;
+  float tanfx, tanfy, fx, fy, scale_mod;
+  int D, M;
+  int gx, gy;
+  bool prefiltered;
+};
+
+__global__ void __launch_bounds__(kThreads)
+k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
+             const float* __restrict__ scales, const float* __restrict__ rots,
+             const float* __restrict__ cov_pre, const float* __restrict__ shs,
+             const float* __restrict__ colors_pre, const float* __restrict__ opac,
+             const float* __restrict__ vm, const float* __restrict__ pm,
+             const float* __restrict__ campos, int32_t* __restrict__ radii, GeomState g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  radii[i] = 0;
+  g.tiles[i] = 0;
+  const float mx = means[i * 3 + 0], my = means[i * 3 + 1], mz = means[i * 3 + 2];
+  float pv[3];
+  xform43(vm, mx, my, mz, pv);
+  if (pv[2] <= 0.2f) return;  // in_frustum near-plane cull
+  float ph[4];
+  xform44(pm, mx, my, mz, ph);
+  const float pw = 1.0f / (ph[3] + 0.0000001f);
+  const float ppx = ph[0] * pw, ppy = ph[1] * pw;
+
+  float cov3[6];
+  if (cov_pre) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) cov3[k] = cov_pre[i * 6 + k];
+  } else {
+    cov3d_from_scale_rot(scales + i * 3, cam.scale_mod, rots + i * 4, cov3);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) g.cov3D[i * 6 + k] = cov3[k];
+  }
+  Ewa e = ewa_project(mx, my, mz, cov3, vm, cam.fx, cam.fy, cam.tanfx, cam.tanfy);
+  const float a = e.a + 0.3f, b = e.b, c = e.c + 0.3f;
+  const float det = a * c - b * b;
+  if (det == 0.0f) return;
+  const float det_inv = 1.0f / det;
+  const float mid = 0.5f * (a + c);
+  const float disc = sqrtf(fmaxf(0.1f, mid * mid - det));
+  const float l1 = mid + disc, l2 = mid - disc;
+  const int r = (int)ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
+  const float px = ndc2pix(ppx, cam.W), py = ndc2pix(ppy, cam.H);
+  int x0, y0, x1, y1;
+  get_rect(px, py, r, cam.gx, cam.gy, &x0, &y0, &x1, &y1);
+  if ((x1 - x0) * (y1 - y0) == 0) return;
+
+  float rgb[3];
+  if (colors_pre) {
+    rgb[0] = colors_pre[i * 3 + 0]; rgb[1] = colors_pre[i * 3 + 1]; rgb[2] = colors_pre[i * 3 + 2];
+  } else {
+    float dx = mx - campos[0], dy = my - campos[1], dz = mz - campos[2];
+    float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    dx = dx / len; dy = dy / len; dz = dz / len;
+    float B[16];
+    sh_basis(cam.D, dx, dy, dz, B);
+    const int nb = (cam.D + 1) * (cam.D + 1);
+    const float* sh = shs + i * (int64_t)cam.M * 3;
+    for (int ch = 0; ch < 3; ++ch) {
+      float acc = B[0] * sh[ch];
+      for (int k = 1; k < nb; ++k) acc = acc + B[k] * sh[k * 3 + ch];
+      acc = acc + 0.5f;
+      g.clamped[i * 3 + ch] = acc < 0.0f;
+      rgb[ch] = fmaxf(acc, 0.0f);
+    }
+  }
+  g.rgb[i * 3 + 0] = rgb[0]; g.rgb[i * 3 + 1] = rgb[1]; g.rgb[i * 3 + 2] = rgb[2];
+  g.depth[i] = pv[2];
+  radii[i] = r;
+  g.rec0[i] = make_float4(px, py, c * det_inv, -b * det_inv);
+  g.rec1[i] = make_float4(a * det_inv, opac[i], 0.0f, 0.0f);
+  g.tiles[i] = (uint32_t)((y1 - y0) * (x1 - x0));
+}
+
+// ------------------------------------------------------------- binning ----
+__global__ void __launch_bounds__(kThreads)
+k_duplicate(int64_t P, int gx, int gy, const int32_t* __restrict__ radii, GeomState g,
+            uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P || radii[i] <= 0) return;
+  uint32_t off = i == 0 ? 0u : g.offsets[i - 1];
+  const float4 r0 = g.rec0[i];
+  int x0, y0, x1, y1;
+  get_rect(r0.x, r0.y, radii[i], gx, gy, &x0, &y0, &x1, &y1);
+  const uint64_t dbits = (uint64_t)__float_as_uint(g.depth[i]);
+  for (int y = y0; y < y1; ++y)
+    for (int x = x0; x < x1; ++x) {
+      keys[off] = ((uint64_t)(y * gx + x) << 32) | dbits;
+      vals[off] = (uint32_t)i;
+      ++off;
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_ranges(int64_t R, const uint64_t* __restrict__ keys, uint2* __restrict__ ranges) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R) return;
+  const uint32_t cur = (uint32_t)(keys[i] >> 32);
+  if (i == 0) {
+    ranges[cur].x = 0;
+  } else {
+    const uint32_t prev = (uint32_t)(keys[i - 1] >> 32);
+    if (cur != prev) {
+      ranges[prev].y = (uint32_t)i;
+      ranges[cur].x = (uint32_t)i;
+    }
+  }
+  if (i == R - 1) ranges[cur].y = (uint32_t)R;
+}
+
+// --------------------------------------------------------------- blend ----
+__global__ void __launch_bounds__(BS)
+k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
+        const uint32_t* __restrict__ point_list, GeomState g, const float* __restrict__ bg,
+        float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+        float* __restrict__ out) {
+  __shared__ float4 s_r0[BS];
+  __shared__ float4 s_r1[BS];  // (conic.c, opacity, r, g)
+  __shared__ float s_b[BS];
+  const int tile = xcd_tile(blockIdx.x, ntiles);
+  const int tx = tile % gx, ty = tile / gx;
+  const int lx = threadIdx.x % BX, ly = threadIdx.x / BX;
+  const int px = tx * BX + lx, py = ty * BY + ly;
+  const bool inside = px < W && py < H;
+  const float pxf = (float)px, pyf = (float)py;
+  const uint2 range = ranges[tile];
+  const int todo_total = (int)(range.y - range.x);
+  const int rounds = (todo_total + BS - 1) / BS;
+  bool done = !inside;
+  float T = 1.0f;
+  uint32_t contributor = 0, last_contributor = 0;
+  float C0 = 0.f, C1 = 0.f, C2 = 0.f;
+  int todo = todo_total;
+  for (int rd = 0; rd < rounds; ++rd, todo -= BS) {
+    if (__syncthreads_count(done) == BS) break;
+    const int prog = rd * BS + threadIdx.x;
+    if ((int64_t)range.x + prog < range.y) {
+      const uint32_t id = point_list[range.x + prog];
+      const float4 r1 = g.rec1[id];
+      s_r0[threadIdx.x] = g.rec0[id];
+      s_r1[threadIdx.x] = make_float4(r1.x, r1.y, g.rgb[id * 3 + 0], g.rgb[id * 3 + 1]);
+      s_b[threadIdx.x] = g.rgb[id * 3 + 2];
+    }
+    __syncthreads();
+    const int n = todo < BS ? todo : BS;
+    for (int j = 0; !done && j < n; ++j) {
+      ++contributor;
+      const float4 a = s_r0[j];
+      const float4 b = s_r1[j];
+      const float dx = a.x - pxf, dy = a.y - pyf;
+      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      if (power > 0.0f) continue;
+      const float alpha = fminf(0.99f, b.y * fexp(power));
+      if (alpha < 1.0f / 255.0f) continue;
+      const float test_T = T * (1.0f - alpha);
+      if (test_T < 0.0001f) {
+        done = true;
+        continue;
+      }
+      // C += feature * alpha * T, evaluated left to right as the reference
+      C0 = C0 + b.z * alpha * T;
+      C1 = C1 + b.w * alpha * T;
+      C2 = C2 + s_b[j] * alpha * T;
+      T = test_T;
+      last_contributor = contributor;
+    }
+  }
+  if (inside) {
+    const int pid = py * W + px;
+    final_T[pid] = T;
+    n_contrib[pid] = last_contributor;
+    out[pid] = C0 + T * bg[0];
+    out[H * W + pid] = C1 + T * bg[1];
+    out[2 * H * W + pid] = C2 + T * bg[2];
+  }
+}
+
+// ----------------------------------------------------------- backward -----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(BS)
+k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
+                 const uint32_t* __restrict__ point_list, GeomState g,
+                 const float* __restrict__ bg, const float* __restrict__ final_Ts,
+                 const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
+                 float* __restrict__ dL_dmean2D, float* __restrict__ dL_dconic,
+                 float* __restrict__ dL_dopacity, float* __restrict__ dL_dcolors) {
+  __shared__ float4 s_r0[BS];
+  __shared__ float4 s_r1[BS];
+  __shared__ float s_b[BS];
+  __shared__ uint32_t s_id[BS];
+  const int tile = xcd_tile(blockIdx.x, ntiles);
+  const int tx = tile % gx, ty = tile / gx;
+  const int lx = threadIdx.x % BX, ly = threadIdx.x / BX;
+  const int px = tx * BX + lx, py = ty * BY + ly;
+  const bool inside = px < W && py < H;
+  const int pid = py * W + px;
+  const float pxf = (float)px, pyf = (float)py;
+  const uint2 range = ranges[tile];
+  const int todo_total = (int)(range.y - range.x);
+  const int rounds = (todo_total + BS - 1) / BS;
+  const float T_final = inside ? final_Ts[pid] : 0.0f;
+  float T = T_final;
+  uint32_t contributor = (uint32_t)todo_total;
+  const uint32_t last_contributor = inside ? n_contrib[pid] : 0;
+  float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
+  if (inside) {
+    dpix0 = dL_dpix[pid];
+    dpix1 = dL_dpix[H * W + pid];
+    dpix2 = dL_dpix[2 * H * W + pid];
+  }
+  const float bg_dot = bg[0] * dpix0 + bg[1] * dpix1 + bg[2] * dpix2;
+  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
+  float last_alpha = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;
+  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+  const int lane = threadIdx.x & 63;
+  int todo = todo_total;
+  for (int rd = 0; rd < rounds; ++rd, todo -= BS) {
+    __syncthreads();
+    const int prog = rd * BS + threadIdx.x;
+    if (prog < todo_total) {
+      const uint32_t id = point_list[range.y - prog - 1];
+      const float4 r1 = g.rec1[id];
+      s_id[threadIdx.x] = id;
+      s_r0[threadIdx.x] = g.rec0[id];
+      s_r1[threadIdx.x] = make_float4(r1.x, r1.y, g.rgb[id * 3 + 0], g.rgb[id * 3 + 1]);
+      s_b[threadIdx.x] = g.rgb[id * 3 + 2];
+    }
+    __syncthreads();
+    const int n = todo < BS ? todo : BS;
+    for (int j = 0; j < n; ++j) {
+      --contributor;
+      bool ok = inside && contributor < last_contributor;
+      const float4 a = s_r0[j];
+      const float4 b = s_r1[j];
+      const float dx = a.x - pxf, dy = a.y - pyf;
+      const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+      ok = ok && !(power > 0.0f);
+      const float G = fexp(power);
+      const float alpha = fminf(0.99f, b.y * G);
+      ok = ok && !(alpha < 1.0f / 255.0f);
+      if (!__any(ok)) continue;
+      float gm_x = 0.f, gm_y = 0.f, gc_x = 0.f, gc_y = 0.f, gc_w = 0.f, go = 0.f;
+      float gr = 0.f, gg = 0.f, gb = 0.f;
+      if (ok) {
+        T = T / (1.0f - alpha);
+        const float dchannel_dcolor = alpha * T;
+        const float c0 = b.z, c1 = b.w, c2 = s_b[j];
+        acc0 = last_alpha * lc0 + (1.0f - last_alpha) * acc0;
+        acc1 = last_alpha * lc1 + (1.0f - last_alpha) * acc1;
+        acc2 = last_alpha * lc2 + (1.0f - last_alpha) * acc2;
+        lc0 = c0; lc1 = c1; lc2 = c2;
+        float dL_dalpha = (c0 - acc0) * dpix0 + (c1 - acc1) * dpix1 + (c2 - acc2) * dpix2;
+        gr = dchannel_dcolor * dpix0;
+        gg = dchannel_dcolor * dpix1;
+        gb = dchannel_dcolor * dpix2;
+        dL_dalpha = dL_dalpha * T;
+        last_alpha = alpha;
+        dL_dalpha = dL_dalpha + (-T_final / (1.0f - alpha)) * bg_dot;
+        const float dL_dG = b.y * dL_dalpha;
+        const float gdx = G * dx, gdy = G * dy;
+        const float dG_ddelx = -gdx * a.z - gdy * a.w;
+        const float dG_ddely = -gdy * b.x - gdx * a.w;
+        gm_x = dL_dG * dG_ddelx * ddelx_dx;
+        gm_y = dL_dG * dG_ddely * ddely_dy;
+        gc_x = -0.5f * gdx * dx * dL_dG;
+        gc_y = -0.5f * gdx * dy * dL_dG;
+        gc_w = -0.5f * gdy * dy * dL_dG;
+        go = G * dL_dalpha;
+      }
+      gm_x = wave_sum(gm_x); gm_y = wave_sum(gm_y);
+      gc_x = wave_sum(gc_x); gc_y = wave_sum(gc_y); gc_w = wave_sum(gc_w);
+      go = wave_sum(go);
+      gr = wave_sum(gr); gg = wave_sum(gg); gb = wave_sum(gb);
+      if (lane == 0) {
+        const uint32_t id = s_id[j];
+        atomicAdd(&dL_dmean2D[id * 3 + 0], gm_x);
+        atomicAdd(&dL_dmean2D[id * 3 + 1], gm_y);
+        atomicAdd(&dL_dconic[id * 4 + 0], gc_x);
+        atomicAdd(&dL_dconic[id * 4 + 1], gc_y);
+        atomicAdd(&dL_dconic[id * 4 + 3], gc_w);
+        atomicAdd(&dL_dopacity[id], go);
+        atomicAdd(&dL_dcolors[id * 3 + 0], gr);
+        atomicAdd(&dL_dcolors[id * 3 + 1], gg);
+        atomicAdd(&dL_dcolors[id * 3 + 2], gb);
+      }
+    }
+  }
+}
+
+// Per-Gaussian chain rule: conic -> 2-D cov -> (3-D cov, view mean) and
+// screen mean -> world mean; SH colour -> coefficients / view direction;
+// 3-D cov -> scale / rotation.
+__global__ void __launch_bounds__(kThreads)
+k_preprocess_backward(int64_t P, Cam cam, const float* __restrict__ means,
+                      const float* __restrict__ scales, const float* __restrict__ rots,
+                      const float* __restrict__ cov_pre, const float* __restrict__ shs,
+                      const int32_t* __restrict__ radii, GeomState g,
+                      const float* __restrict__ vm, const float* __restrict__ pm,
+                      const float* __restrict__ campos, const float* __restrict__ dL_dmean2D,
+                      const float* __restrict__ dL_dconic, const float* __restrict__ dL_dcolor,
+                      float* __restrict__ dL_dmeans, float* __restrict__ dL_dcov,
+                      float* __restrict__ dL_dsh, float* __restrict__ dL_dscale,
+                      float* __restrict__ dL_drot) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P || !(radii[i] > 0)) return;
+  const float mx = means[i * 3 + 0], my = means[i * 3 + 1], mz = means[i * 3 + 2];
+  const float* cov3 = cov_pre ? cov_pre + i * 6 : g.cov3D + i * 6;
+  Ewa e = ewa_project(mx, my, mz, cov3, vm, cam.fx, cam.fy, cam.tanfx, cam.tanfy);
+  const float a = e.a + 0.3f, b = e.b, c = e.c + 0.3f;
+  const float dcx = dL_dconic[i * 4 + 0], dcy = dL_dconic[i * 4 + 1], dcz = dL_dconic[i * 4 + 3];
+  const float denom = a * c - b * b;
+  const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+  float da = 0.f, db = 0.f, dc = 0.f;
+  float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float* T = e.T;  // T[0..2] row 0, T[3..5] row 1
+  if (denom2inv != 0.0f) {
+    da = denom2inv * (-c * c * dcx + 2.0f * b * c * dcy + (denom - a * c) * dcz);
+    dc = denom2inv * (-a * a * dcz + 2.0f * a * b * dcy + (denom - a * c) * dcx);
+    db = denom2inv * 2.0f * (b * c * dcx - (denom + 2.0f * b * b) * dcy + a * b * dcz);
+    dcov[0] = T[0] * T[0] * da + T[0] * T[3] * db + T[3] * T[3] * dc;
+    dcov[3] = T[1] * T[1] * da + T[1] * T[4] * db + T[4] * T[4] * dc;
+    dcov[5] = T[2] * T[2] * da + T[2] * T[5] * db + T[5] * T[5] * dc;
+    dcov[1] = 2.0f * T[0] * T[1] * da + (T[0] * T[4] + T[1] * T[3]) * db + 2.0f * T[3] * T[4] * dc;
+    dcov[2] = 2.0f * T[0] * T[2] * da + (T[0] * T[5] + T[2] * T[3]) * db + 2.0f * T[3] * T[5] * dc;
+    dcov[4] = 2.0f * T[2] * T[1] * da + (T[1] * T[5] + T[2] * T[4]) * db + 2.0f * T[4] * T[5] * dc;
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dL_dcov[i * 6 + k] = dcov[k];
+  const float V[9] = {cov3[0], cov3[1], cov3[2], cov3[1], cov3[3], cov3[4],
+                      cov3[2], cov3[4], cov3[5]};
+  float dT0[3], dT1[3];
+  for (int k = 0; k < 3; ++k) {
+    const float t0v = T[0] * V[k] + T[1] * V[3 + k] + T[2] * V[6 + k];
+    const float t1v = T[3] * V[k] + T[4] * V[3 + k] + T[5] * V[6 + k];
+    dT0[k] = 2.0f * t0v * da + t1v * db;
+    dT1[k] = 2.0f * t1v * dc + t0v * db;
+  }
+  // T = J Wv, Wv[r][c] = vm[r + 4c]
+  const float dJ00 = vm[0] * dT0[0] + vm[4] * dT0[1] + vm[8] * dT0[2];
+  const float dJ02 = vm[2] * dT0[0] + vm[6] * dT0[1] + vm[10] * dT0[2];
+  const float dJ11 = vm[1] * dT1[0] + vm[5] * dT1[1] + vm[9] * dT1[2];
+  const float dJ12 = vm[2] * dT1[0] + vm[6] * dT1[1] + vm[10] * dT1[2];
+  const float tz = 1.0f / e.tz, tz2 = tz * tz, tz3 = tz2 * tz;
+  const float dtx = e.xmul * -cam.fx * tz2 * dJ02;
+  const float dty = e.ymul * -cam.fy * tz2 * dJ12;
+  const float dtz = -cam.fx * tz2 * dJ00 - cam.fy * tz2 * dJ11 +
+                    (2.0f * cam.fx * e.tx) * tz3 * dJ02 + (2.0f * cam.fy * e.ty) * tz3 * dJ12;
+  float gmx = vm[0] * dtx + vm[1] * dty + vm[2] * dtz;
+  float gmy = vm[4] * dtx + vm[5] * dty + vm[6] * dtz;
+  float gmz = vm[8] * dtx + vm[9] * dty + vm[10] * dtz;
+
+  // screen-space mean -> world mean
+  float ph[4];
+  xform44(pm, mx, my, mz, ph);
+  const float mw = 1.0f / (ph[3] + 0.0000001f);
+  const float mul1 = (pm[0] * mx + pm[4] * my + pm[8] * mz + pm[12]) * mw * mw;
+  const float mul2 = (pm[1] * mx + pm[5] * my + pm[9] * mz + pm[13]) * mw * mw;
+  const float d2x = dL_dmean2D[i * 3 + 0], d2y = dL_dmean2D[i * 3 + 1];
+  gmx = gmx + ((pm[0] * mw - pm[3] * mul1) * d2x + (pm[1] * mw - pm[3] * mul2) * d2y);
+  gmy = gmy + ((pm[4] * mw - pm[7] * mul1) * d2x + (pm[5] * mw - pm[7] * mul2) * d2y);
+  gmz = gmz + ((pm[8] * mw - pm[11] * mul1) * d2x + (pm[9] * mw - pm[11] * mul2) * d2y);
+
+  if (shs) {
+    const float ox = mx - campos[0], oy = my - campos[1], oz = mz - campos[2];
+    const float len = sqrtf(ox * ox + oy * oy + oz * oz);
+    const float x = ox / len, y = oy / len, z = oz / len;
+    float B[16], dX[16], dY[16], dZ[16];
+    sh_basis(cam.D, x, y, z, B);
+    sh_basis_grad(cam.D, x, y, z, dX, dY, dZ);
+    const int nb = (cam.D + 1) * (cam.D + 1);
+    const float* sh = shs + i * (int64_t)cam.M * 3;
+    float* dsh = dL_dsh + i * (int64_t)cam.M * 3;
+    float drgb[3];
+    for (int ch = 0; ch < 3; ++ch)
+      drgb[ch] = g.clamped[i * 3 + ch] ? 0.0f : dL_dcolor[i * 3 + ch];
+    for (int k = 0; k < cam.M; ++k)
+      for (int ch = 0; ch < 3; ++ch) dsh[k * 3 + ch] = k < nb ? B[k] * drgb[ch] : 0.0f;
+    float ddx = 0.f, ddy = 0.f, ddz = 0.f;
+    for (int k = 1; k < nb; ++k)
+      for (int ch = 0; ch < 3; ++ch) {
+        const float s = sh[k * 3 + ch] * drgb[ch];
+        ddx = ddx + dX[k] * s;
+        ddy = ddy + dY[k] * s;
+        ddz = ddz + dZ[k] * s;
+      }
+    // d normalize(o) / d o applied to (ddx, ddy, ddz)
+    const float s2 = ox * ox + oy * oy + oz * oz;
+    const float inv32 = 1.0f / sqrtf(s2 * s2 * s2);
+    gmx = gmx + ((s2 - ox * ox) * ddx - oy * ox * ddy - oz * ox * ddz) * inv32;
+    gmy = gmy + (-ox * oy * ddx + (s2 - oy * oy) * ddy - oz * oy * ddz) * inv32;
+    gmz = gmz + (-ox * oz * ddx - oy * oz * ddy + (s2 - oz * oz) * ddz) * inv32;
+  }
+  dL_dmeans[i * 3 + 0] = gmx;
+  dL_dmeans[i * 3 + 1] = gmy;
+  dL_dmeans[i * 3 + 2] = gmz;
+
+  if (scales && dL_dscale) {
+    // Sigma = M M^T, M = R diag(s): dL/dM = (G + G^T) M with G = dL/dSigma
+    const float* q = rots + i * 4;
+    const float r = q[0], x = q[1], y = q[2], z = q[3];
+    const float R[9] = {1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                        2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                        2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y)};
+    const float s[3] = {cam.scale_mod * scales[i * 3 + 0], cam.scale_mod * scales[i * 3 + 1],
+                        cam.scale_mod * scales[i * 3 + 2]};
+    const float* dc6 = dcov;
+    // symmetric gradient matrix: off-diagonal entries shared by (i,j),(j,i)
+    const float Gs[9] = {dc6[0], 0.5f * dc6[1], 0.5f * dc6[2], 0.5f * dc6[1], dc6[3],
+                         0.5f * dc6[4], 0.5f * dc6[2], 0.5f * dc6[4], dc6[5]};
+    float dM[9];
+    for (int ii = 0; ii < 3; ++ii)
+      for (int jj = 0; jj < 3; ++jj) {
+        float acc = 0.f;
+        for (int k = 0; k < 3; ++k) acc = acc + 2.0f * Gs[3 * ii + k] * R[3 * k + jj] * s[jj];
+        dM[3 * ii + jj] = acc;
+      }
+    for (int jj = 0; jj < 3; ++jj)
+      dL_dscale[i * 3 + jj] =
+          cam.scale_mod * (dM[jj] * R[jj] + dM[3 + jj] * R[3 + jj] + dM[6 + jj] * R[6 + jj]);
+    float dR[9];
+    for (int k = 0; k < 9; ++k) dR[k] = dM[k] * s[k % 3];
+    // dR/dq for the (unnormalised) quaternion formula above
+    dL_drot[i * 4 + 0] = 2.f * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
+    dL_drot[i * 4 + 1] = 2.f * (y * dR[1] + z * dR[2] + y * dR[3] - 2.f * x * dR[4] - r * dR[5] +
+                                z * dR[6] + r * dR[7] - 2.f * x * dR[8]);
+    dL_drot[i * 4 + 2] = 2.f * (-2.f * y * dR[0] + x * dR[1] + r * dR[2] + x * dR[3] + z * dR[5] -
+                                r * dR[6] + z * dR[7] - 2.f * y * dR[8]);
+    dL_drot[i * 4 + 3] = 2.f * (-2.f * z * dR[0] - r * dR[1] + x * dR[2] + r * dR[3] -
+                                2.f * z * dR[4] + y * dR[5] + x * dR[6] + y * dR[7]);
+  }
+}
+
+__global__ void k_mark_visible(int64_t P, const float* __restrict__ means,
+                               const float* __restrict__ vm, uint8_t* __restrict__ present) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  float pv[3];
+  xform43(vm, means[i * 3 + 0], means[i * 3 + 1], means[i * 3 + 2], pv);
+  present[i] = pv[2] > 0.2f;
+}
+
+// ------------------------------------------------------------- timing -----
+struct Timing {
+  bool enabled = false;
+  hipEvent_t ev[7] = {};
+  bool created = false;
+  bool valid = false;
+};
+thread_local Timing g_timing;
+
+void tmark(int k, hipStream_t s) {
+  if (!g_timing.enabled) return;
+  if (!g_timing.created) {
+    for (auto& e : g_timing.ev) (void)hipEventCreate(&e);
+    g_timing.created = true;
+  }
+  (void)hipEventRecord(g_timing.ev[k], s);
+  if (k == 6) g_timing.valid = true;
+}
+
+Cam make_cam(const gsr_settings* s, int M) {
+  Cam c;
+  c.W = s->image_width;
+  c.H = s->image_height;
+  c.tanfx = s->tanfovx;
+  c.tanfy = s->tanfovy;
+  c.fx = c.W / (2.0f * s->tanfovx);
+  c.fy = c.H / (2.0f * s->tanfovy);
+  c.scale_mod = s->scale_modifier;
+  c.D = s->sh_degree;
+  c.M = M;
+  c.gx = (c.W + BX - 1) / BX;
+  c.gy = (c.H + BY - 1) / BY;
+  c.prefiltered = s->prefiltered != 0;
+  return c;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gsr_geom_bytes(int64_t P) { return geom_bytes(P > 0 ? P : 1); }
+size_t gsr_image_bytes(int height, int width) { return image_bytes(height, width); }
+size_t gsr_binning_bytes(int64_t R) { return binning_bytes(R > 0 ? R : 1); }
+
+void gsr_set_timing(int enabled) { g_timing.enabled = enabled != 0; }
+
+int gsr_last_timing(float* phases_ms, int n) {
+  if (!g_timing.valid) return S3_ERR_INVALID;
+  S3_HIP(hipEventSynchronize(g_timing.ev[6]));
+  // (preprocess, scan, duplicate+sort, ranges, blend); event 2 -> 3 spans the
+  // host read-back of num_rendered and is not a device phase.
+  const int from[5] = {0, 1, 3, 4, 5};
+  for (int k = 0; k < n && k < 5; ++k) {
+    float ms = 0.f;
+    S3_HIP(hipEventElapsedTime(&ms, g_timing.ev[from[k]], g_timing.ev[from[k] + 1]));
+    phases_ms[k] = ms;
+  }
+  return S3_OK;
+}
+
+int gsr_preprocess(const gsr_settings* s, int64_t P, int M, const float* means3D,
+                   const float* scales, const float* rotations, const float* cov3D_precomp,
+                   const float* shs, const float* colors_precomp, const float* opacities,
+                   int32_t* radii, void* geom, int64_t* num_rendered, void* stream) {
+  S3_REQUIRE(s && num_rendered && P >= 0, "gsr_preprocess: bad arguments");
+  S3_REQUIRE(P < (int64_t)1 << 31, "gsr_preprocess: P too large");
+  S3_REQUIRE((shs == nullptr) != (colors_precomp == nullptr),
+             "Please provide excatly one of either SHs or precomputed colors!");
+  S3_REQUIRE((cov3D_precomp == nullptr) != (scales == nullptr || rotations == nullptr),
+             "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+  S3_REQUIRE(s->sh_degree >= 0 && s->sh_degree <= 3, "gsr_preprocess: sh_degree must be 0..3");
+  S3_REQUIRE(shs == nullptr || M >= (s->sh_degree + 1) * (s->sh_degree + 1),
+             "gsr_preprocess: M=%d too small for sh_degree %d", M, s->sh_degree);
+  *num_rendered = 0;
+  if (P == 0) return S3_OK;
+  hipStream_t st = s3::as_stream(stream);
+  Cam cam = make_cam(s, M);
+  GeomState g = carve_geom(geom, P);
+  tmark(0, st);
+  k_preprocess<<<(unsigned)s3::cdiv(P, kThreads), kThreads, 0, st>>>(
+      P, cam, means3D, scales, rotations, cov3D_precomp, shs, colors_precomp, opacities,
+      s->viewmatrix, s->projmatrix, s->campos, radii, g);
+  S3_LAUNCH_CHECK();
+  tmark(1, st);
+  size_t tb = g.scan_bytes;
+  S3_HIP(hipcub::DeviceScan::InclusiveSum(g.scan_tmp, tb, g.tiles, g.offsets, (int)P, st));
+  tmark(2, st);
+  uint32_t last = 0;
+  S3_HIP(hipMemcpyAsync(&last, g.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  S3_HIP(hipStreamSynchronize(st));
+  *num_rendered = last;
+  return S3_OK;
+}
+
+int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii,
+               void* geom, void* binning, void* image, float* out_color, void* stream) {
+  S3_REQUIRE(s && P >= 0 && R >= 0, "gsr_render: bad arguments");
+  S3_REQUIRE(R < ((int64_t)1 << 32), "gsr_render: too many tile instances");
+  hipStream_t st = s3::as_stream(stream);
+  const int W = s->image_width, H = s->image_height;
+  const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY, ntiles = gx * gy;
+  if (P == 0) {
+    S3_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)H * W, st));
+    return S3_OK;
+  }
+  GeomState g = carve_geom(geom, P);
+  BinningState b = carve_binning(binning, R);
+  ImageState im = carve_image(image, H, W);
+  tmark(3, st);
+  S3_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * ntiles, st));
+  if (R > 0) {
+    k_duplicate<<<(unsigned)s3::cdiv(P, kThreads), kThreads, 0, st>>>(
+        P, gx, gy, radii, g, b.keys_unsorted, b.vals_unsorted);
+    S3_LAUNCH_CHECK();
+    size_t tb = b.sort_bytes;
+    S3_HIP(hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, tb, b.keys_unsorted, b.keys,
+                                              b.vals_unsorted, b.vals, (int)R, 0,
+                                              32 + tile_bits(ntiles), st));
+  }
+  tmark(4, st);
+  if (R > 0) {
+    k_ranges<<<(unsigned)s3::cdiv(R, kThreads), kThreads, 0, st>>>(R, b.keys, im.ranges);
+    S3_LAUNCH_CHECK();
+  }
+  tmark(5, st);
+  k_blend<<<ntiles, BS, 0, st>>>(W, H, gx, ntiles, im.ranges, b.vals, g, s->bg, im.final_T,
+                                 im.n_contrib, out_color);
+  S3_LAUNCH_CHECK();
+  tmark(6, st);
+  return S3_OK;
+}
+
+int gsr_backward(const gsr_settings* s, int64_t P, int M, int64_t R, const float* means3D,
+                 const float* scales, const float* rotations, const float* cov3D_precomp,
+                 const float* shs, const float* colors_precomp, const float* opacities,
+                 const int32_t* radii, const void* geom, const void* binning,
+                 const void* image, const float* dL_dout, float* dL_dmeans2D,
+                 float* dL_dconic, float* dL_dopacity, float* dL_dcolors, float* dL_dmeans3D,
+                 float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                 void* stream) {
+  S3_REQUIRE(s && P >= 0 && R >= 0, "gsr_backward: bad arguments");
+  (void)colors_precomp;
+  (void)opacities;
+  hipStream_t st = s3::as_stream(stream);
+  auto zero = [&](float* p, size_t n) -> hipError_t {
+    return p ? hipMemsetAsync(p, 0, n * sizeof(float), st) : hipSuccess;
+  };
+  S3_HIP(zero(dL_dmeans2D, P * 3));
+  S3_HIP(zero(dL_dconic, P * 4));
+  S3_HIP(zero(dL_dopacity, P));
+  S3_HIP(zero(dL_dcolors, P * 3));
+  S3_HIP(zero(dL_dmeans3D, P * 3));
+  S3_HIP(zero(dL_dcov3D, P * 6));
+  if (shs) S3_HIP(zero(dL_dsh, P * (size_t)M * 3));
+  if (scales) {
+    S3_HIP(zero(dL_dscales, P * 3));
+    S3_HIP(zero(dL_drotations, P * 4));
+  }
+  if (P == 0) return S3_OK;
+  const int W = s->image_width, H = s->image_height;
+  const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY, ntiles = gx * gy;
+  GeomState g = carve_geom(const_cast<void*>(geom), P);
+  BinningState b = carve_binning(const_cast<void*>(binning), R);
+  ImageState im = carve_image(const_cast<void*>(image), H, W);
+  k_blend_backward<<<ntiles, BS, 0, st>>>(W, H, gx, ntiles, im.ranges, b.vals, g, s->bg,
+                                          im.final_T, im.n_contrib, dL_dout, dL_dmeans2D,
+                                          dL_dconic, dL_dopacity, dL_dcolors);
+  S3_LAUNCH_CHECK();
+  Cam cam = make_cam(s, M);
+  k_preprocess_backward<<<(unsigned)s3::cdiv(P, kThreads), kThreads, 0, st>>>(
+      P, cam, means3D, scales, rotations, cov3D_precomp, shs, radii, g, s->viewmatrix,
+      s->projmatrix, s->campos, dL_dmeans2D, dL_dconic, dL_dcolors, dL_dmeans3D, dL_dcov3D,
+      dL_dsh, dL_dscales, dL_drotations);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+int gsr_mark_visible(int64_t P, const float* means3D, const float* viewmatrix,
+                     const float* projmatrix, uint8_t* present, void* stream) {
+  (void)projmatrix;
+  S3_REQUIRE(P >= 0, "gsr_mark_visible: P < 0");
+  if (P == 0) return S3_OK;
+  k_mark_visible<<<(unsigned)s3::cdiv(P, kThreads), kThreads, 0, s3::as_stream(stream)>>>(
+      P, means3D, viewmatrix, present);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,179 @@
+// Per-Gaussian math of the tile rasterizer, shared by the forward and the
+// backward kernels (raster.hip).  Canonical graphdeco 3DGS formulas written
+// in explicit row-major form; compiled with -ffp-contract=off and with a
+// fixed-sequence exponential so the forward is reproducible operation by
+// operation by the CPU oracle (oracle/raster_ref.c).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#define GSR_HD __host__ __device__ __forceinline__
+
+namespace gsr {
+
+constexpr int BX = 16, BY = 16, BS = BX * BY;  // 16x16 pixel tiles, 256 threads
+
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+constexpr float SH_C2_0 = 1.0925484305920792f, SH_C2_1 = -1.0925484305920792f,
+                SH_C2_2 = 0.31539156525252005f, SH_C2_3 = -1.0925484305920792f,
+                SH_C2_4 = 0.5462742152960396f;
+constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f,
+                SH_C3_2 = -0.4570457994644658f, SH_C3_3 = 0.3731763325901154f,
+                SH_C3_4 = -0.4570457994644658f, SH_C3_5 = 1.445305721320277f,
+                SH_C3_6 = -0.5900435899266435f;
+
+// exp(x) by Cody-Waite reduction + degree-6 Taylor/Horner, <= 2 ulp on the
+// blend's domain (x <= 0).  A fixed operation sequence (no libm / ocml) so
+// the GPU forward and the CPU oracle agree bit for bit.
+GSR_HD float fexp(float x) {
+  if (x < -87.0f) return 0.0f;
+  float k = rintf(x * 1.44269504088896341f);
+  float r = x - k * 0.693145751953125f;
+  r = r - k * 1.42860682030941723e-06f;
+  float p = 0.00138888888888889f;
+  p = p * r + 0.00833333333333333f;
+  p = p * r + 0.0416666666666667f;
+  p = p * r + 0.166666666666667f;
+  p = p * r + 0.5f;
+  p = p * r + 1.0f;
+  p = p * r + 1.0f;
+  return ldexpf(p, (int)k);
+}
+
+GSR_HD float ndc2pix(float v, int S) { return ((v + 1.0f) * S - 1.0f) * 0.5f; }
+
+// Tile rectangle of a splat (reference getRect, int radius).
+GSR_HD void get_rect(float px, float py, int r, int gx, int gy, int* xmin, int* ymin,
+                     int* xmax, int* ymax) {
+  int a = (int)((px - r) / BX), b = (int)((py - r) / BY);
+  int c = (int)((px + r + BX - 1) / BX), d = (int)((py + r + BY - 1) / BY);
+  *xmin = a < 0 ? 0 : (a > gx ? gx : a);
+  *ymin = b < 0 ? 0 : (b > gy ? gy : b);
+  *xmax = c < 0 ? 0 : (c > gx ? gx : c);
+  *ymax = d < 0 ? 0 : (d > gy ? gy : d);
+}
+
+// p (3) through a column-major 4x4 stored as the reference passes it.
+GSR_HD void xform43(const float* m, float x, float y, float z, float* o) {
+  o[0] = m[0] * x + m[4] * y + m[8] * z + m[12];
+  o[1] = m[1] * x + m[5] * y + m[9] * z + m[13];
+  o[2] = m[2] * x + m[6] * y + m[10] * z + m[14];
+}
+GSR_HD void xform44(const float* m, float x, float y, float z, float* o) {
+  xform43(m, x, y, z, o);
+  o[3] = m[3] * x + m[7] * y + m[11] * z + m[15];
+}
+
+// 3-D covariance from scale (x modifier) and unit quaternion (r, x, y, z):
+// Sigma = R S S^T R^T, upper triangle (xx, xy, xz, yy, yz, zz).
+GSR_HD void cov3d_from_scale_rot(const float* s3, float mod, const float* q, float* cov) {
+  float r = q[0], x = q[1], y = q[2], z = q[3];
+  float R[9] = {1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y)};
+  float s[3] = {mod * s3[0], mod * s3[1], mod * s3[2]};
+  // M = R diag(s); Sigma = M M^T
+  float M[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) M[3 * i + j] = R[3 * i + j] * s[j];
+  int k = 0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = i; j < 3; ++j)
+      cov[k++] = M[3 * i + 0] * M[3 * j + 0] + M[3 * i + 1] * M[3 * j + 1] +
+                 M[3 * i + 2] * M[3 * j + 2];
+}
+
+// Jacobian-clamped EWA projection: returns T = J Wv (2x3) and the 2-D
+// covariance (a, b, c) before the 0.3 low-pass, plus the clamped view point.
+struct Ewa {
+  float T[6];
+  float a, b, c;
+  float tx, ty, tz;
+  float xmul, ymul;
+};
+
+GSR_HD Ewa ewa_project(float mx, float my, float mz, const float* cov3, const float* vm,
+                       float fx, float fy, float tanfx, float tanfy) {
+  Ewa e;
+  float t[3];
+  xform43(vm, mx, my, mz, t);
+  const float limx = 1.3f * tanfx, limy = 1.3f * tanfy;
+  const float txtz = t[0] / t[2], tytz = t[1] / t[2];
+  e.xmul = (txtz < -limx || txtz > limx) ? 0.0f : 1.0f;
+  e.ymul = (tytz < -limy || tytz > limy) ? 0.0f : 1.0f;
+  e.tx = fminf(limx, fmaxf(-limx, txtz)) * t[2];
+  e.ty = fminf(limy, fmaxf(-limy, tytz)) * t[2];
+  e.tz = t[2];
+  const float J00 = fx / e.tz, J02 = -(fx * e.tx) / (e.tz * e.tz);
+  const float J11 = fy / e.tz, J12 = -(fy * e.ty) / (e.tz * e.tz);
+  // Wv[r][c] = vm[r + 4c]
+  for (int c = 0; c < 3; ++c) {
+    e.T[c] = J00 * vm[0 + 4 * c] + J02 * vm[2 + 4 * c];
+    e.T[3 + c] = J11 * vm[1 + 4 * c] + J12 * vm[2 + 4 * c];
+  }
+  const float V[9] = {cov3[0], cov3[1], cov3[2], cov3[1], cov3[3], cov3[4],
+                      cov3[2], cov3[4], cov3[5]};
+  float TV0[3], TV1[3];  // rows of T V
+  for (int c = 0; c < 3; ++c) {
+    TV0[c] = e.T[0] * V[c] + e.T[1] * V[3 + c] + e.T[2] * V[6 + c];
+    TV1[c] = e.T[3] * V[c] + e.T[4] * V[3 + c] + e.T[5] * V[6 + c];
+  }
+  e.a = TV0[0] * e.T[0] + TV0[1] * e.T[1] + TV0[2] * e.T[2];
+  e.b = TV0[0] * e.T[3] + TV0[1] * e.T[4] + TV0[2] * e.T[5];
+  e.c = TV1[0] * e.T[3] + TV1[1] * e.T[4] + TV1[2] * e.T[5];
+  return e;
+}
+
+// View-dependent colour from SH (degree <= 3).  sh points at the M x 3
+// coefficients of one Gaussian; dir is the unit view direction.
+GSR_HD void sh_basis(int deg, float x, float y, float z, float* B /*16*/) {
+  B[0] = SH_C0;
+  if (deg > 0) {
+    B[1] = -SH_C1 * y; B[2] = SH_C1 * z; B[3] = -SH_C1 * x;
+    if (deg > 1) {
+      float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+      B[4] = SH_C2_0 * xy;
+      B[5] = SH_C2_1 * yz;
+      B[6] = SH_C2_2 * (2.0f * zz - xx - yy);
+      B[7] = SH_C2_3 * xz;
+      B[8] = SH_C2_4 * (xx - yy);
+      if (deg > 2) {
+        B[9] = SH_C3_0 * y * (3.0f * xx - yy);
+        B[10] = SH_C3_1 * xy * z;
+        B[11] = SH_C3_2 * y * (4.0f * zz - xx - yy);
+        B[12] = SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+        B[13] = SH_C3_4 * x * (4.0f * zz - xx - yy);
+        B[14] = SH_C3_5 * z * (xx - yy);
+        B[15] = SH_C3_6 * x * (xx - 3.0f * yy);
+      }
+    }
+  }
+}
+
+// d(basis)/d(x,y,z) for the direction backward (degree <= 3).
+GSR_HD void sh_basis_grad(int deg, float x, float y, float z, float* dX, float* dY, float* dZ) {
+  for (int i = 0; i < 16; ++i) { dX[i] = 0.f; dY[i] = 0.f; dZ[i] = 0.f; }
+  if (deg < 1) return;
+  dY[1] = -SH_C1; dZ[2] = SH_C1; dX[3] = -SH_C1;
+  if (deg < 2) return;
+  float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+  dX[4] = SH_C2_0 * y; dY[4] = SH_C2_0 * x;
+  dY[5] = SH_C2_1 * z; dZ[5] = SH_C2_1 * y;
+  dX[6] = SH_C2_2 * -2.0f * x; dY[6] = SH_C2_2 * -2.0f * y; dZ[6] = SH_C2_2 * 4.0f * z;
+  dX[7] = SH_C2_3 * z; dZ[7] = SH_C2_3 * x;
+  dX[8] = SH_C2_4 * 2.0f * x; dY[8] = SH_C2_4 * -2.0f * y;
+  if (deg < 3) return;
+  dX[9] = SH_C3_0 * 6.0f * xy; dY[9] = SH_C3_0 * 3.0f * (xx - yy);
+  dX[10] = SH_C3_1 * yz; dY[10] = SH_C3_1 * xz; dZ[10] = SH_C3_1 * xy;
+  dX[11] = SH_C3_2 * -2.0f * xy; dY[11] = SH_C3_2 * (4.0f * zz - xx - 3.0f * yy);
+  dZ[11] = SH_C3_2 * 8.0f * yz;
+  dX[12] = SH_C3_3 * -6.0f * xz; dY[12] = SH_C3_3 * -6.0f * yz;
+  dZ[12] = SH_C3_3 * (6.0f * zz - 3.0f * xx - 3.0f * yy);
+  dX[13] = SH_C3_4 * (4.0f * zz - 3.0f * xx - yy); dY[13] = SH_C3_4 * -2.0f * xy;
+  dZ[13] = SH_C3_4 * 8.0f * xz;
+  dX[14] = SH_C3_5 * 2.0f * xz; dY[14] = SH_C3_5 * -2.0f * yz; dZ[14] = SH_C3_5 * (xx - yy);
+  dX[15] = SH_C3_6 * 3.0f * (xx - yy); dY[15] = SH_C3_6 * -6.0f * xy;
+}
+
+}  // namespace gsr

@@ -1,0 +1,194 @@
+"""Splat-decoder glue, mirroring the reference's pixelsplat glue:
+
+  get_fov                  splatt3r_core/src/pixelsplat_src/projection.py:219-233
+  get_projection_matrix    splatt3r_core/src/pixelsplat_src/cuda_splatting.py:18-45
+  render_cuda              cuda_splatting.py:48-128
+  DecoderSplattingCUDA     splatt3r_core/src/pixelsplat_src/decoder_splatting_cuda.py:20-83
+  normalize_intrinsics     splatt3r_core/utils/geometry.py:6-11
+
+Camera bookkeeping (4x4 inverses, fov) is a handful of tiny torch ops; the
+per-splat work (covariance, SH residual, scale-invariant rescale, triu
+packing) is one fused HIP kernel (s3r_pack_splats) feeding the HIP
+rasterizer directly.
+"""
+from __future__ import annotations
+
+import ctypes
+from math import isqrt
+
+import torch
+
+from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+from splatt3r_amd import _lib
+
+_lib.register({
+    "s3r_pack_splats": (ctypes.c_int, [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.c_int,
+                        ctypes.c_float, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_void_p]),
+})
+
+
+def normalize_intrinsics(intrinsics, image_shape):
+    intrinsics = intrinsics.clone()
+    intrinsics[..., 0, :] /= image_shape[1]
+    intrinsics[..., 1, :] /= image_shape[0]
+    return intrinsics
+
+
+def get_fov(intrinsics):
+    intrinsics_inv = intrinsics.inverse()
+
+    def process_vector(vector):
+        vector = torch.tensor(vector, dtype=torch.float32, device=intrinsics.device)
+        vector = torch.einsum("bij,j->bi", intrinsics_inv, vector)
+        return vector / vector.norm(dim=-1, keepdim=True)
+
+    left = process_vector([0, 0.5, 1])
+    right = process_vector([1, 0.5, 1])
+    top = process_vector([0.5, 0, 1])
+    bottom = process_vector([0.5, 1, 1])
+    fov_x = (left * right).sum(dim=-1).acos()
+    fov_y = (top * bottom).sum(dim=-1).acos()
+    return torch.stack((fov_x, fov_y), dim=-1)
+
+
+def get_projection_matrix(near, far, fov_x, fov_y):
+    tan_fov_x = (0.5 * fov_x).tan()
+    tan_fov_y = (0.5 * fov_y).tan()
+    top = tan_fov_y * near
+    bottom = -top
+    right = tan_fov_x * near
+    left = -right
+    (b,) = near.shape
+    result = torch.zeros((b, 4, 4), dtype=torch.float32, device=near.device)
+    result[:, 0, 0] = 2 * near / (right - left)
+    result[:, 1, 1] = 2 * near / (top - bottom)
+    result[:, 0, 2] = (right + left) / (right - left)
+    result[:, 1, 2] = (top + bottom) / (top - bottom)
+    result[:, 3, 2] = 1
+    result[:, 2, 2] = far / (far - near)
+    result[:, 2, 3] = -(far * near) / (far - near)
+    return result
+
+
+def camera_settings(extrinsics, intrinsics, near, far, image_shape, background_color,
+                    sh_degree, scale_invariant=True):
+    """The per-view settings render_cuda builds (cuda_splatting.py:67-113),
+    for a batch of views.  Returns (list[GaussianRasterizationSettings], scale)."""
+    scale = 1 / near if scale_invariant else torch.ones_like(near)
+    extrinsics = extrinsics.clone()
+    extrinsics[..., :3, 3] = extrinsics[..., :3, 3] * scale[:, None]
+    near = near * scale
+    far = far * scale
+    h, w = image_shape
+    fov_x, fov_y = get_fov(intrinsics).unbind(dim=-1)
+    tan_fov_x = (0.5 * fov_x).tan()
+    tan_fov_y = (0.5 * fov_y).tan()
+    projection_matrix = get_projection_matrix(near, far, fov_x, fov_y).transpose(1, 2)
+    view_matrix = extrinsics.inverse().transpose(1, 2)
+    full_projection = view_matrix @ projection_matrix
+    tx = tan_fov_x.tolist()
+    ty = tan_fov_y.tolist()
+    out = []
+    for i in range(extrinsics.shape[0]):
+        out.append(GaussianRasterizationSettings(
+            image_height=h, image_width=w, tanfovx=tx[i], tanfovy=ty[i],
+            bg=background_color[i], scale_modifier=1.0, viewmatrix=view_matrix[i],
+            projmatrix=full_projection[i], sh_degree=sh_degree,
+            campos=extrinsics[i, :3, 3], prefiltered=False, debug=False))
+    return out, scale
+
+
+def render_cuda(extrinsics, intrinsics, near, far, image_shape, background_color,
+                gaussian_means, gaussian_covariances, gaussian_sh_coefficients,
+                gaussian_opacities, scale_invariant=True, use_sh=True):
+    """Same contract as cuda_splatting.render_cuda: [b,3,h,w]."""
+    assert use_sh or gaussian_sh_coefficients.shape[-1] == 1
+    _, _, _, n = gaussian_sh_coefficients.shape
+    degree = isqrt(n) - 1
+    settings, scale = camera_settings(extrinsics, intrinsics, near, far, image_shape,
+                                      background_color, degree, scale_invariant)
+    if scale_invariant:
+        gaussian_covariances = gaussian_covariances * (scale[:, None, None, None] ** 2)
+        gaussian_means = gaussian_means * scale[:, None, None]
+    shs = gaussian_sh_coefficients.permute(0, 1, 3, 2).contiguous()
+    row, col = torch.triu_indices(3, 3)
+    images = []
+    for i, rs in enumerate(settings):
+        mean_gradients = torch.zeros_like(gaussian_means[i], requires_grad=True)
+        image, _radii = GaussianRasterizer(rs)(
+            means3D=gaussian_means[i], means2D=mean_gradients,
+            shs=shs[i] if use_sh else None,
+            colors_precomp=None if use_sh else shs[i, :, 0, :],
+            opacities=gaussian_opacities[i, ..., None],
+            cov3D_precomp=gaussian_covariances[i, :, row, col])
+        images.append(image)
+    return torch.stack(images)
+
+
+def pack_splats(views, image_scale):
+    """Fused HIP packing of per-view head outputs into rasterizer inputs.
+
+    views: list of dicts with means [hw,3], scales [hw,3], rotations [hw,4]
+           (xyzw), sh [hw,3,1] (network residual), opacities [hw,1] and
+           img [hw,3] in [0,1] (the RGB2SH residual source), all f32 cuda.
+    image_scale: the scale-invariant factor s (means * s, cov * s^2).
+    Returns (means3D [P,3], cov6 [P,6], shs [P,1,3], opac [P,1]) with
+    P = sum(hw), in view order (view 0 first), as render_cuda receives them.
+    Restates build_covariance (utils/geometry.py:52-62), RGB2SH
+    (utils/sh_utils.py:114-115) and the rescale/triu of cuda_splatting.py:67-76,121-124.
+    """
+    dev = views[0]["means"].device
+    P = sum(v["means"].shape[0] for v in views)
+    means = torch.empty(P, 3, device=dev)
+    cov6 = torch.empty(P, 6, device=dev)
+    shs = torch.empty(P, 1, 3, device=dev)
+    opac = torch.empty(P, 1, device=dev)
+    off = 0
+    stream = _lib.stream(dev)
+    for v in views:
+        n = v["means"].shape[0]
+        ts = [v[k].float().contiguous() for k in ("means", "scales", "rotations", "sh",
+                                                   "opacities", "img")]
+        if ts[3].shape[-1] != 1:
+            raise NotImplementedError("pack_splats: sh_degree 0 (one SH coefficient) only")
+        _lib.call("s3r_pack_splats", *[t.data_ptr() for t in ts], n, 1, float(image_scale), 0,
+                  means[off:].data_ptr(), cov6[off:].data_ptr(), shs[off:].data_ptr(),
+                  opac[off:].data_ptr(), stream)
+        off += n
+    return means, cov6, shs, opac
+
+
+class DecoderSplattingCUDA(torch.nn.Module):
+    """decoder_splatting_cuda.py:20-83, fused packing for the sh_degree-0
+    head (Splatt3R's configuration) and the generic render_cuda otherwise."""
+
+    def __init__(self, background_color):
+        super().__init__()
+        self.register_buffer("background_color",
+                             torch.tensor(background_color, dtype=torch.float32),
+                             persistent=False)
+
+    def forward(self, batch, pred1, pred2, image_shape):
+        base_pose = batch["context"][0]["camera_pose"]
+        inv_base_pose = torch.inverse(base_pose)
+        extrinsics = torch.stack([t["camera_pose"] for t in batch["target"]], dim=1)
+        intrinsics = torch.stack([t["camera_intrinsics"] for t in batch["target"]], dim=1)
+        intrinsics = normalize_intrinsics(intrinsics, image_shape)[..., :3, :3]
+        extrinsics = inv_base_pose[:, None, :, :] @ extrinsics
+        means = torch.stack([pred1["means"], pred2["means_in_other_view"]], dim=1)
+        covariances = torch.stack([pred1["covariances"], pred2["covariances"]], dim=1)
+        harmonics = torch.stack([pred1["sh"], pred2["sh"]], dim=1)
+        opacities = torch.stack([pred1["opacities"], pred2["opacities"]], dim=1)
+        b, v, _, _ = extrinsics.shape
+        near = torch.full((b, v), 0.1, device=means.device)
+        far = torch.full((b, v), 1000.0, device=means.device)
+        bg = self.background_color.to(means.device)
+        flat = lambda x: x.reshape(b, -1, *x.shape[4:])
+        color = render_cuda(
+            extrinsics.reshape(b * v, 4, 4), intrinsics.reshape(b * v, 3, 3),
+            near.reshape(-1), far.reshape(-1), image_shape,
+            bg[None].expand(b * v, 3),
+            flat(means).repeat_interleave(v, 0), flat(covariances).repeat_interleave(v, 0),
+            flat(harmonics).repeat_interleave(v, 0),
+            flat(opacities).reshape(b, -1).repeat_interleave(v, 0))
+        return color.reshape(b, v, *color.shape[1:]), None

@@ -40,7 +40,8 @@ def test_library_exports_every_declared_symbol():
 def test_every_declared_symbol_has_a_ctypes_signature():
     from splatt3r_amd import _lib
     import importlib
-    for mod in ("splatt3r_amd.net", "splatt3r_amd.tracker", "diff_gaussian_rasterization"):
+    for mod in ("splatt3r_amd.net", "splatt3r_amd.tracker", "diff_gaussian_rasterization",
+                "splatt3r_amd.render"):
         try:
             importlib.import_module(mod)  # registers its signatures
         except ModuleNotFoundError:

@@ -1,0 +1,271 @@
+"""Tile rasterizer (include/gsr.h, drop-in diff_gaussian_rasterization).
+
+Oracle: oracle/raster_ref.c (canonical graphdeco algorithm; parity vs the
+reference's CUDA binary is unpinned: the submodule is absent).  The
+boundary inputs are pinned by tests/golden/render_boundary.npz, captured
+from the reference glue with a stub rasterizer (oracle/gen_golden.py).
+Forward bar: bit-exact vs the oracle (same operation order, fixed exp);
+backward: float atomics reorder sums -> rtol 1e-4 scaled tolerance.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import GOLDEN
+from splatt3r_amd.synthetic import (identity_camera_settings, raster_grad,
+                                    raster_microbench_scene, settings_to_dict)
+
+
+def small_scene(P, seed, H=48, W=64, fx=60.0):
+    K = np.array([[fx, 0, W / 2], [0, fx, H / 2], [0, 0, 1]], np.float32)
+    return raster_microbench_scene(P, H=H, W=W, K=K, seed=seed)
+
+
+def cpu_settings(sc):
+    rs, scale = identity_camera_settings(sc["K"], sc["H"], sc["W"], "cpu")
+    return settings_to_dict(rs), scale
+
+
+# ------------------------------------------------------------- CPU: oracle
+def test_oracle_single_gaussian_centre_value():
+    sc = small_scene(1, 0)
+    sd, scale = cpu_settings(sc)
+    H, W = sc["H"], sc["W"]
+    # a splat exactly on pixel (20, 30): invert the projection
+    z = 3.0
+    x = (30 - (W / 2 - 0.5)) / 60.0 * z
+    y = (20 - (H / 2 - 0.5)) / 60.0 * z
+    means = np.array([[x, y, z]], np.float32) * scale
+    cov = np.array([[4e-4, 0, 0, 4e-4, 0, 4e-4]], np.float32) * scale * scale
+    out = oracle.raster(sd, means, [[0.7]], colors_precomp=[[1.0, 0.5, 0.25]], cov3D_precomp=cov)
+    c = out["color"][:, 20, 30]
+    assert out["radii"][0] > 0
+    # power ~ 0 at the centre -> alpha = 0.7, T = 1, bg = 0
+    np.testing.assert_allclose(c, np.array([1.0, 0.5, 0.25]) * 0.7, rtol=1e-3)
+
+
+def test_oracle_front_splat_occludes_back():
+    sc = small_scene(1, 0)
+    sd, scale = cpu_settings(sc)
+    means = np.array([[0, 0, 2.0], [0, 0, 4.0]], np.float32) * scale
+    cov = np.array([[1e-2, 0, 0, 1e-2, 0, 1e-2]] * 2, np.float32) * scale * scale
+    out = oracle.raster(sd, means, [[0.99], [0.99]], colors_precomp=[[1, 0, 0], [0, 1, 0]],
+                        cov3D_precomp=cov)
+    c = out["color"][:, 23, 31]
+    # the splat centre sits half a pixel off (31.5, 23.5): alpha just under 0.99
+    assert c[0] > 0.9 and c[1] < 0.05 and c[0] > 20 * c[1]
+
+
+def test_oracle_culls_behind_near_plane():
+    sc = small_scene(1, 0)
+    sd, scale = cpu_settings(sc)
+    means = np.array([[0, 0, 0.01]], np.float32) * scale  # view z = 0.1 <= 0.2
+    out = oracle.raster(sd, means, [[0.9]], colors_precomp=[[1, 1, 1]],
+                        cov3D_precomp=np.array([[1e-2, 0, 0, 1e-2, 0, 1e-2]], np.float32))
+    assert out["radii"][0] == 0 and out["num_rendered"] == 0
+    assert np.all(out["color"] == 0)
+
+
+def test_oracle_backward_colour_grad_is_exact_and_opacity_grad_matches_fd():
+    sc = small_scene(40, 3)
+    sd, scale = cpu_settings(sc)
+    m = sc["means"] * scale
+    cov = sc["cov6"] * scale * scale
+    op = sc["opacities"]
+    col = np.clip(sc["shs"][:, 0, :] + 0.5, 0, 1).astype(np.float32)
+    g = raster_grad(sc["H"], sc["W"], seed=4)
+    out = oracle.raster(sd, m, op, colors_precomp=col, cov3D_precomp=cov, dL_dout=g)
+    L = lambda o: float((o["color"] * g).sum())
+    # colours enter linearly: finite difference is exact up to rounding
+    k = int(np.argmax(out["radii"]))
+    for ch in range(3):
+        c2 = col.copy(); c2[k, ch] += 1e-2
+        fd = (L(oracle.raster(sd, m, op, colors_precomp=c2, cov3D_precomp=cov)) - L(out)) / 1e-2
+        np.testing.assert_allclose(out["dL_dcolors"][k, ch], fd, rtol=2e-3, atol=2e-3)
+    o2 = op.copy(); o2[k] += 1e-3
+    o3 = op.copy(); o3[k] -= 1e-3
+    fd = (L(oracle.raster(sd, m, o2, colors_precomp=col, cov3D_precomp=cov)) -
+          L(oracle.raster(sd, m, o3, colors_precomp=col, cov3D_precomp=cov))) / 2e-3
+    np.testing.assert_allclose(out["dL_dopacity"][k], fd, rtol=5e-2, atol=5e-3)
+
+
+def test_render_glue_settings_match_reference_boundary():
+    from splatt3r_amd.render import camera_settings, normalize_intrinsics
+    g = np.load(os.path.join(GOLDEN, "render_boundary.npz"))
+    h, w = int(g["settings_image_height"]), int(g["settings_image_width"])
+    ctx = torch.from_numpy(g["head_ctx_pose"])
+    tgt = torch.from_numpy(g["head_tgt_pose"])
+    K = torch.from_numpy(g["head_K"])
+    ext = torch.inverse(ctx) @ tgt
+    intr = normalize_intrinsics(K, (h, w))
+    st, scale = camera_settings(ext, intr, torch.full((1,), 0.1), torch.full((1,), 1000.0),
+                                (h, w), torch.zeros(1, 3), 0)
+    rs = st[0]
+    np.testing.assert_allclose(rs.tanfovx, g["settings_tanfovx"], rtol=1e-6)
+    np.testing.assert_allclose(rs.tanfovy, g["settings_tanfovy"], rtol=1e-6)
+    np.testing.assert_allclose(rs.viewmatrix.numpy(), g["settings_viewmatrix"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(rs.projmatrix.numpy(), g["settings_projmatrix"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(rs.campos.numpy(), g["settings_campos"], rtol=1e-6, atol=1e-6)
+
+
+# -------------------------------------------------------------- GPU: HIP
+def _to(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+def _gpu_render(sc, mode="shs", grad=None, P=None):
+    from diff_gaussian_rasterization import GaussianRasterizer
+    rs, scale = identity_camera_settings(sc["K"], sc["H"], sc["W"], "cuda")
+    m = _to(sc["means"] * scale).requires_grad_(grad is not None)
+    cov = _to(sc["cov6"] * scale * scale).requires_grad_(grad is not None)
+    op = _to(sc["opacities"]).requires_grad_(grad is not None)
+    m2 = torch.zeros_like(m, requires_grad=True)
+    kw = dict(means3D=m, means2D=m2, opacities=op, cov3D_precomp=cov)
+    if mode == "shs":
+        shs = _to(sc["shs"]).requires_grad_(grad is not None)
+        kw["shs"] = shs
+    else:
+        col = _to(np.clip(sc["shs"][:, 0, :] + 0.5, 0, 1)).requires_grad_(grad is not None)
+        kw["colors_precomp"] = col
+    img, radii = GaussianRasterizer(rs)(**kw)
+    if grad is not None:
+        (img * _to(grad)).sum().backward()
+    return rs, scale, img, radii, kw
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,seed,mode", [(2000, 0, "shs"), (5000, 1, "colors"), (1, 2, "shs")])
+def test_hip_forward_bitexact_vs_oracle(P, seed, mode):
+    sc = small_scene(P, seed)
+    rs, scale, img, radii, kw = _gpu_render(sc, mode)
+    sd = settings_to_dict(rs)
+    ref = oracle.raster(sd, sc["means"] * scale, sc["opacities"],
+                        shs=sc["shs"] if mode == "shs" else None,
+                        colors_precomp=None if mode == "shs" else np.clip(sc["shs"][:, 0, :] + 0.5, 0, 1),
+                        cov3D_precomp=sc["cov6"] * scale * scale)
+    np.testing.assert_array_equal(radii.cpu().numpy(), ref["radii"])
+    np.testing.assert_array_equal(img.detach().cpu().numpy(), ref["color"])
+
+
+@pytest.mark.gpu
+def test_hip_forward_c3_resolution_vs_oracle():
+    sc = raster_microbench_scene(200_000, seed=0)
+    rs, scale, img, radii, _ = _gpu_render(sc, "shs")
+    ref = oracle.raster(settings_to_dict(rs), sc["means"] * scale, sc["opacities"], shs=sc["shs"],
+                        cov3D_precomp=sc["cov6"] * scale * scale, nthreads=16)
+    np.testing.assert_array_equal(radii.cpu().numpy(), ref["radii"])
+    np.testing.assert_array_equal(img.detach().cpu().numpy(), ref["color"])
+
+
+@pytest.mark.gpu
+def test_hip_backward_vs_oracle():
+    sc = small_scene(3000, 5)
+    g = raster_grad(sc["H"], sc["W"], seed=6)
+    rs, scale, img, radii, kw = _gpu_render(sc, "shs", grad=g)
+    ref = oracle.raster(settings_to_dict(rs), sc["means"] * scale, sc["opacities"], shs=sc["shs"],
+                        cov3D_precomp=sc["cov6"] * scale * scale, dL_dout=g)
+
+    def close(a, b, name):
+        a = a.detach().cpu().numpy().reshape(b.shape)
+        tol = 1e-4 * (np.abs(b).max() + 1e-12)
+        err = np.abs(a - b).max()
+        assert err <= tol + 1e-6, f"{name}: max err {err} > {tol}"
+
+    close(kw["means2D"].grad[:, :2], ref["dL_dmeans2D"][:, :2], "means2D")
+    close(kw["opacities"].grad, ref["dL_dopacity"].reshape(-1, 1), "opacity")
+    close(kw["shs"].grad, ref["dL_dsh"], "sh")
+    close(kw["cov3D_precomp"].grad, ref["dL_dcov3D"], "cov3D")
+    close(kw["means3D"].grad, ref["dL_dmeans3D"], "means3D")
+
+
+@pytest.mark.gpu
+def test_hip_api_contract():
+    from diff_gaussian_rasterization import GaussianRasterizer
+    sc = small_scene(10, 0)
+    rs, scale = identity_camera_settings(sc["K"], sc["H"], sc["W"], "cuda")
+    m = _to(sc["means"])
+    with pytest.raises(Exception, match="excatly one of either SHs"):
+        GaussianRasterizer(rs)(means3D=m, means2D=m, opacities=_to(sc["opacities"]),
+                               cov3D_precomp=_to(sc["cov6"]))
+    with pytest.raises(Exception, match="scale/rotation pair"):
+        GaussianRasterizer(rs)(means3D=m, means2D=m, opacities=_to(sc["opacities"]),
+                               shs=_to(sc["shs"]))
+    # empty input: image of zeros, empty radii (reference: P == 0 -> no render)
+    img, radii = GaussianRasterizer(rs)(means3D=m[:0], means2D=m[:0], opacities=_to(sc["opacities"])[:0],
+                                        shs=_to(sc["shs"])[:0], cov3D_precomp=_to(sc["cov6"])[:0])
+    assert img.shape == (3, sc["H"], sc["W"]) and radii.shape == (0,)
+    assert float(img.abs().sum()) == 0.0
+    vis = GaussianRasterizer(rs).markVisible(_to(sc["means"] * scale))
+    assert vis.dtype == torch.bool and bool(vis.all())
+    # inference_mode + requires_grad means2D (cuda_splatting.py:94)
+    with torch.inference_mode():
+        img, radii = GaussianRasterizer(rs)(means3D=_to(sc["means"] * scale), means2D=m,
+                                            opacities=_to(sc["opacities"]), shs=_to(sc["shs"]),
+                                            cov3D_precomp=_to(sc["cov6"] * scale * scale))
+    assert img.shape == (3, sc["H"], sc["W"])
+
+
+@pytest.mark.gpu
+def test_hip_scale_rotation_path_matches_precomputed_cov():
+    from diff_gaussian_rasterization import GaussianRasterizer
+    rng = np.random.default_rng(0)
+    sc = small_scene(500, 7)
+    rs, scale = identity_camera_settings(sc["K"], sc["H"], sc["W"], "cuda")
+    s3 = np.exp(rng.uniform(np.log(0.005), np.log(0.03), (500, 3))).astype(np.float32) * scale
+    q = rng.normal(size=(500, 4)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)  # (r, x, y, z) order on this path
+    R = oracle_rot_wxyz(q)
+    cov = np.einsum("nik,nk,njk->nij", R, s3 * s3, R)
+    iu = np.triu_indices(3)
+    m = _to(sc["means"] * scale)
+    base = dict(means3D=m, means2D=torch.zeros_like(m), opacities=_to(sc["opacities"]),
+                shs=_to(sc["shs"]))
+    a, _ = GaussianRasterizer(rs)(**base, scales=_to(s3), rotations=_to(q))
+    b, _ = GaussianRasterizer(rs)(**base, cov3D_precomp=_to(cov[:, iu[0], iu[1]].astype(np.float32)))
+    np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), atol=2e-4)
+
+
+def oracle_rot_wxyz(q):
+    r, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    return np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y),
+                     2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x),
+                     2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)],
+                    -1).reshape(-1, 3, 3)
+
+
+@pytest.mark.gpu
+def test_hip_render_glue_boundary_vs_reference_capture():
+    """Our fused packing + settings reproduce what the reference glue hands
+    the rasterizer (render_boundary.npz), then the HIP render matches the
+    oracle on exactly the captured inputs."""
+    from splatt3r_amd.render import pack_splats
+    g = np.load(os.path.join(GOLDEN, "render_boundary.npz"))
+    hw = g["head_m1"].shape[1] * g["head_m1"].shape[2]
+    views = []
+    for v in ("1", "2"):
+        views.append(dict(means=_to(g["head_m" + v].reshape(hw, 3)),
+                          scales=_to(g["head_s" + v].reshape(hw, 3)),
+                          rotations=_to(g["head_r" + v].reshape(hw, 4)),
+                          sh=_to(g["head_sh" + v].reshape(hw, 3, 1)),
+                          opacities=_to(g["head_o" + v].reshape(hw, 1)),
+                          img=_to(g["head_img" + v].reshape(3, hw))))
+    scale = float(1.0 / torch.tensor(0.1, dtype=torch.float32))
+    from splatt3r_amd import _lib
+    means, cov6, shs, opac = [], [], [], []
+    P = 2 * hw
+    means = torch.empty(P, 3, device="cuda"); cov6 = torch.empty(P, 6, device="cuda")
+    shs = torch.empty(P, 1, 3, device="cuda"); opac = torch.empty(P, 1, device="cuda")
+    for i, v in enumerate(views):
+        o = i * hw
+        _lib.call("s3r_pack_splats", v["means"].data_ptr(), v["scales"].data_ptr(),
+                  v["rotations"].data_ptr(), v["sh"].data_ptr(), v["opacities"].data_ptr(),
+                  v["img"].data_ptr(), hw, 1, scale, 1, means[o:].data_ptr(), cov6[o:].data_ptr(),
+                  shs[o:].data_ptr(), opac[o:].data_ptr(), _lib.stream())
+    np.testing.assert_allclose(means.cpu().numpy(), g["in_means3D"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(cov6.cpu().numpy(), g["in_cov3D_precomp"], rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(shs.cpu().numpy(), g["in_shs"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(opac.cpu().numpy(), g["in_opacities"])
+    del pack_splats

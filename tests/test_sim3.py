@@ -141,10 +141,12 @@ def test_hip_sim3_ops_vs_oracle():
                                   oracle.sim3_act(Tn, Xn))
     np.testing.assert_array_equal((T * U).data.cpu().numpy(), oracle.sim3_mul(Tn, Un))
     np.testing.assert_array_equal(T.inv().data.cpu().numpy(), oracle.sim3_inv(Tn))
-    # exp / retr go through sinf/cosf/expf (libm vs device ocml): 2 ulp class
+    # exp / retr go through sinf/cosf/expf (libm vs device ocml, ~1 ulp); the
+    # W coefficients (C - ...)/theta^2 (gn_kernels.cu:367-370) cancel, which
+    # amplifies that to ~1e-5 absolute on the translation.
     xi = torch.from_numpy(xin).cuda()
     np.testing.assert_allclose(lietorch.Sim3.exp(xi).data.cpu().numpy(), oracle.sim3_exp(xin),
-                               rtol=2e-6, atol=2e-6)
+                               rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(T.retr(xi).data.cpu().numpy(), oracle.sim3_retr(Tn, xin),
                                rtol=1e-5, atol=1e-5)
 
