@@ -54,7 +54,7 @@ _lib.register({
     "gsr_geom_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
     "gsr_image_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
     "gsr_binning_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
-    "gsr_preprocess": (ctypes.c_int, [_SP, ctypes.c_int64, ctypes.c_int] + [P_] * 8 +
+    "gsr_preprocess": (ctypes.c_int, [_SP, ctypes.c_int64, ctypes.c_int] + [P_] * 7 +
                        [P_, P_, ctypes.POINTER(ctypes.c_int64), P_]),
     "gsr_render": (ctypes.c_int, [_SP, ctypes.c_int64, ctypes.c_int64, P_, P_, P_, P_, P_, P_]),
     "gsr_backward": (ctypes.c_int, [_SP, ctypes.c_int64, ctypes.c_int, ctypes.c_int64] +

@@ -50,6 +50,38 @@ def test_every_declared_symbol_has_a_ctypes_signature():
     assert not missing, f"no ctypes signature for: {missing}"
 
 
+def declared_param_counts():
+    counts = {}
+    for h in glob.glob(os.path.join(REPO, "include", "*.h")):
+        txt = open(h).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        txt = re.sub(r"//.*", "", txt)
+        body = txt.split('extern "C" {', 1)[-1]
+        for m in re.finditer(r"\b([a-z][a-z0-9_]*)\s*\(([^;{]*?)\)\s*;", body, flags=re.S):
+            name, params = m.group(1), m.group(2).strip()
+            if not name.startswith(("s3", "gsr")):
+                continue
+            counts[name] = 0 if params in ("", "void") else params.count(",") + 1
+    return counts
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every ctypes argtypes list has exactly as many entries as the C
+    declaration has parameters (catches binding drift without a GPU)."""
+    from splatt3r_amd import _lib
+    import importlib
+    for mod in ("splatt3r_amd.net", "splatt3r_amd.tracker", "diff_gaussian_rasterization",
+                "splatt3r_amd.render"):
+        try:
+            importlib.import_module(mod)
+        except ModuleNotFoundError:
+            pass
+    counts = declared_param_counts()
+    bad = {n: (len(_lib.SIGNATURES[n][1]), c) for n, c in counts.items()
+           if n in _lib.SIGNATURES and len(_lib.SIGNATURES[n][1]) != c}
+    assert not bad, f"argtypes arity (ctypes, header) mismatch: {bad}"
+
+
 def test_abi_metadata():
     from splatt3r_amd import _lib
     lib = _lib.lib()
