@@ -1,0 +1,143 @@
+/*
+ * s3n.h — MASt3RGaussians network kernels (ViT-L encoder, Base decoder,
+ * DPT-Gaussian heads) for gfx950 MFMA.
+ *
+ * Replaces the torch/cuBLAS/cuDNN execution of
+ *   splatt3r_core/src/mast3r_src/dust3r/dust3r/model.py:121-193
+ *   (_encode_image, _decoder, _downstream_head),
+ *   croco/models/blocks.py:58-191 (Mlp, Attention, Block, CrossAttention,
+ *   DecoderBlock), croco/models/pos_embed.py:106-159 (RoPE2D) ==
+ *   croco/models/curope/kernels.cu:18-82, croco/models/dpt_block.py
+ *   (DPT adapter), mast3r/catmlp_dpt_head.py:140-278 (GaussianHead,
+ *   gaussian_postprocess), dust3r/heads/postprocess.py:22-58.
+ * The Python model object behind the reference API
+ * (model.encoder._encode_image / _decoder / _downstream_head) lives in
+ * splatt3r-slam_amd/splatt3r_amd/net.py and drives these entry points.
+ *
+ * Data types: activations entering a matrix product are fp16 (10-bit
+ * mantissa, the TF32 class of the reference's matmuls); every product
+ * accumulates in fp32 on MFMA; the transformer residual stream and every
+ * head output are fp32.
+ * "groups" batch up to 4 independent problems of identical shape with
+ * different pointers in one launch (decoder branch 1/2, heads 1/2, the four
+ * DPTs), i.e. a grouped GEMM.
+ */
+#ifndef S3N_H
+#define S3N_H
+#include "s3_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define S3N_MAX_GROUPS 4
+
+enum { S3N_ACT_NONE = 0, S3N_ACT_GELU = 1, S3N_ACT_RELU = 2 };
+enum { S3N_STORE_PLAIN = 0, S3N_STORE_CONVT = 1, S3N_STORE_PIXSHUF = 2 };
+enum { S3N_A_DENSE = 0, S3N_A_CONV = 1 };
+
+/* C[M,N] = epilogue( A[M,K] . B[N,K]^T ).
+ * A: fp16, dense row-major (lda) or an implicit im2col of an NHWC fp16
+ *    image (a_mode = S3N_A_CONV: k = (ky*ks + kx)*Cin + ci, zero padding,
+ *    optional ReLU applied to the loaded input).
+ * B: fp16 weights [N, K] row-major (ldb), i.e. nn.Linear layout / conv
+ *    weight permuted to [Cout, ky, kx, Cin].
+ * Epilogue: + bias[N] (fp32) -> act -> + R1 -> + R2 -> store C (fp32 or
+ *    fp16, row-major ldc, or scattered: CONVT = ConvTranspose2d(k=s)
+ *    pixel scatter into NHWC [B, sH*s, sW*s, sCout] with n = (i*s+j)*sCout+co;
+ *    PIXSHUF = transpose + F.pixel_shuffle(s) into NHWC [B, sH*s, sW*s, sCout]
+ *    with n = co*s*s + i*s + j) and optionally a second fp16 copy C2 (ldc2). */
+typedef struct {
+  int M, N, K, groups;
+  const void* A[S3N_MAX_GROUPS];
+  int64_t lda;
+  const void* B[S3N_MAX_GROUPS];
+  int64_t ldb;
+  const float* bias[S3N_MAX_GROUPS];
+  const void* R1[S3N_MAX_GROUPS];
+  int64_t ldr1;
+  int r1_f16;
+  const void* R2[S3N_MAX_GROUPS];
+  int64_t ldr2;
+  int r2_f16;
+  void* C[S3N_MAX_GROUPS];
+  int64_t ldc;
+  int c_f16;
+  void* C2[S3N_MAX_GROUPS];
+  int64_t ldc2;
+  int act;
+  int store_mode;
+  int a_mode;
+  /* implicit conv (a_mode == S3N_A_CONV): input NHWC [Bn, cH, cW, cC] */
+  int cH, cW, cC, ksize, stride, pad, oH, oW, relu_in;
+  /* scatter stores: token grid sH x sW, factor s, output channels sCout */
+  int sH, sW, sS, sCout;
+} s3n_gemm_args;
+
+int s3n_gemm(const s3n_gemm_args* args, void* stream);
+
+/* Fused multi-head attention softmax(Q K^T * scale) V with 2-D RoPE
+ * (pos_embed.py:142-159, base 100, F0 1) applied to Q and K on load.
+ * Q rows at Q + (b*Nq + n)*q_stride + h*64, K/V likewise; O rows at
+ * O + (b*Nq + n)*o_stride + h*64 (fp16).  pos: int64 [B, N, 2] (y, x);
+ * NULL disables RoPE.  cos/sin tables: [maxpos, 16] fp32 computed as the
+ * reference computes them. head_dim is 64. */
+typedef struct {
+  int B, Nq, Nk, H, groups;
+  const void* Q[S3N_MAX_GROUPS];
+  const void* K[S3N_MAX_GROUPS];
+  const void* V[S3N_MAX_GROUPS];
+  int64_t q_stride, k_stride, v_stride;
+  const int64_t* qpos[S3N_MAX_GROUPS];
+  const int64_t* kpos[S3N_MAX_GROUPS];
+  const float* rope_cos;
+  const float* rope_sin;
+  int rope_maxpos;
+  void* O[S3N_MAX_GROUPS];
+  int64_t o_stride;
+  float scale;
+} s3n_attn_args;
+
+int s3n_attention(const s3n_attn_args* args, void* stream);
+
+/* LayerNorm over the last dim C (eps), per group gamma/beta:
+ * y = (x - mean) * rsqrt(var + eps) * gamma + beta.  x fp32 [rows, ldx];
+ * out16 (fp16, ld16) and/or out32 (fp32, ld32) may be NULL. */
+int s3n_layernorm(int rows, int C, int groups, const float* const* x, int64_t ldx,
+                  const float* const* gamma, const float* const* beta, float eps,
+                  void* const* out16, int64_t ld16, float* const* out32, int64_t ld32,
+                  void* stream);
+
+/* Patch embedding im2col (patch_embed.py:42-70, landscape): image
+ * [B,3,H,W] fp32 -> A [B*(H/p)*(W/p), 3*p*p] fp16, k = c*p*p + ky*p + kx. */
+int s3n_patch_im2col(const float* img, int B, int H, int W, int p, void* A, void* stream);
+
+/* Bilinear x2 upsample, align_corners=True (dpt_block.py:207-212,
+ * Interpolate :262-270), NHWC fp16 -> NHWC fp16, per group. */
+int s3n_upsample2x(int groups, const void* const* in, void* const* out, int B, int H, int W,
+                   int C, void* stream);
+
+/* gaussian_postprocess (catmlp_dpt_head.py:140-178) + the 43-channel
+ * concatenation of GaussianHead.forward (:245-278) for one view:
+ * pts [n, ld_pts] (4: xyz, conf), feat [n, 25] (desc 24, desc_conf),
+ * gauss [n, ld_g] (14: offset 3, scales 3, rot 4, sh 3, opacity 1) ->
+ * pts3d [n,3], conf [n], desc [n,24] (+ optional fp16 copy desc16),
+ * desc_conf [n], scales [n,3], rotations [n,4], sh [n,3], opacities [n],
+ * means [n,3].  depth mode ('exp',-inf,inf), conf mode ('exp',1,inf). */
+int s3n_gaussian_postprocess(int64_t n, const float* pts, int ld_pts, const float* feat,
+                             const float* gauss, int ld_g, int use_offsets, float* pts3d,
+                             float* conf, float* desc, void* desc16, float* desc_conf,
+                             float* scales, float* rotations, float* sh, float* opacities,
+                             float* means, void* stream);
+
+/* Portable counter-based weights: w[i] = (2u-1)*a + c with
+ * u = (splitmix64(seed + (i+1)*0x9E3779B97F4A7C15) >> 40) * 2^-24, fp32. */
+int s3n_prng_fill(float* out, int64_t n, uint64_t seed, float a, float c, void* stream);
+
+/* fp32 -> fp16 conversion (round to nearest even), n elements. */
+int s3n_cast_f16(const float* in, void* out, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* S3N_H */

@@ -153,7 +153,105 @@ def gen_render():
     print("wrote render_boundary.npz", {k: v.shape for k, v in out.items() if k.startswith("in_")})
 
 
-SECTIONS = {"matching": gen_matching, "render": gen_render}
+def build_reference_model(cfg):
+    """mast3r.model.AsymmetricMASt3R with the Splatt3R arguments
+    (splatt3r_core/main.py:54-71), imported from /root/reference."""
+    src = os.path.join(REF, "splatt3r_core", "src", "mast3r_src")
+    for p in (os.path.join(src, "dust3r"), src):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import mast3r.model as mm
+    return mm.AsymmetricMASt3R(
+        pos_embed="RoPE100", patch_embed_cls="ManyAR_PatchEmbed", img_size=(512, 512),
+        head_type="gaussian_head", output_mode=f"pts3d+gaussian+desc{cfg.desc_dim}",
+        depth_mode=("exp", -mm.inf, mm.inf), conf_mode=("exp", 1, mm.inf),
+        enc_embed_dim=cfg.enc_dim, enc_depth=cfg.enc_depth, enc_num_heads=cfg.enc_heads,
+        dec_embed_dim=cfg.dec_dim, dec_depth=cfg.dec_depth, dec_num_heads=cfg.dec_heads,
+        two_confs=True, use_offsets=cfg.use_offsets, sh_degree=cfg.sh_degree).eval()
+
+
+def load_prng(model, cfg, seed):
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "splatt3r-slam_amd"))
+    from splatt3r_amd import weights as W
+    sd = model.state_dict()
+    man = W.manifest(cfg)
+    assert [n for n, _ in man] == list(sd.keys()), "manifest order differs from the reference"
+    assert all(tuple(sd[n].shape) == tuple(s) for n, s in man), "manifest shapes differ"
+    new = {n: torch.from_numpy(W.prng_tensor_numpy(seed, n, s)) for n, s in man}
+    model.load_state_dict(new)
+    return man
+
+
+def run_reference(model, img1, img2):
+    """dust3r model.py:121-193 driven as splatt3r_utils.decoder() does
+    (encode each view, _decoder, heads in fp32)."""
+    shape = torch.tensor([list(img1.shape[-2:])], dtype=torch.int32)
+    f1, p1, _ = model._encode_image(img1, shape)
+    f2, p2, _ = model._encode_image(img2, shape)
+    dec1, dec2 = model._decoder(f1, p1, f2, p2)
+    dec1, dec2 = list(dec1), list(dec2)
+    r1 = model._downstream_head(1, [t.float() for t in dec1], shape)
+    r2 = model._downstream_head(2, [t.float() for t in dec2], shape)
+    return f1, f2, p1, dec1, dec2, r1, r2
+
+
+def gen_net():
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "splatt3r-slam_amd"))
+    from splatt3r_amd import weights as W
+    import dataclasses
+    keys = ("pts3d", "conf", "desc", "desc_conf", "scales", "rotations", "sh", "opacities", "means")
+    # (a) reduced config, full outputs, both use_offsets values
+    for use_off in (True, False):
+        cfg = dataclasses.replace(W.SMALL, use_offsets=use_off)
+        torch.manual_seed(0)
+        model = build_reference_model(cfg)
+        man = load_prng(model, cfg, seed=1234)
+        g = torch.Generator().manual_seed(5)
+        H, Wd = 48, 64
+        img1 = torch.rand(1, 3, H, Wd, generator=g) * 2 - 1
+        img2 = torch.rand(1, 3, H, Wd, generator=g) * 2 - 1
+        f1, f2, p1, dec1, dec2, r1, r2 = run_reference(model, img1, img2)
+        out = dict(img1=img1.numpy(), img2=img2.numpy(), feat1=f1.numpy(), feat2=f2.numpy(),
+                   pos=p1.numpy())
+        for hk in cfg.hooks:
+            out[f"dec1_{hk}"] = dec1[hk].numpy()
+            out[f"dec2_{hk}"] = dec2[hk].numpy()
+        for k in keys:
+            out["res1_" + k] = r1[k].numpy()
+            out["res2_" + k] = r2[k].numpy()
+        tag = "small_off" if use_off else "small_nooff"
+        np.savez_compressed(os.path.join(GOLDEN, f"net_{tag}.npz"), **out)
+        print(f"wrote net_{tag}.npz")
+        if use_off:
+            with open(os.path.join(GOLDEN, "manifest_small.txt"), "w") as f:
+                f.writelines(f"{n} {list(s)}\n" for n, s in man)
+    # (b) full Splatt3R architecture at 384x512: slices + checksums
+    cfg = W.FULL
+    torch.manual_seed(0)
+    model = build_reference_model(cfg)
+    man = load_prng(model, cfg, seed=1234)
+    with open(os.path.join(GOLDEN, "manifest_full.txt"), "w") as f:
+        f.writelines(f"{n} {list(s)}\n" for n, s in man)
+    g = torch.Generator().manual_seed(6)
+    img1 = torch.rand(1, 3, 384, 512, generator=g) * 2 - 1
+    img2 = torch.rand(1, 3, 384, 512, generator=g) * 2 - 1
+    f1, f2, p1, dec1, dec2, r1, r2 = run_reference(model, img1, img2)
+    out = dict(img1=img1.numpy(), img2=img2.numpy(), feat1_rows=f1[0, ::37].numpy(),
+               feat1_sum=f1.double().sum().numpy(), feat1_abs=f1.double().abs().sum().numpy())
+    for hk in cfg.hooks:
+        out[f"dec1_{hk}_rows"] = dec1[hk][0, ::37].numpy()
+        out[f"dec2_{hk}_rows"] = dec2[hk][0, ::37].numpy()
+    for k in keys:
+        for ri, r in (("1", r1), ("2", r2)):
+            v = r[k][0]
+            out[f"res{ri}_{k}_sub"] = v[::8, ::8].numpy()
+            out[f"res{ri}_{k}_sum"] = v.double().sum().numpy()
+            out[f"res{ri}_{k}_abs"] = v.double().abs().sum().numpy()
+    np.savez_compressed(os.path.join(GOLDEN, "net_full_384x512.npz"), **out)
+    print("wrote net_full_384x512.npz")
+
+
+SECTIONS = {"matching": gen_matching, "render": gen_render, "net": gen_net}
 
 
 def main(argv):

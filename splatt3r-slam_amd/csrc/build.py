@@ -39,8 +39,7 @@ SOURCES = {
     "splat_pack.hip": STRICT,
     "net_gemm.hip": FAST,
     "net_attn.hip": FAST,
-    "net_ops.hip": FAST,
-    "net_conv.hip": FAST,
+    "net_ops.hip": STRICT,
 }
 
 

@@ -1,0 +1,284 @@
+// Fused RoPE2D + multi-head attention, head_dim 64 (include/s3n.h).
+//
+// One 256-lane workgroup = 64 query rows of one (group, batch, head); each
+// wave owns 16 rows.  S = Q K^T and O += P V run on v_mfma_f32_16x16x32_f16
+// with fp32 accumulation; softmax is online (running max / sum per row,
+// base-2 exponent).  K and V tiles of 64 keys are staged global -> registers
+// -> LDS (double buffered): K with RoPE applied while staging (each lane
+// rotates a (d, d+16) chunk pair), V row-major and consumed through the
+// gfx950 transpose read ds_read_b64_tr_b16 so it needs no transpose pass.
+// P goes through a 2 KiB per-wave LDS scratch to change from the MFMA C
+// layout (key on the lane) to the A layout (query on the lane).
+// RoPE (croco/models/pos_embed.py:106-159): head dims [0,32) rotate with
+// the y position, [32,64) with x; within each half, dim d pairs with d+16:
+// out[d] = x[d] cos - x[d+16] sin, out[d+16] = x[d+16] cos + x[d] sin.
+#include "common.hpp"
+#include "s3n.h"
+
+namespace {
+
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int QT = 64;   // query rows per workgroup
+constexpr int KT = 64;   // keys per tile
+constexpr int D = 64;
+constexpr int kThreads = 256;
+
+struct AttnP {
+  int B, Nq, Nk, H, groups;
+  const f16* Q[S3N_MAX_GROUPS];
+  const f16* K[S3N_MAX_GROUPS];
+  const f16* V[S3N_MAX_GROUPS];
+  int64_t qs, ks, vs;
+  const int64_t* qpos[S3N_MAX_GROUPS];
+  const int64_t* kpos[S3N_MAX_GROUPS];
+  const float* cosT;
+  const float* sinT;
+  int maxpos;
+  f16* O[S3N_MAX_GROUPS];
+  int64_t os;
+  float scale_log2;
+};
+
+__device__ __forceinline__ int kswz(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+// Rotate chunk `c` (8 dims) of a head row given both it and its partner
+// chunk c^2; returns the rotated chunk c.
+__device__ __forceinline__ f16x8 rope_chunk(f16x8 x, f16x8 partner, int c, int64_t py, int64_t px,
+                                            const float* cosT, const float* sinT) {
+  const int half = c >> 2;             // 0: y dims, 1: x dims
+  const int lo = ((c & 3) < 2);        // chunk holds dims [0,16) of its half
+  const int64_t pos = half ? px : py;
+  const int f0 = (c & 1) * 8;          // frequency index of the first dim
+  f16x8 out;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float cs = cosT[pos * 16 + f0 + j];
+    const float sn = sinT[pos * 16 + f0 + j];
+    const float a = (float)x[j], b = (float)partner[j];
+    out[j] = lo ? (f16)(a * cs - b * sn) : (f16)(a * cs + b * sn);
+  }
+  return out;
+}
+
+__global__ void __launch_bounds__(kThreads) k_attn(AttnP p) {
+  __shared__ __attribute__((aligned(16))) f16 Ks[2][KT * D];
+  __shared__ __attribute__((aligned(16))) f16 Vs[2][KT * D];
+  __shared__ __attribute__((aligned(16))) f16 Ps[4][16 * KT];
+
+  const int qtile = blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / p.H, h = bh % p.H;
+  const int g = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const f16* __restrict__ Qg = p.Q[g];
+  const f16* __restrict__ Kg = p.K[g];
+  const f16* __restrict__ Vg = p.V[g];
+  const int64_t* __restrict__ qpos = p.qpos[g];
+  const int64_t* __restrict__ kpos = p.kpos[g];
+
+  // ---- Q fragments (A operand of 16x16x32): row = lane&15, dims chunk
+  // (4*ks + (lane>>4)) for ks = 0,1.
+  const int qrow = qtile * QT + wave * 16 + (lane & 15);
+  const bool qok = qrow < p.Nq;
+  f16x8 qf[2];
+  {
+    const f16* qp = Qg + ((int64_t)b * p.Nq + (qok ? qrow : 0)) * p.qs + h * D;
+    int64_t py = 0, px = 0;
+    if (qpos) {
+      py = qpos[((int64_t)b * p.Nq + (qok ? qrow : 0)) * 2 + 0];
+      px = qpos[((int64_t)b * p.Nq + (qok ? qrow : 0)) * 2 + 1];
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = 4 * ks + (lane >> 4);
+      f16x8 x = *reinterpret_cast<const f16x8*>(qp + c * 8);
+      if (qpos) {
+        const f16x8 y = *reinterpret_cast<const f16x8*>(qp + (c ^ 2) * 8);
+        x = rope_chunk(x, y, c, py, px, p.cosT, p.sinT);
+      }
+      if (!qok) x = f16x8{};
+      qf[ks] = x;
+    }
+  }
+
+  // ---- staging assignment: K: one (row, chunk pair) per lane; V: 2 chunks
+  const int k_row = tid >> 2;              // 0..63
+  const int k_pair = tid & 3;              // pairs (0,2) (1,3) (4,6) (5,7)
+  const int k_c0 = (k_pair & 1) + (k_pair >> 1) * 4;
+  const int k_c1 = k_c0 ^ 2;
+  f16x8 rk0, rk1, rv0, rv1;
+  const int v_row0 = tid >> 3, v_c0 = tid & 7;   // chunk tid and tid+256
+  auto gload = [&](int t) {
+    const int key = t * KT + k_row;
+    const bool ok = key < p.Nk;
+    const f16* kp = Kg + ((int64_t)b * p.Nk + (ok ? key : 0)) * p.ks + h * D;
+    f16x8 a = *reinterpret_cast<const f16x8*>(kp + k_c0 * 8);
+    f16x8 c = *reinterpret_cast<const f16x8*>(kp + k_c1 * 8);
+    if (kpos) {
+      const int64_t py = kpos[((int64_t)b * p.Nk + (ok ? key : 0)) * 2 + 0];
+      const int64_t px = kpos[((int64_t)b * p.Nk + (ok ? key : 0)) * 2 + 1];
+      rk0 = rope_chunk(a, c, k_c0, py, px, p.cosT, p.sinT);
+      rk1 = rope_chunk(c, a, k_c1, py, px, p.cosT, p.sinT);
+    } else {
+      rk0 = a;
+      rk1 = c;
+    }
+    if (!ok) { rk0 = f16x8{}; rk1 = f16x8{}; }
+    const int key0 = t * KT + v_row0, key1 = key0 + 32;
+    rv0 = key0 < p.Nk ? *reinterpret_cast<const f16x8*>(Vg + ((int64_t)b * p.Nk + key0) * p.vs + h * D + v_c0 * 8) : f16x8{};
+    rv1 = key1 < p.Nk ? *reinterpret_cast<const f16x8*>(Vg + ((int64_t)b * p.Nk + key1) * p.vs + h * D + v_c0 * 8) : f16x8{};
+  };
+  auto sstore = [&](int buf) {
+    *reinterpret_cast<f16x8*>(&Ks[buf][k_row * D + kswz(k_row, k_c0) * 8]) = rk0;
+    *reinterpret_cast<f16x8*>(&Ks[buf][k_row * D + kswz(k_row, k_c1) * 8]) = rk1;
+    *reinterpret_cast<f16x8*>(&Vs[buf][v_row0 * D + v_c0 * 8]) = rv0;
+    *reinterpret_cast<f16x8*>(&Vs[buf][(v_row0 + 32) * D + v_c0 * 8]) = rv1;
+  };
+
+  // running state for the 4 rows this lane touches: rows 4*(lane>>4) + r
+  float m_run[4], l_run[4];
+  f32x4 o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { m_run[r] = -INFINITY; l_run[r] = 0.f; }
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) o[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int NT = (p.Nk + KT - 1) / KT;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  f16* Pw = Ps[wave];
+  for (int t = 0; t < NT; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < NT) gload(t + 1);
+    // S = Q K^T for 4 blocks of 16 keys
+    f32x4 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int krow = kb * 16 + (lane & 15);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = 4 * ks + (lane >> 4);
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(&Ks[cur][krow * D + kswz(krow, c) * 8]);
+        s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[ks], kf, s[kb], 0, 0, 0);
+      }
+    }
+    // mask keys beyond Nk (lane holds key kb*16 + (lane&15))
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const bool kok = t * KT + kb * 16 + (lane & 15) < p.Nk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[kb][r] = kok ? s[kb][r] * p.scale_log2 : -INFINITY;
+    }
+    // online softmax per row (16 lanes with equal lane>>4 share a row)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = fmaxf(fmaxf(s[0][r], s[1][r]), fmaxf(s[2][r], s[3][r]));
+#pragma unroll
+      for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
+      const float m_new = fmaxf(m_run[r], mx);
+      const float alpha = exp2f(m_run[r] - m_new);
+      m_run[r] = m_new;
+      l_run[r] *= alpha;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) o[nb][r] *= alpha;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float e = exp2f(s[kb][r] - m_new);
+        s[kb][r] = e;
+        l_run[r] += e;
+      }
+    }
+    // P -> per-wave LDS scratch as [q row 16][key 64] (A-operand layout)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qr = 4 * (lane >> 4) + r;
+        Pw[qr * KT + kb * 16 + (lane & 15)] = (f16)s[kb][r];
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed
+    __builtin_amdgcn_wave_barrier();
+    // O += P V
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const f16x8 pa = *reinterpret_cast<const f16x8*>(&Pw[(lane & 15) * KT + ks * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        // B operand: V[key = 32ks + 8(lane>>4) + j][d = 16nb + (lane&15)]
+        // via two transpose reads of 4 rows x 16 cols (lane 4q+p supplies
+        // row q, cols 4p..4p+3 of its 16-lane group's block).
+        const int grp = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+        const int key0 = ks * 32 + 8 * grp + q4;
+        const int dcol = nb * 16 + 4 * p4;
+        typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_i16x4*)(&Vs[cur][key0 * D + dcol]));
+        const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_i16x4*)(&Vs[cur][(key0 + 4) * D + dcol]));
+        f16x8 vb;
+        const f16x4 lo16 = __builtin_bit_cast(f16x4, lo);
+        const f16x4 hi16 = __builtin_bit_cast(f16x4, hi);
+        vb[0] = lo16[0]; vb[1] = lo16[1]; vb[2] = lo16[2]; vb[3] = lo16[3];
+        vb[4] = hi16[0]; vb[5] = hi16[1]; vb[6] = hi16[2]; vb[7] = hi16[3];
+        o[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa, vb, o[nb], 0, 0, 0);
+      }
+    }
+    if (t + 1 < NT) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  // finalize: reduce row sums across the 16 lanes, normalise, store fp16
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float l = l_run[r];
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) l += __shfl_xor(l, o2, 64);
+    l_run[r] = 1.0f / l;
+  }
+  f16* Og = p.O[g];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = qtile * QT + wave * 16 + 4 * (lane >> 4) + r;
+    if (row >= p.Nq) continue;
+    f16* op = Og + ((int64_t)b * p.Nq + row) * p.os + h * D;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) op[nb * 16 + (lane & 15)] = (f16)(o[nb][r] * l_run[r]);
+  }
+}
+
+}  // namespace
+
+extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
+  S3_REQUIRE(a && a->B > 0 && a->Nq >= 0 && a->Nk > 0 && a->H > 0, "s3n_attention: bad sizes");
+  S3_REQUIRE(a->groups >= 1 && a->groups <= S3N_MAX_GROUPS, "s3n_attention: groups 1..4");
+  S3_REQUIRE(a->q_stride % 8 == 0 && a->k_stride % 8 == 0 && a->v_stride % 8 == 0,
+             "s3n_attention: row strides must be multiples of 8 elements");
+  if (a->Nq == 0) return S3_OK;
+  AttnP p;
+  p.B = a->B; p.Nq = a->Nq; p.Nk = a->Nk; p.H = a->H; p.groups = a->groups;
+  for (int g = 0; g < S3N_MAX_GROUPS; ++g) {
+    const bool on = g < a->groups;
+    p.Q[g] = on ? (const f16*)a->Q[g] : nullptr;
+    p.K[g] = on ? (const f16*)a->K[g] : nullptr;
+    p.V[g] = on ? (const f16*)a->V[g] : nullptr;
+    p.qpos[g] = on ? a->qpos[g] : nullptr;
+    p.kpos[g] = on ? a->kpos[g] : nullptr;
+    p.O[g] = on ? (f16*)a->O[g] : nullptr;
+    if (on) S3_REQUIRE(p.Q[g] && p.K[g] && p.V[g] && p.O[g], "s3n_attention: null operand");
+    if (on && (p.qpos[g] || p.kpos[g]))
+      S3_REQUIRE(a->rope_cos && a->rope_sin, "s3n_attention: RoPE tables missing");
+  }
+  p.qs = a->q_stride; p.ks = a->k_stride; p.vs = a->v_stride; p.os = a->o_stride;
+  p.cosT = a->rope_cos; p.sinT = a->rope_sin; p.maxpos = a->rope_maxpos;
+  p.scale_log2 = a->scale * 1.4426950408889634f;
+  dim3 grid((a->Nq + QT - 1) / QT, a->B * a->H, a->groups);
+  k_attn<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}

@@ -1,0 +1,244 @@
+"""Thin Python plans over the network entry points of include/s3n.h.
+
+Every op is built once into a ctypes argument struct (`Call`) and then run
+many times; the model composes these into a `Plan` (a list of prebuilt
+calls over static buffers) that is replayed per frame, optionally captured
+into a HIP graph.  No op has a torch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+from splatt3r_amd import _lib
+
+P = ctypes.c_void_p
+G = 4  # S3N_MAX_GROUPS
+I64 = ctypes.c_int64
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int), ("groups", ctypes.c_int),
+        ("A", P * G), ("lda", I64),
+        ("B", P * G), ("ldb", I64),
+        ("bias", P * G),
+        ("R1", P * G), ("ldr1", I64), ("r1_f16", ctypes.c_int),
+        ("R2", P * G), ("ldr2", I64), ("r2_f16", ctypes.c_int),
+        ("C", P * G), ("ldc", I64), ("c_f16", ctypes.c_int),
+        ("C2", P * G), ("ldc2", I64),
+        ("act", ctypes.c_int), ("store_mode", ctypes.c_int), ("a_mode", ctypes.c_int),
+        ("cH", ctypes.c_int), ("cW", ctypes.c_int), ("cC", ctypes.c_int), ("ksize", ctypes.c_int),
+        ("stride", ctypes.c_int), ("pad", ctypes.c_int), ("oH", ctypes.c_int), ("oW", ctypes.c_int),
+        ("relu_in", ctypes.c_int),
+        ("sH", ctypes.c_int), ("sW", ctypes.c_int), ("sS", ctypes.c_int), ("sCout", ctypes.c_int),
+    ]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("Nq", ctypes.c_int), ("Nk", ctypes.c_int), ("H", ctypes.c_int),
+        ("groups", ctypes.c_int),
+        ("Q", P * G), ("K", P * G), ("V", P * G),
+        ("q_stride", I64), ("k_stride", I64), ("v_stride", I64),
+        ("qpos", P * G), ("kpos", P * G),
+        ("rope_cos", P), ("rope_sin", P), ("rope_maxpos", ctypes.c_int),
+        ("O", P * G), ("o_stride", I64),
+        ("scale", ctypes.c_float),
+    ]
+
+
+_GP = ctypes.POINTER(GemmArgs)
+_AP = ctypes.POINTER(AttnArgs)
+_PP = ctypes.POINTER(P)
+_lib.register({
+    "s3n_gemm": (ctypes.c_int, [_GP, P]),
+    "s3n_attention": (ctypes.c_int, [_AP, P]),
+    "s3n_layernorm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _PP, I64, _PP, _PP,
+                                     ctypes.c_float, _PP, I64, _PP, I64, P]),
+    "s3n_patch_im2col": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        P, P]),
+    "s3n_upsample2x": (ctypes.c_int, [ctypes.c_int, _PP, _PP, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, P]),
+    "s3n_gaussian_postprocess": (ctypes.c_int, [I64, P, ctypes.c_int, P, P, ctypes.c_int,
+                                                ctypes.c_int] + [P] * 10 + [P]),
+    "s3n_prng_fill": (ctypes.c_int, [P, I64, ctypes.c_uint64, ctypes.c_float, ctypes.c_float, P]),
+    "s3n_cast_f16": (ctypes.c_int, [P, P, I64, P]),
+})
+
+ACT = {"none": 0, "gelu": 1, "relu": 2}
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+def _parr(items: Sequence, n=G):
+    arr = (P * n)()
+    for i, t in enumerate(items):
+        arr[i] = _ptr(t)
+    return arr
+
+
+class Call:
+    """A prebuilt library call: fn(*args) with status check."""
+    __slots__ = ("fn", "args", "name", "keep")
+
+    def __init__(self, name, *args, keep=()):
+        self.name = name
+        self.fn = getattr(_lib.lib(), name)
+        self.args = args
+        self.keep = keep  # objects that must outlive the call (ctypes arrays, structs)
+
+    def __call__(self, stream):
+        st = self.fn(*self.args, stream)
+        if st != 0:
+            _lib.check(st, self.name)
+
+
+def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1=None,
+         ldr1=0, R2=None, ldr2=0, C2=None, ldc2=0, conv=None, store=None) -> Call:
+    """Grouped GEMM: A, B, C, bias, R1, R2, C2 are lists (one entry per group)
+    of tensors / raw pointers.  conv = dict(H, W, C, k, stride, pad, oH, oW,
+    relu_in) switches A to implicit im2col of an NHWC image.  store =
+    ("convt"|"pixshuf", sH, sW, s, Cout)."""
+    a = GemmArgs()
+    groups = len(A)
+    a.M, a.N, a.K, a.groups = int(M), int(N), int(K), groups
+    a.A = _parr(A)
+    a.B = _parr(B)
+    a.C = _parr(C)
+    a.lda = int(lda)
+    a.ldb = int(ldb if ldb is not None else K)
+    a.ldc = int(ldc if ldc is not None else N)
+    a.bias = _parr(bias or [])
+    a.act = ACT[act]
+
+    def dtype_f16(x):
+        return isinstance(x, torch.Tensor) and x.dtype == torch.float16
+
+    if R1 is not None:
+        a.R1 = _parr(R1)
+        a.ldr1 = int(ldr1)
+        a.r1_f16 = int(dtype_f16(R1[0]))
+    if R2 is not None:
+        a.R2 = _parr(R2)
+        a.ldr2 = int(ldr2)
+        a.r2_f16 = int(dtype_f16(R2[0]))
+    a.c_f16 = int(dtype_f16(C[0]))
+    if C2 is not None:
+        a.C2 = _parr(C2)
+        a.ldc2 = int(ldc2)
+    if conv is not None:
+        a.a_mode = 1
+        a.cH, a.cW, a.cC = conv["H"], conv["W"], conv["C"]
+        a.ksize, a.stride, a.pad = conv["k"], conv["stride"], conv["pad"]
+        a.oH, a.oW = conv["oH"], conv["oW"]
+        a.relu_in = int(conv.get("relu_in", False))
+    if store is not None:
+        mode, sH, sW, s, cout = store
+        a.store_mode = {"convt": 1, "pixshuf": 2}[mode]
+        a.sH, a.sW, a.sS, a.sCout = sH, sW, s, cout
+    return Call("s3n_gemm", ctypes.byref(a), keep=(a,))
+
+
+def attention(Q, K, V, O, *, B, Nq, Nk, H, q_stride, k_stride, v_stride, o_stride, qpos=None,
+              kpos=None, rope=None, scale=0.125) -> Call:
+    a = AttnArgs()
+    a.B, a.Nq, a.Nk, a.H, a.groups = B, Nq, Nk, H, len(Q)
+    a.Q, a.K, a.V, a.O = _parr(Q), _parr(K), _parr(V), _parr(O)
+    a.q_stride, a.k_stride, a.v_stride, a.o_stride = q_stride, k_stride, v_stride, o_stride
+    if qpos is not None:
+        a.qpos = _parr(qpos)
+    if kpos is not None:
+        a.kpos = _parr(kpos)
+    if rope is not None:
+        a.rope_cos, a.rope_sin = rope[0].data_ptr(), rope[1].data_ptr()
+        a.rope_maxpos = rope[0].shape[0]
+    a.scale = scale
+    return Call("s3n_attention", ctypes.byref(a), keep=(a,))
+
+
+def layernorm(x, gamma, beta, *, rows, C, ldx, eps=1e-6, out16=None, ld16=0, out32=None,
+              ld32=0) -> Call:
+    xs, gs, bs = _parr(x), _parr(gamma), _parr(beta)
+    o16 = _parr(out16) if out16 is not None else None
+    o32 = _parr(out32) if out32 is not None else None
+    return Call("s3n_layernorm", rows, C, len(x), ctypes.cast(xs, _PP), ldx,
+                ctypes.cast(gs, _PP), ctypes.cast(bs, _PP), ctypes.c_float(eps),
+                ctypes.cast(o16, _PP) if o16 is not None else None, ld16,
+                ctypes.cast(o32, _PP) if o32 is not None else None, ld32,
+                keep=(xs, gs, bs, o16, o32))
+
+
+def upsample2x(inp, out, *, B, H, W, C) -> Call:
+    i, o = _parr(inp), _parr(out)
+    return Call("s3n_upsample2x", len(inp), ctypes.cast(i, _PP), ctypes.cast(o, _PP), B, H, W, C,
+                keep=(i, o))
+
+
+def patch_im2col(img, A, *, B, H, W, p) -> Call:
+    return Call("s3n_patch_im2col", _ptr(img), B, H, W, p, _ptr(A))
+
+
+def gaussian_postprocess(n, pts, ld_pts, feat, gauss, ld_g, use_offsets, out: dict,
+                         desc16=None) -> Call:
+    return Call("s3n_gaussian_postprocess", n, _ptr(pts), ld_pts, _ptr(feat), _ptr(gauss), ld_g,
+                int(use_offsets), _ptr(out["pts3d"]), _ptr(out["conf"]), _ptr(out["desc"]),
+                _ptr(desc16), _ptr(out["desc_conf"]), _ptr(out["scales"]),
+                _ptr(out["rotations"]), _ptr(out["sh"]), _ptr(out["opacities"]),
+                _ptr(out["means"]))
+
+
+def prng_fill(out: torch.Tensor, seed: int, a: float, c: float) -> None:
+    _lib.call("s3n_prng_fill", out.data_ptr(), out.numel(), ctypes.c_uint64(seed & (2**64 - 1)),
+              ctypes.c_float(a), ctypes.c_float(c), _lib.stream(out.device))
+
+
+def cast_f16(x: torch.Tensor, out: torch.Tensor) -> None:
+    _lib.call("s3n_cast_f16", x.data_ptr(), out.data_ptr(), x.numel(), _lib.stream(x.device))
+
+
+class Plan:
+    """An ordered list of prebuilt calls over static buffers."""
+
+    def __init__(self):
+        self.calls: list[Call] = []
+        self.graph = None
+
+    def add(self, c: Call):
+        self.calls.append(c)
+        return c
+
+    def extend(self, other: "Plan"):
+        self.calls.extend(other.calls)
+
+    def run(self, stream=None):
+        st = stream if stream is not None else _lib.stream()
+        for c in self.calls:
+            c(st)
+
+    def capture(self):
+        """Capture the plan into a HIP graph (torch.cuda.CUDAGraph)."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.run()  # warm-up outside capture (module load, lazy init)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.run()
+        self.graph = g
+        return g
+
+    def replay(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.run()
