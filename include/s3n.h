@@ -113,9 +113,11 @@ int s3n_layernorm(int rows, int C, int groups, const float* const* x, int64_t ld
 int s3n_patch_im2col(const float* img, int B, int H, int W, int p, void* A, void* stream);
 
 /* Bilinear x2 upsample, align_corners=True (dpt_block.py:207-212,
- * Interpolate :262-270), NHWC fp16 -> NHWC fp16, per group. */
+ * Interpolate :262-270), NHWC fp16 -> NHWC fp16, per group.  The output
+ * grid is the top-left crop [oh, ow] (oh <= 2H, ow <= 2W) of the 2H x 2W
+ * result (refinenet4 crop, dpt_head.py:56). */
 int s3n_upsample2x(int groups, const void* const* in, void* const* out, int B, int H, int W,
-                   int C, void* stream);
+                   int C, int oh, int ow, void* stream);
 
 /* gaussian_postprocess (catmlp_dpt_head.py:140-178) + the 43-channel
  * concatenation of GaussianHead.forward (:245-278) for one view:
@@ -134,8 +136,10 @@ int s3n_gaussian_postprocess(int64_t n, const float* pts, int ld_pts, const floa
  * u = (splitmix64(seed + (i+1)*0x9E3779B97F4A7C15) >> 40) * 2^-24, fp32. */
 int s3n_prng_fill(float* out, int64_t n, uint64_t seed, float a, float c, void* stream);
 
-/* fp32 -> fp16 conversion (round to nearest even), n elements. */
-int s3n_cast_f16(const float* in, void* out, int64_t n, void* stream);
+/* fp32 -> fp16 conversion (round to nearest even) of a rows x cols block
+ * with row strides ld_in / ld_out (elements). */
+int s3n_cast_f16(const float* in, int64_t ld_in, void* out, int64_t ld_out, int64_t rows,
+                 int cols, void* stream);
 
 #ifdef __cplusplus
 }

@@ -100,21 +100,21 @@ k_patch_im2col(const float* __restrict__ img, int B, int H, int W, int p, f16* _
 struct UpP {
   const f16* in[S3N_MAX_GROUPS];
   f16* out[S3N_MAX_GROUPS];
-  int B, H, W, C;
+  int B, H, W, C, oh, ow;
 };
 
 __global__ void __launch_bounds__(kThreads) k_upsample2x(UpP p) {
   const int g = blockIdx.y;
   const int OH = 2 * p.H, OW = 2 * p.W, C8 = p.C / 8;
-  const int64_t total = (int64_t)p.B * OH * OW * C8;
+  const int64_t total = (int64_t)p.B * p.oh * p.ow * C8;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c8 = (int)(i % C8);
   int64_t t = i / C8;
-  const int ox = (int)(t % OW);
-  t /= OW;
-  const int oy = (int)(t % OH);
-  const int b = (int)(t / OH);
+  const int ox = (int)(t % p.ow);
+  t /= p.ow;
+  const int oy = (int)(t % p.oh);
+  const int b = (int)(t / p.oh);
   const float sh = OH > 1 ? (float)(p.H - 1) / (float)(OH - 1) : 0.f;
   const float sw = OW > 1 ? (float)(p.W - 1) / (float)(OW - 1) : 0.f;
   const float fy = sh * oy, fx = sw * ox;
@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(kThreads) k_upsample2x(UpP p) {
 #pragma unroll
   for (int j = 0; j < 8; ++j)
     o[j] = (f16)(hy * (hx * (float)a[j] + lx * (float)bq[j]) + ly * (hx * (float)cq[j] + lx * (float)d[j]));
-  *reinterpret_cast<f16x8*>(p.out[g] + (((int64_t)b * OH + oy) * OW + ox) * p.C + c8 * 8) = o;
+  *reinterpret_cast<f16x8*>(p.out[g] + (((int64_t)b * p.oh + oy) * p.ow + ox) * p.C + c8 * 8) = o;
 }
 
 // ------------------------------------------------------ postprocess -------
@@ -204,9 +204,12 @@ k_prng(float* __restrict__ out, int64_t n, uint64_t seed, float a, float c) {
 }
 
 __global__ void __launch_bounds__(kThreads)
-k_cast(const float* __restrict__ in, f16* __restrict__ out, int64_t n) {
+k_cast(const float* __restrict__ in, int64_t ldi, f16* __restrict__ out, int64_t ldo,
+       int64_t rows, int cols) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (f16)in[i];
+  if (i >= rows * cols) return;
+  const int64_t r = i / cols, c = i % cols;
+  out[r * ldo + c] = (f16)in[r * ldi + c];
 }
 
 }  // namespace
@@ -253,16 +256,17 @@ int s3n_patch_im2col(const float* img, int B, int H, int W, int p, void* A, void
 }
 
 int s3n_upsample2x(int groups, const void* const* in, void* const* out, int B, int H, int W,
-                   int C, void* stream) {
+                   int C, int oh, int ow, void* stream) {
   S3_REQUIRE(groups >= 1 && groups <= S3N_MAX_GROUPS && B > 0 && H > 0 && W > 0 && C % 8 == 0,
              "s3n_upsample2x: bad sizes");
+  S3_REQUIRE(oh > 0 && ow > 0 && oh <= 2 * H && ow <= 2 * W, "s3n_upsample2x: bad crop");
   UpP p;
-  p.B = B; p.H = H; p.W = W; p.C = C;
+  p.B = B; p.H = H; p.W = W; p.C = C; p.oh = oh; p.ow = ow;
   for (int g = 0; g < S3N_MAX_GROUPS; ++g) {
     p.in[g] = g < groups ? (const f16*)in[g] : nullptr;
     p.out[g] = g < groups ? (f16*)out[g] : nullptr;
   }
-  const int64_t total = (int64_t)B * 4 * H * W * (C / 8);
+  const int64_t total = (int64_t)B * oh * ow * (C / 8);
   dim3 grid((unsigned)s3::cdiv(total, kThreads), (unsigned)groups);
   k_upsample2x<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
   S3_LAUNCH_CHECK();
@@ -291,10 +295,13 @@ int s3n_prng_fill(float* out, int64_t n, uint64_t seed, float a, float c, void* 
   return S3_OK;
 }
 
-int s3n_cast_f16(const float* in, void* out, int64_t n, void* stream) {
-  S3_REQUIRE(n >= 0, "s3n_cast_f16: n < 0");
+int s3n_cast_f16(const float* in, int64_t ld_in, void* out, int64_t ld_out, int64_t rows,
+                 int cols, void* stream) {
+  S3_REQUIRE(rows >= 0 && cols >= 0, "s3n_cast_f16: bad sizes");
+  const int64_t n = rows * cols;
   if (n == 0) return S3_OK;
-  k_cast<<<(unsigned)s3::cdiv(n, kThreads), kThreads, 0, s3::as_stream(stream)>>>(in, (f16*)out, n);
+  k_cast<<<(unsigned)s3::cdiv(n, kThreads), kThreads, 0, s3::as_stream(stream)>>>(
+      in, ld_in, (f16*)out, ld_out, rows, cols);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

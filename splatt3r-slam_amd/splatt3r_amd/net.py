@@ -1,0 +1,563 @@
+"""MASt3RGaussians inference on the HIP kernels of include/s3n.h.
+
+Reference structure (all citations under splatt3r_core/src/mast3r_src/):
+  encoder   dust3r/dust3r/model.py:121-136  (_encode_image: ManyAR_PatchEmbed
+            patch_embed.py:42-70 -> 24 x Block blocks.py:114-130 -> enc_norm)
+  decoder   dust3r/dust3r/model.py:168-187  (_decoder: decoder_embed -> 12 x
+            (DecoderBlock blocks.py:171-191 for each branch) -> dec_norm)
+  heads     dust3r/dust3r/model.py:189-193 -> mast3r/catmlp_dpt_head.py:245-278
+            (GaussianHead: DPT dust3r/heads/dpt_head.py:34-65 +
+            croco/models/dpt_block.py, MLP + pixel_shuffle, Gaussian DPT,
+            gaussian_postprocess :140-178)
+
+MI355X-first execution:
+  * every matrix product is the grouped fp16 MFMA GEMM (fp32 accumulate):
+    the two decoder branches run as one grouped launch per op (2 groups),
+    the two heads' MLPs as 2 groups and the four DPTs (head1/head2 x
+    pts/gaussian) as 4 groups;
+  * convolutions are implicit GEMMs on NHWC fp16 activations; ReLU before a
+    conv is applied on the operand load, bias / ReLU / GELU / residual adds
+    are GEMM epilogues; ConvTranspose(k=s) and pixel_shuffle are scatter
+    epilogues;
+  * FeatureFusionBlock's 1x1 out_conv runs before the x2 bilinear
+    upsample (both are linear and the align_corners interpolation weights
+    sum to 1, so conv1x1(up(x)) == up(conv1x1(x)) up to rounding) at a
+    quarter of the FLOPs;
+  * RoPE is applied inside the attention kernel;
+  * each forward is a prebuilt Plan (list of ctypes calls over static
+    buffers) that can be captured into a HIP graph.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from splatt3r_amd import ops
+from splatt3r_amd.weights import FULL, NetConfig, check_state_dict, prng_state_dict
+
+F16 = torch.float16
+F32 = torch.float32
+
+
+def rope_tables(maxpos: int, device, base: float = 100.0):
+    """cos/sin [maxpos, 16] exactly as RoPE2D.get_cos_sin computes them
+    (croco/models/pos_embed.py:119-129) for D = head_dim/2 = 32."""
+    D = 32
+    inv_freq = 1.0 / (base ** (torch.arange(0, D, 2).float().to(device) / D))
+    t = torch.arange(maxpos, device=device, dtype=inv_freq.dtype)
+    freqs = torch.einsum("i,j->ij", t, inv_freq).to(F32)
+    return freqs.cos().contiguous(), freqs.sin().contiguous()
+
+
+def positions(B: int, ht: int, wt: int, device):
+    """PositionGetter (croco/models/blocks.py:193-205): (y, x) per token."""
+    y = torch.arange(ht, device=device)
+    x = torch.arange(wt, device=device)
+    pos = torch.cartesian_prod(y, x).view(1, ht * wt, 2).expand(B, -1, 2).contiguous()
+    return pos.to(torch.int64)
+
+
+class PackedWeights:
+    """state_dict repacked into kernel layouts (fp16 matrices [N, K],
+    fp32 biases / norms), stacked per group where ops are grouped."""
+
+    def __init__(self, cfg: NetConfig, sd: dict, device):
+        self.cfg = cfg
+        E, D = cfg.enc_dim, cfg.dec_dim
+        f16 = lambda t: t.to(device=device, dtype=F16).contiguous()
+        f32 = lambda t: t.to(device=device, dtype=F32).contiguous()
+        lin = lambda name: f16(sd[name])
+        conv = lambda name: f16(sd[name].permute(0, 2, 3, 1).reshape(sd[name].shape[0], -1))
+        self.pe_w = f16(sd["patch_embed.proj.weight"].reshape(E, -1))
+        self.pe_b = f32(sd["patch_embed.proj.bias"])
+        self.enc = []
+        for i in range(cfg.enc_depth):
+            p = f"enc_blocks.{i}."
+            self.enc.append(dict(
+                n1w=f32(sd[p + "norm1.weight"]), n1b=f32(sd[p + "norm1.bias"]),
+                qkv_w=lin(p + "attn.qkv.weight"), qkv_b=f32(sd[p + "attn.qkv.bias"]),
+                proj_w=lin(p + "attn.proj.weight"), proj_b=f32(sd[p + "attn.proj.bias"]),
+                n2w=f32(sd[p + "norm2.weight"]), n2b=f32(sd[p + "norm2.bias"]),
+                fc1_w=lin(p + "mlp.fc1.weight"), fc1_b=f32(sd[p + "mlp.fc1.bias"]),
+                fc2_w=lin(p + "mlp.fc2.weight"), fc2_b=f32(sd[p + "mlp.fc2.bias"])))
+        self.enc_nw, self.enc_nb = f32(sd["enc_norm.weight"]), f32(sd["enc_norm.bias"])
+        self.emb_w, self.emb_b = lin("decoder_embed.weight"), f32(sd["decoder_embed.bias"])
+        self.dec = []
+        st = lambda key, fn: torch.stack([fn(f"dec_blocks.{i}." + key), fn(f"dec_blocks2.{i}." + key)])
+        for i in range(cfg.dec_depth):
+            L = lambda n: lin(n)
+            V = lambda n: f32(sd[n])
+            kv = lambda b: torch.cat([sd[f"{b}.{i}.cross_attn.projk.weight"],
+                                      sd[f"{b}.{i}.cross_attn.projv.weight"]], 0)
+            kvb = lambda b: torch.cat([sd[f"{b}.{i}.cross_attn.projk.bias"],
+                                       sd[f"{b}.{i}.cross_attn.projv.bias"]], 0)
+            self.dec.append(dict(
+                n1w=st("norm1.weight", V), n1b=st("norm1.bias", V),
+                qkv_w=st("attn.qkv.weight", L), qkv_b=st("attn.qkv.bias", V),
+                proj_w=st("attn.proj.weight", L), proj_b=st("attn.proj.bias", V),
+                nyw=st("norm_y.weight", V), nyb=st("norm_y.bias", V),
+                n2w=st("norm2.weight", V), n2b=st("norm2.bias", V),
+                q_w=st("cross_attn.projq.weight", L), q_b=st("cross_attn.projq.bias", V),
+                kv_w=torch.stack([f16(kv("dec_blocks")), f16(kv("dec_blocks2"))]),
+                kv_b=torch.stack([f32(kvb("dec_blocks")), f32(kvb("dec_blocks2"))]),
+                cp_w=st("cross_attn.proj.weight", L), cp_b=st("cross_attn.proj.bias", V),
+                n3w=st("norm3.weight", V), n3b=st("norm3.bias", V),
+                fc1_w=st("mlp.fc1.weight", L), fc1_b=st("mlp.fc1.bias", V),
+                fc2_w=st("mlp.fc2.weight", L), fc2_b=st("mlp.fc2.bias", V)))
+        self.dec_nw, self.dec_nb = f32(sd["dec_norm.weight"]), f32(sd["dec_norm.bias"])
+        # head MLPs: groups (head1, head2)
+        hp = ("downstream_head1", "downstream_head2")
+        self.mlp_fc1_w = torch.stack([lin(f"{h}.head_local_features.fc1.weight") for h in hp])
+        self.mlp_fc1_b = torch.stack([f32(sd[f"{h}.head_local_features.fc1.bias"]) for h in hp])
+        self.mlp_fc2_w = torch.stack([lin(f"{h}.head_local_features.fc2.weight") for h in hp])
+        self.mlp_fc2_b = torch.stack([f32(sd[f"{h}.head_local_features.fc2.bias"]) for h in hp])
+        # DPTs: groups (h1 pts, h1 gauss, h2 pts, h2 gauss)
+        dp = (f"{hp[0]}.dpt", f"{hp[0]}.gaussian_dpt.dpt", f"{hp[1]}.dpt", f"{hp[1]}.gaussian_dpt.dpt")
+        S = lambda fn: torch.stack([fn(d) for d in dp])
+        ap = lambda d, s: f"{d}.act_postprocess.{s}"
+
+        def convt(name, k):
+            w = sd[name]  # [Cin, Cout, k, k] -> [(i*k+j)*Cout + co, ci]
+            return f16(w.permute(2, 3, 1, 0).reshape(k * k * w.shape[1], w.shape[0]))
+
+        self.ap0a_w = S(lambda d: conv(ap(d, "0.0") + ".weight"))
+        self.ap0a_b = S(lambda d: f32(sd[ap(d, "0.0") + ".bias"]))
+        self.ap0b_w = S(lambda d: convt(ap(d, "0.1") + ".weight", 4))
+        self.ap0b_b = S(lambda d: f32(sd[ap(d, "0.1") + ".bias"].repeat(16)))
+        self.ap1a_w = S(lambda d: conv(ap(d, "1.0") + ".weight"))
+        self.ap1a_b = S(lambda d: f32(sd[ap(d, "1.0") + ".bias"]))
+        self.ap1b_w = S(lambda d: convt(ap(d, "1.1") + ".weight", 2))
+        self.ap1b_b = S(lambda d: f32(sd[ap(d, "1.1") + ".bias"].repeat(4)))
+        self.ap2_w = S(lambda d: conv(ap(d, "2.0") + ".weight"))
+        self.ap2_b = S(lambda d: f32(sd[ap(d, "2.0") + ".bias"]))
+        self.ap3a_w = S(lambda d: conv(ap(d, "3.0") + ".weight"))
+        self.ap3a_b = S(lambda d: f32(sd[ap(d, "3.0") + ".bias"]))
+        self.ap3b_w = S(lambda d: conv(ap(d, "3.1") + ".weight"))
+        self.ap3b_b = S(lambda d: f32(sd[ap(d, "3.1") + ".bias"]))
+        self.rn_w = [S(lambda d: conv(f"{d}.scratch.layer{i + 1}_rn.weight")) for i in range(4)]
+        self.ref = []
+        for r in (1, 2, 3, 4):
+            rp = lambda d, s: f"{d}.scratch.refinenet{r}.{s}"
+            blk = dict(out_w=S(lambda d: conv(rp(d, "out_conv.weight"))),
+                       out_b=S(lambda d: f32(sd[rp(d, "out_conv.bias")])))
+            for u in (1, 2):
+                for c in (1, 2):
+                    blk[f"u{u}c{c}_w"] = S(lambda d: conv(rp(d, f"resConfUnit{u}.conv{c}.weight")))
+                    blk[f"u{u}c{c}_b"] = S(lambda d: f32(sd[rp(d, f"resConfUnit{u}.conv{c}.bias")]))
+            self.ref.append(blk)
+        self.h0_w = S(lambda d: conv(f"{d}.head.0.weight"))
+        self.h0_b = S(lambda d: f32(sd[f"{d}.head.0.bias"]))
+        self.h2_w = S(lambda d: conv(f"{d}.head.2.weight"))
+        self.h2_b = S(lambda d: f32(sd[f"{d}.head.2.bias"]))
+        # final 1x1 conv padded to 16 output channels (4 pts+conf / 14 gaussian)
+        self.NOUT = 16
+        fin_w = torch.zeros(4, self.NOUT, cfg.feature_dim // 2, device=device, dtype=F16)
+        fin_b = torch.zeros(4, self.NOUT, device=device, dtype=F32)
+        for g, d in enumerate(dp):
+            w = sd[f"{d}.head.4.weight"]
+            fin_w[g, :w.shape[0]] = w.reshape(w.shape[0], -1).to(device=device, dtype=F16)
+            fin_b[g, :w.shape[0]] = sd[f"{d}.head.4.bias"].to(device=device, dtype=F32)
+        self.h4_w, self.h4_b = fin_w, fin_b
+
+
+def _g(t: torch.Tensor, n: int):
+    """Group views of a stacked tensor: [t[0], t[1], ...]."""
+    return [t[i] for i in range(n)]
+
+
+class EncoderPlan:
+    """_encode_image for a fixed (B, H, W): img [B,3,H,W] fp32 -> feat [B,N,E]
+    fp32 (+ fp16 copy with row stride ld16), pos [B,N,2]."""
+
+    def __init__(self, net: "Splatt3RNet", B: int, H: int, W: int):
+        cfg, w, dev = net.cfg, net.w, net.device
+        E, p = cfg.enc_dim, cfg.patch
+        ht, wt = H // p, W // p
+        N = ht * wt
+        M = B * N
+        self.B, self.H, self.W, self.N = B, H, W, N
+        self.img = torch.zeros(B, 3, H, W, device=dev, dtype=F32)
+        self.pos = positions(B, ht, wt, dev)
+        a_pe = torch.empty(M, 3 * p * p, device=dev, dtype=F16)
+        x = torch.empty(M, E, device=dev, dtype=F32)
+        h = torch.empty(M, E, device=dev, dtype=F16)
+        qkv = torch.empty(M, 3 * E, device=dev, dtype=F16)
+        ao = torch.empty(M, E, device=dev, dtype=F16)
+        hid = int(E * cfg.mlp_ratio)
+        u = torch.empty(M, hid, device=dev, dtype=F16)
+        self.feat = torch.empty(B, N, E, device=dev, dtype=F32)
+        self.feat16 = torch.empty(M, E, device=dev, dtype=F16)
+        self._bufs = (a_pe, x, h, qkv, ao, u)
+        P = ops.Plan()
+        P.add(ops.patch_im2col(self.img, a_pe, B=B, H=H, W=W, p=p))
+        P.add(ops.gemm([a_pe], [w.pe_w], [x], M, E, 3 * p * p, lda=3 * p * p, bias=[w.pe_b]))
+        H_ = cfg.enc_heads
+        for blk in w.enc:
+            P.add(ops.layernorm([x], [blk["n1w"]], [blk["n1b"]], rows=M, C=E, ldx=E, eps=cfg.ln_eps,
+                                out16=[h], ld16=E))
+            P.add(ops.gemm([h], [blk["qkv_w"]], [qkv], M, 3 * E, E, lda=E, bias=[blk["qkv_b"]]))
+            P.add(ops.attention([qkv], [qkv[:, E:]], [qkv[:, 2 * E:]], [ao], B=B, Nq=N, Nk=N, H=H_,
+                                q_stride=3 * E, k_stride=3 * E, v_stride=3 * E, o_stride=E,
+                                qpos=[self.pos], kpos=[self.pos], rope=net.rope,
+                                scale=(E // H_) ** -0.5))
+            P.add(ops.gemm([ao], [blk["proj_w"]], [x], M, E, E, lda=E, bias=[blk["proj_b"]],
+                           R1=[x], ldr1=E))
+            P.add(ops.layernorm([x], [blk["n2w"]], [blk["n2b"]], rows=M, C=E, ldx=E, eps=cfg.ln_eps,
+                                out16=[h], ld16=E))
+            P.add(ops.gemm([h], [blk["fc1_w"]], [u], M, hid, E, lda=E, bias=[blk["fc1_b"]], act="gelu"))
+            P.add(ops.gemm([u], [blk["fc2_w"]], [x], M, E, hid, lda=hid, bias=[blk["fc2_b"]],
+                           R1=[x], ldr1=E))
+        P.add(ops.layernorm([x], [w.enc_nw], [w.enc_nb], rows=M, C=E, ldx=E, eps=cfg.ln_eps,
+                            out16=[self.feat16], ld16=E, out32=[self.feat.view(M, E)], ld32=E))
+        self.plan = P
+
+    def __call__(self, img: torch.Tensor):
+        self.img.copy_(img)
+        self.plan.replay()
+        return self.feat, self.pos
+
+
+class PairPlan:
+    """_decoder + both _downstream_heads for Bp pairs of one image size.
+
+    Inputs (static): feat16 [2, Bp*N, E+D] (cols [0,E) hold the fp16
+    encoder features of branch 1 / 2), pos1/pos2 [Bp, N, 2], img1/img2
+    [Bp, 3, H, W] not needed (the SH residual is added at render time).
+    Outputs: res[0], res[1] dicts of [Bp, H, W, ...] fp32 tensors (keys of
+    gaussian_postprocess) + desc16 fp16 copies for matching.
+    """
+
+    KEYS = {"pts3d": 3, "conf": 0, "desc": 24, "desc_conf": 0, "scales": 3, "rotations": 4,
+            "sh": 3, "opacities": 1, "means": 3}
+
+    def __init__(self, net: "Splatt3RNet", Bp: int, H: int, W: int, keep_tokens=False):
+        cfg, w, dev = net.cfg, net.w, net.device
+        E, D, p = cfg.enc_dim, cfg.dec_dim, cfg.patch
+        ht, wt = H // p, W // p
+        N = ht * wt
+        M = Bp * N
+        ED = E + D
+        self.Bp, self.H, self.W, self.N = Bp, H, W, N
+        self.cat = torch.zeros(2, M, ED, device=dev, dtype=F16)  # [enc16 | dec_norm16]
+        self.pos = torch.zeros(2, Bp, N, 2, device=dev, dtype=torch.int64)
+        X = torch.empty(2, M, D, device=dev, dtype=F32)
+        h = torch.empty(2, M, D, device=dev, dtype=F16)
+        yh = torch.empty(2, M, D, device=dev, dtype=F16)
+        qkv = torch.empty(2, M, 3 * D, device=dev, dtype=F16)
+        q = torch.empty(2, M, D, device=dev, dtype=F16)
+        kv = torch.empty(2, M, 2 * D, device=dev, dtype=F16)
+        ao = torch.empty(2, M, D, device=dev, dtype=F16)
+        hid = int(D * cfg.mlp_ratio)
+        u = torch.empty(2, M, hid, device=dev, dtype=F16)
+        hooks = cfg.hooks
+        self.hook16 = {k: torch.empty(2, M, D, device=dev, dtype=F16) for k in hooks[1:3]}
+        self.tokens = None
+        if keep_tokens:  # fp32 copies of all 13 decoder outputs (API path)
+            self.tokens = torch.empty(cfg.dec_depth + 1, 2, M, D, device=dev, dtype=F32)
+        self._bufs = [X, h, yh, qkv, q, kv, ao, u]
+        P = ops.Plan()
+        g2 = lambda t: _g(t, 2)
+        Hd = cfg.dec_heads
+        sc = (D // Hd) ** -0.5
+        pos = [self.pos[0], self.pos[1]]
+        # decoder_embed (both branches, shared weights)
+        P.add(ops.gemm(g2(self.cat), [w.emb_w, w.emb_w], g2(X), M, D, E, lda=ED,
+                       bias=[w.emb_b, w.emb_b]))
+        for li, blk in enumerate(w.dec):
+            # y_ = norm_y(other branch's previous output), before X changes
+            P.add(ops.layernorm([X[1], X[0]], g2(blk["nyw"]), g2(blk["nyb"]), rows=M, C=D, ldx=D,
+                                eps=cfg.ln_eps, out16=g2(yh), ld16=D))
+            # self attention
+            P.add(ops.layernorm(g2(X), g2(blk["n1w"]), g2(blk["n1b"]), rows=M, C=D, ldx=D,
+                                eps=cfg.ln_eps, out16=g2(h), ld16=D))
+            P.add(ops.gemm(g2(h), g2(blk["qkv_w"]), g2(qkv), M, 3 * D, D, lda=D, bias=g2(blk["qkv_b"])))
+            P.add(ops.attention(g2(qkv), [qkv[0][:, D:], qkv[1][:, D:]],
+                                [qkv[0][:, 2 * D:], qkv[1][:, 2 * D:]], g2(ao), B=Bp, Nq=N, Nk=N, H=Hd,
+                                q_stride=3 * D, k_stride=3 * D, v_stride=3 * D, o_stride=D,
+                                qpos=pos, kpos=pos, rope=net.rope, scale=sc))
+            P.add(ops.gemm(g2(ao), g2(blk["proj_w"]), g2(X), M, D, D, lda=D, bias=g2(blk["proj_b"]),
+                           R1=g2(X), ldr1=D))
+            # cross attention: q from norm2(x), k/v from norm_y(y)
+            P.add(ops.layernorm(g2(X), g2(blk["n2w"]), g2(blk["n2b"]), rows=M, C=D, ldx=D,
+                                eps=cfg.ln_eps, out16=g2(h), ld16=D))
+            P.add(ops.gemm(g2(h), g2(blk["q_w"]), g2(q), M, D, D, lda=D, bias=g2(blk["q_b"])))
+            P.add(ops.gemm(g2(yh), g2(blk["kv_w"]), g2(kv), M, 2 * D, D, lda=D, bias=g2(blk["kv_b"])))
+            P.add(ops.attention(g2(q), g2(kv), [kv[0][:, D:], kv[1][:, D:]], g2(ao), B=Bp, Nq=N, Nk=N,
+                                H=Hd, q_stride=D, k_stride=2 * D, v_stride=2 * D, o_stride=D,
+                                qpos=pos, kpos=[pos[1], pos[0]], rope=net.rope, scale=sc))
+            P.add(ops.gemm(g2(ao), g2(blk["cp_w"]), g2(X), M, D, D, lda=D, bias=g2(blk["cp_b"]),
+                           R1=g2(X), ldr1=D))
+            # MLP (+ fp16 copy of the block output when it is a DPT hook)
+            P.add(ops.layernorm(g2(X), g2(blk["n3w"]), g2(blk["n3b"]), rows=M, C=D, ldx=D,
+                                eps=cfg.ln_eps, out16=g2(h), ld16=D))
+            P.add(ops.gemm(g2(h), g2(blk["fc1_w"]), g2(u), M, hid, D, lda=D, bias=g2(blk["fc1_b"]),
+                           act="gelu"))
+            hk = self.hook16.get(li + 1)
+            P.add(ops.gemm(g2(u), g2(blk["fc2_w"]), g2(X), M, D, hid, lda=hid, bias=g2(blk["fc2_b"]),
+                           R1=g2(X), ldr1=D, C2=g2(hk) if hk is not None else None, ldc2=D))
+            if self.tokens is not None and li + 1 < cfg.dec_depth:
+                tk = self.tokens[li + 1]
+                P.add(_Copy(tk, X))
+        # dec_norm -> cat[:, E:] (MLP input and DPT hook 3)
+        P.add(ops.layernorm(g2(X), [w.dec_nw, w.dec_nw], [w.dec_nb, w.dec_nb], rows=M, C=D, ldx=D,
+                            eps=cfg.ln_eps, out16=[self.cat[0][:, E:], self.cat[1][:, E:]], ld16=ED,
+                            out32=g2(self.tokens[cfg.dec_depth]) if self.tokens is not None else None,
+                            ld32=D))
+        self.decoder_plan = P
+        self.head_plan = self._build_heads(net, Bp, H, W)
+
+    def _build_heads(self, net, Bp, H, W):
+        cfg, w, dev = net.cfg, net.w, net.device
+        E, D, p = cfg.enc_dim, cfg.dec_dim, cfg.patch
+        ED = E + D
+        Fd = cfg.feature_dim
+        ld = cfg.layer_dims
+        ht, wt = H // p, W // p
+        N = ht * wt
+        M = Bp * N
+        P = ops.Plan()
+        # ---- MLP local features: [2, M, ED] -> fc1 GELU -> fc2 -> pixel shuffle
+        hidm = w.mlp_fc1_w.shape[1]
+        nloc = w.mlp_fc2_w.shape[1]
+        um = torch.empty(2, M, hidm, device=dev, dtype=F16)
+        self.feat25 = torch.empty(2, Bp, H, W, nloc // (p * p), device=dev, dtype=F32)
+        P.add(ops.gemm(_g(self.cat, 2), _g(w.mlp_fc1_w, 2), _g(um, 2), M, hidm, ED, lda=ED,
+                       bias=_g(w.mlp_fc1_b, 2), act="gelu"))
+        P.add(ops.gemm(_g(um, 2), _g(w.mlp_fc2_w, 2), _g(self.feat25, 2), M, nloc, hidm, lda=hidm,
+                       bias=_g(w.mlp_fc2_b, 2),
+                       store=("pixshuf", ht, wt, p, nloc // (p * p))))
+        # ---- DPTs: 4 groups (h1 pts, h1 gauss, h2 pts, h2 gauss)
+        g4 = lambda t: _g(t, 4)
+        head_of = (0, 0, 1, 1)
+        cat = self.cat
+        L0 = [cat[head_of[g]][:, :E] for g in range(4)]
+        L1 = [self.hook16[cfg.hooks[1]][head_of[g]] for g in range(4)]
+        L2 = [self.hook16[cfg.hooks[2]][head_of[g]] for g in range(4)]
+        L3 = [cat[head_of[g]][:, E:] for g in range(4)]
+        e = lambda *s, dt=F16: torch.empty(*s, device=dev, dtype=dt)
+        # act_postprocess
+        t0 = e(4, M, ld[0]); l0 = e(4, Bp, 4 * ht, 4 * wt, ld[0])
+        P.add(ops.gemm(L0, g4(w.ap0a_w), g4(t0), M, ld[0], E, lda=ED, bias=g4(w.ap0a_b)))
+        P.add(ops.gemm(g4(t0), g4(w.ap0b_w), g4(l0), M, 16 * ld[0], ld[0], lda=ld[0],
+                       bias=g4(w.ap0b_b), store=("convt", ht, wt, 4, ld[0])))
+        t1 = e(4, M, ld[1]); l1 = e(4, Bp, 2 * ht, 2 * wt, ld[1])
+        P.add(ops.gemm(L1, g4(w.ap1a_w), g4(t1), M, ld[1], D, lda=D, bias=g4(w.ap1a_b)))
+        P.add(ops.gemm(g4(t1), g4(w.ap1b_w), g4(l1), M, 4 * ld[1], ld[1], lda=ld[1],
+                       bias=g4(w.ap1b_b), store=("convt", ht, wt, 2, ld[1])))
+        l2 = e(4, Bp, ht, wt, ld[2])
+        P.add(ops.gemm(L2, g4(w.ap2_w), g4(l2), M, ld[2], D, lda=D, bias=g4(w.ap2_b)))
+        t3 = e(4, M, ld[3])
+        h3, w3 = (ht + 1) // 2, (wt + 1) // 2
+        l3 = e(4, Bp, h3, w3, ld[3])
+        P.add(ops.gemm(L3, g4(w.ap3a_w), g4(t3), M, ld[3], D, lda=D, bias=g4(w.ap3a_b)))
+        P.add(self._conv(g4(t3), w.ap3b_w, g4(l3), Bp, ht, wt, ld[3], ld[3], 3, 2, 1,
+                         bias=g4(w.ap3b_b)))
+        # layer_rn: 3x3, no bias -> 256
+        sizes = [(4 * ht, 4 * wt), (2 * ht, 2 * wt), (ht, wt), (h3, w3)]
+        ins = [l0, l1, l2, l3]
+        rs = []
+        for i in range(4):
+            hh, ww = sizes[i]
+            r = e(4, Bp, hh, ww, Fd)
+            P.add(self._conv(g4(ins[i]), w.rn_w[i], g4(r), Bp, hh, ww, ld[i], Fd, 3, 1, 1))
+            rs.append(r)
+        # refinenets 4 -> 1
+        prev = None
+        for stage in (3, 2, 1, 0):
+            blk = w.ref[stage]
+            hh, ww = sizes[stage]
+            x = rs[stage]
+            t = e(4, Bp, hh, ww, Fd)
+            s = e(4, Bp, hh, ww, Fd)
+            if prev is not None:
+                # out = prev + RCU1(x):  conv1(relu x) -> relu -> conv2 + x + prev
+                P.add(self._conv(g4(x), blk["u1c1_w"], g4(t), Bp, hh, ww, Fd, Fd, 3, 1, 1,
+                                 bias=g4(blk["u1c1_b"]), relu_in=True, act="relu"))
+                P.add(self._conv(g4(t), blk["u1c2_w"], g4(s), Bp, hh, ww, Fd, Fd, 3, 1, 1,
+                                 bias=g4(blk["u1c2_b"]), R1=g4(x), R2=g4(prev)))
+                x = s
+                s = e(4, Bp, hh, ww, Fd)
+            # RCU2
+            P.add(self._conv(g4(x), blk["u2c1_w"], g4(t), Bp, hh, ww, Fd, Fd, 3, 1, 1,
+                             bias=g4(blk["u2c1_b"]), relu_in=True, act="relu"))
+            P.add(self._conv(g4(t), blk["u2c2_w"], g4(s), Bp, hh, ww, Fd, Fd, 3, 1, 1,
+                             bias=g4(blk["u2c2_b"]), R1=g4(x)))
+            # out_conv 1x1 at low resolution, then x2 bilinear (align_corners)
+            oc = e(4, Bp, hh, ww, Fd)
+            P.add(ops.gemm(g4(s), g4(blk["out_w"]), g4(oc), Bp * hh * ww, Fd, Fd, lda=Fd,
+                           bias=g4(blk["out_b"])))
+            if stage > 0:
+                oh, ow = sizes[stage - 1]  # refinenet4 output is cropped to layer 3's grid
+            else:
+                oh, ow = 2 * hh, 2 * ww
+            up = e(4, Bp, oh, ow, Fd)
+            P.add(ops.upsample2x(g4(oc), g4(up), B=Bp, H=hh, W=ww, C=Fd, oh=oh, ow=ow))
+            prev = up
+        # head: conv3x3 256->128, up x2, conv3x3 128->128 + ReLU, conv1x1 -> 16
+        hh, ww = 8 * ht, 8 * wt
+        c1 = e(4, Bp, hh, ww, Fd // 2)
+        P.add(self._conv(g4(prev), w.h0_w, g4(c1), Bp, hh, ww, Fd, Fd // 2, 3, 1, 1, bias=g4(w.h0_b)))
+        c1u = e(4, Bp, 2 * hh, 2 * ww, Fd // 2)
+        P.add(ops.upsample2x(g4(c1), g4(c1u), B=Bp, H=hh, W=ww, C=Fd // 2))
+        c2 = e(4, Bp, 2 * hh, 2 * ww, Fd // 2)
+        P.add(self._conv(g4(c1u), w.h2_w, g4(c2), Bp, 2 * hh, 2 * ww, Fd // 2, Fd // 2, 3, 1, 1,
+                         bias=g4(w.h2_b), act="relu"))
+        self.dpt_out = e(4, Bp * H * W, w.NOUT, dt=F32)
+        P.add(ops.gemm(g4(c2), g4(w.h4_w), g4(self.dpt_out), Bp * H * W, w.NOUT, Fd // 2,
+                       lda=Fd // 2, bias=g4(w.h4_b)))
+        # gaussian_postprocess per head
+        n = Bp * H * W
+        self.res = []
+        self.desc16 = e(2, Bp, H, W, cfg.desc_dim)
+        for hd in range(2):
+            out = {}
+            for k, c in self.KEYS.items():
+                shape = (Bp, H, W) if c == 0 else (Bp, H, W, c)
+                out[k] = torch.empty(*shape, device=dev, dtype=F32)
+            out["sh"] = out["sh"].view(Bp, H, W, 3, 1)
+            P.add(ops.gaussian_postprocess(n, self.dpt_out[2 * hd], w.NOUT, self.feat25[hd],
+                                           self.dpt_out[2 * hd + 1], w.NOUT, cfg.use_offsets, out,
+                                           desc16=self.desc16[hd]))
+            self.res.append(out)
+        self._head_bufs = (um, t0, l0, t1, l1, l2, t3, l3, rs, c1, c1u, c2)
+        return P
+
+    @staticmethod
+    def _conv(A, Wt, C, Bp, H, W, Cin, Cout, k, stride, pad, bias=None, relu_in=False, act="none",
+              R1=None, R2=None):
+        oh = (H + 2 * pad - k) // stride + 1
+        ow = (W + 2 * pad - k) // stride + 1
+        M = Bp * oh * ow
+        conv = dict(H=H, W=W, C=Cin, k=k, stride=stride, pad=pad, oH=oh, oW=ow, relu_in=relu_in)
+        return ops.gemm(A, _g(Wt, len(A)), C, M, Cout, k * k * Cin, lda=0, bias=bias, act=act,
+                        R1=R1, ldr1=Cout, R2=R2, ldr2=Cout, conv=conv)
+
+    def run(self):
+        self.decoder_plan.replay()
+        self.head_plan.replay()
+
+
+class _Copy:
+    """Device-to-device copy step inside a Plan (torch copy_ on the stream)."""
+
+    def __init__(self, dst, src):
+        self.dst, self.src = dst, src
+
+    def __call__(self, stream):
+        self.dst.copy_(self.src)
+
+
+class Splatt3RNet:
+    """The network with the reference's `model.encoder` API
+    (dust3r/dust3r/model.py:121-193) plus fused fast paths."""
+
+    def __init__(self, cfg: NetConfig = FULL, state_dict=None, seed: int = 1234, device="cuda",
+                 graphs: bool = True):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        sd = state_dict if state_dict is not None else prng_state_dict(cfg, seed, self.device)
+        check_state_dict(cfg, sd)
+        self.w = PackedWeights(cfg, sd, self.device)
+        del sd
+        self.rope = rope_tables(512, self.device, cfg.rope_base)
+        self.graphs = graphs
+        self._enc: dict = {}
+        self._pair: dict = {}
+
+    # ---------------------------------------------------------- plans ----
+    def encoder_plan(self, B, H, W) -> EncoderPlan:
+        key = (B, H, W)
+        if key not in self._enc:
+            ep = EncoderPlan(self, B, H, W)
+            if self.graphs:
+                ep.plan.capture()
+            self._enc[key] = ep
+        return self._enc[key]
+
+    def pair_plan(self, Bp, H, W, keep_tokens=False) -> PairPlan:
+        key = (Bp, H, W, keep_tokens)
+        if key not in self._pair:
+            pp = PairPlan(self, Bp, H, W, keep_tokens)
+            if self.graphs and not keep_tokens:
+                pp.decoder_plan.capture()
+                pp.head_plan.capture()
+            self._pair[key] = pp
+        return self._pair[key]
+
+    # ------------------------------------------------- reference API -----
+    def _encode_image(self, image: torch.Tensor, true_shape=None):
+        B, C, H, W = image.shape
+        if W < H:
+            raise NotImplementedError("portrait input: transpose to landscape first "
+                                      "(ManyAR_PatchEmbed asserts W >= H)")
+        ep = self.encoder_plan(B, H, W)
+        feat, pos = ep(image.to(device=self.device, dtype=F32))
+        return feat.clone(), pos.clone(), None
+
+    def infer_pair(self, feat1, pos1, feat2, pos2, hw):
+        """Fused decoder + both heads for Bp pairs: returns (res1, res2)
+        dicts of [Bp, H, W, ...] tensors (views into static buffers: copy
+        before the next call if they must persist) and the plan."""
+        Bp, N, E = feat1.shape
+        H, W = hw
+        pp = self.pair_plan(Bp, H, W)
+        self._load_pair_inputs(pp, feat1, pos1, feat2, pos2)
+        pp.run()
+        return pp.res[0], pp.res[1], pp
+
+    def _load_pair_inputs(self, pp, feat1, pos1, feat2, pos2):
+        E = self.cfg.enc_dim
+        M = pp.Bp * pp.N
+        for b, (f, p) in enumerate(((feat1, pos1), (feat2, pos2))):
+            if f.dtype == F16:
+                pp.cat[b][:, :E].copy_(f.reshape(M, E))
+            else:
+                ops.cast_f16(f.reshape(M, E).contiguous(), pp.cat[b], rows=M, cols=E, ld_in=E,
+                             ld_out=E + self.cfg.dec_dim)(ops._lib.stream(self.device))
+            pp.pos[b].copy_(p.reshape(pp.Bp, pp.N, 2))
+
+    def _decoder(self, f1, pos1, f2, pos2):
+        """Returns zip(dec1, dec2) with 13 fp32 token tensors each, like
+        dust3r model.py:168-187 (hook-free API path)."""
+        Bp, N, E = f1.shape
+        ht_wt = N
+        pp = self._api_pair(Bp, N)
+        self._load_pair_inputs(pp, f1, pos1, f2, pos2)
+        pp.decoder_plan.run()
+        toks = pp.tokens
+        outs1 = [f1.float()] + [toks[i][0].view(Bp, N, -1).clone() for i in range(1, self.cfg.dec_depth + 1)]
+        outs2 = [f2.float()] + [toks[i][1].view(Bp, N, -1).clone() for i in range(1, self.cfg.dec_depth + 1)]
+        del ht_wt
+        return zip(*zip(outs1, outs2))
+
+    def _api_pair(self, Bp, N):
+        # token grid is unknown from N alone; the API path keeps the last
+        # image size seen by _encode_image (landscape, patch 16)
+        if not self._enc:
+            raise RuntimeError("_decoder called before _encode_image (image size unknown)")
+        B, H, W = list(self._enc.keys())[-1]
+        return self.pair_plan(Bp, H, W, keep_tokens=True)
+
+    def _downstream_head(self, head_num, decout, img_shape):
+        """GaussianHead.forward for one head on the given 13 token tensors."""
+        cfg = self.cfg
+        if torch.is_tensor(img_shape):
+            H, W = int(img_shape.min()), int(img_shape.max())
+        else:
+            H, W = int(img_shape[0]), int(img_shape[1])
+        Bp, N, _ = decout[-1].shape
+        pp = self.pair_plan(Bp, H, W, keep_tokens=True)
+        E, D = cfg.enc_dim, cfg.dec_dim
+        b = head_num - 1
+        st = ops._lib.stream(self.device)
+        M = Bp * N
+        ops.cast_f16(decout[0].reshape(M, E).float().contiguous(), pp.cat[b], rows=M, cols=E,
+                     ld_in=E, ld_out=E + D)(st)
+        ops.cast_f16(decout[-1].reshape(M, D).float().contiguous(), pp.cat[b][:, E:], rows=M,
+                     cols=D, ld_in=D, ld_out=E + D)(st)
+        for hk in cfg.hooks[1:3]:
+            ops.cast_f16(decout[hk].reshape(M, D).float().contiguous(), pp.hook16[hk][b], rows=M,
+                         cols=D, ld_in=D, ld_out=D)(st)
+        pp.head_plan.run()
+        return {k: v.clone() for k, v in pp.res[b].items()}

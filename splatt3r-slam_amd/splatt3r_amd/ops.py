@@ -61,11 +61,11 @@ _lib.register({
     "s3n_patch_im2col": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         P, P]),
     "s3n_upsample2x": (ctypes.c_int, [ctypes.c_int, _PP, _PP, ctypes.c_int, ctypes.c_int,
-                                      ctypes.c_int, ctypes.c_int, P]),
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]),
     "s3n_gaussian_postprocess": (ctypes.c_int, [I64, P, ctypes.c_int, P, P, ctypes.c_int,
                                                 ctypes.c_int] + [P] * 10 + [P]),
     "s3n_prng_fill": (ctypes.c_int, [P, I64, ctypes.c_uint64, ctypes.c_float, ctypes.c_float, P]),
-    "s3n_cast_f16": (ctypes.c_int, [P, P, I64, P]),
+    "s3n_cast_f16": (ctypes.c_int, [P, I64, P, I64, I64, ctypes.c_int, P]),
 })
 
 ACT = {"none": 0, "gelu": 1, "relu": 2}
@@ -177,10 +177,10 @@ def layernorm(x, gamma, beta, *, rows, C, ldx, eps=1e-6, out16=None, ld16=0, out
                 keep=(xs, gs, bs, o16, o32))
 
 
-def upsample2x(inp, out, *, B, H, W, C) -> Call:
+def upsample2x(inp, out, *, B, H, W, C, oh=None, ow=None) -> Call:
     i, o = _parr(inp), _parr(out)
     return Call("s3n_upsample2x", len(inp), ctypes.cast(i, _PP), ctypes.cast(o, _PP), B, H, W, C,
-                keep=(i, o))
+                oh or 2 * H, ow or 2 * W, keep=(i, o))
 
 
 def patch_im2col(img, A, *, B, H, W, p) -> Call:
@@ -201,8 +201,9 @@ def prng_fill(out: torch.Tensor, seed: int, a: float, c: float) -> None:
               ctypes.c_float(a), ctypes.c_float(c), _lib.stream(out.device))
 
 
-def cast_f16(x: torch.Tensor, out: torch.Tensor) -> None:
-    _lib.call("s3n_cast_f16", x.data_ptr(), out.data_ptr(), x.numel(), _lib.stream(x.device))
+def cast_f16(x, out, *, rows, cols, ld_in, ld_out) -> Call:
+    """fp32 [rows, cols] (row stride ld_in) -> fp16 (row stride ld_out)."""
+    return Call("s3n_cast_f16", _ptr(x), ld_in, _ptr(out), ld_out, rows, cols)
 
 
 class Plan:

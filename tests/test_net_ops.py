@@ -1,0 +1,214 @@
+"""Network kernels (include/s3n.h) vs plain PyTorch fp32 references of the
+same op, on the same (fp16-rounded) inputs.  Tolerances are stated per test:
+fp16 operands with fp32 MFMA accumulation vs an fp32 matmul of the same
+fp16-rounded operands -> only accumulation-order differences (~1e-6 rel),
+plus one fp16 rounding when the kernel writes fp16."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+def _rand(*shape, scale=1.0, dtype=torch.float16, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return (torch.randn(*shape, device="cuda", generator=g) * scale).to(dtype)
+
+
+@pytest.mark.parametrize("M,N,K,groups", [(768, 3072, 1024, 1), (200, 96, 72, 2), (37, 1536, 96, 4),
+                                          (4096, 256, 2304, 1), (768, 6400, 64, 2)])
+def test_gemm_dense_bias_residual(M, N, K, groups):
+    from splatt3r_amd import ops, _lib
+    A = [_rand(M, K, seed=g) for g in range(groups)]
+    W = [_rand(N, K, scale=K ** -0.5, seed=10 + g) for g in range(groups)]
+    b = [_rand(N, dtype=torch.float32, seed=20 + g) for g in range(groups)]
+    R = [_rand(M, N, dtype=torch.float32, seed=30 + g) for g in range(groups)]
+    C = [torch.empty(M, N, device="cuda") for _ in range(groups)]
+    ops.gemm(A, W, C, M, N, K, lda=K, bias=b, R1=R, ldr1=N)(_lib.stream())
+    for g in range(groups):
+        ref = A[g].float() @ W[g].float().T + b[g] + R[g]
+        assert rel_err(C[g], ref) < 1e-5, (g, rel_err(C[g], ref))
+
+
+def test_gemm_gelu_fp16_out_and_copy():
+    from splatt3r_amd import ops, _lib
+    M, N, K = 300, 512, 256
+    A, W, b = _rand(M, K), _rand(N, K, scale=K ** -0.5, seed=1), _rand(N, dtype=torch.float32, seed=2)
+    C = torch.empty(M, N, device="cuda", dtype=torch.float16)
+    C2 = torch.empty(M, N, device="cuda", dtype=torch.float16)
+    ops.gemm([A], [W], [C], M, N, K, lda=K, bias=[b], act="gelu", C2=[C2], ldc2=N)(_lib.stream())
+    ref = F.gelu(A.float() @ W.float().T + b)
+    assert rel_err(C, ref) < 2e-3
+    assert torch.equal(C, C2)
+
+
+def test_gemm_transposed_operand_layout_catches_swaps():
+    """A = I, asymmetric B (guide §3): C must equal B^T exactly."""
+    from splatt3r_amd import ops, _lib
+    n = 128
+    A = torch.eye(n, device="cuda", dtype=torch.float16)
+    B = (torch.arange(n * n, device="cuda").view(n, n) % 61).to(torch.float16)
+    C = torch.empty(n, n, device="cuda")
+    ops.gemm([A], [B], [C], n, n, n, lda=n)(_lib.stream())
+    assert torch.equal(C, B.float().T)
+
+
+@pytest.mark.parametrize("H,W,Cin,Cout,k,stride,relu", [(24, 32, 96, 256, 3, 1, False),
+                                                          (12, 16, 768, 768, 3, 2, False),
+                                                          (96, 128, 256, 256, 3, 1, True),
+                                                          (7, 9, 16, 40, 3, 2, True),
+                                                          (10, 12, 128, 16, 1, 1, False)])
+def test_gemm_implicit_conv(H, W, Cin, Cout, k, stride, relu):
+    from splatt3r_amd import ops, _lib
+    B, pad = 2, k // 2
+    x = _rand(B, H, W, Cin, seed=3)
+    w = _rand(Cout, Cin, k, k, scale=(Cin * k * k) ** -0.5, seed=4)
+    b = _rand(Cout, dtype=torch.float32, seed=5)
+    oh, ow = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    out = torch.empty(B, oh, ow, Cout, device="cuda")
+    wk = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous()
+    conv = dict(H=H, W=W, C=Cin, k=k, stride=stride, pad=pad, oH=oh, oW=ow, relu_in=relu)
+    ops.gemm([x], [wk], [out], B * oh * ow, Cout, k * k * Cin, lda=0, bias=[b], conv=conv)(_lib.stream())
+    xin = x.float().permute(0, 3, 1, 2)
+    if relu:
+        xin = xin.clamp_min(0)
+    ref = F.conv2d(xin, w.float(), b, stride=stride, padding=pad).permute(0, 2, 3, 1)
+    assert rel_err(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("s", [4, 2])
+def test_gemm_convtranspose_scatter(s):
+    from splatt3r_amd import ops, _lib
+    B, ht, wt, Cin, Cout = 2, 6, 8, 96, 96
+    x = _rand(B, ht, wt, Cin, seed=6)
+    w = _rand(Cin, Cout, s, s, scale=Cin ** -0.5, seed=7)
+    b = _rand(Cout, dtype=torch.float32, seed=8)
+    wk = w.permute(2, 3, 1, 0).reshape(s * s * Cout, Cin).contiguous()
+    out = torch.empty(B, ht * s, wt * s, Cout, device="cuda", dtype=torch.float16)
+    ops.gemm([x], [wk], [out], B * ht * wt, s * s * Cout, Cin, lda=Cin, bias=[b.repeat(s * s)],
+             store=("convt", ht, wt, s, Cout))(_lib.stream())
+    ref = F.conv_transpose2d(x.float().permute(0, 3, 1, 2), w.float(), b, stride=s).permute(0, 2, 3, 1)
+    assert rel_err(out, ref) < 2e-3
+
+
+def test_gemm_pixel_shuffle_scatter():
+    from splatt3r_amd import ops, _lib
+    B, ht, wt, K, p, c = 1, 3, 4, 64, 16, 25
+    N = c * p * p
+    x = _rand(B * ht * wt, K, seed=9)
+    w = _rand(N, K, scale=K ** -0.5, seed=10)
+    out = torch.empty(B, ht * p, wt * p, c, device="cuda")
+    ops.gemm([x], [w], [out], B * ht * wt, N, K, lda=K, store=("pixshuf", ht, wt, p, c))(_lib.stream())
+    lf = (x.float() @ w.float().T).view(B, ht * wt, N).transpose(-1, -2).reshape(B, N, ht, wt)
+    ref = F.pixel_shuffle(lf, p).permute(0, 2, 3, 1)  # catmlp_dpt_head.py:263-265
+    assert rel_err(out, ref) < 1e-5
+
+
+def rope_ref(t, pos, cos, sin):
+    """croco/models/pos_embed.py:142-159 on [B, H, N, 64]."""
+    def rot(x):
+        x1, x2 = x[..., :16], x[..., 16:]
+        return torch.cat((-x2, x1), -1)
+
+    def r1d(x, p):
+        c = F.embedding(p, torch.cat([cos, cos], -1))[:, None]
+        s = F.embedding(p, torch.cat([sin, sin], -1))[:, None]
+        return x * c + rot(x) * s
+
+    y, xx = t.chunk(2, dim=-1)
+    return torch.cat((r1d(y, pos[:, :, 0]), r1d(xx, pos[:, :, 1])), -1)
+
+
+@pytest.mark.parametrize("B,N,Nk,H,cross", [(1, 768, 768, 16, False), (2, 12, 12, 2, False),
+                                             (1, 640, 640, 12, True), (3, 100, 70, 4, True)])
+def test_attention_rope_vs_torch(B, N, Nk, H, cross):
+    from splatt3r_amd import ops, _lib
+    from splatt3r_amd.net import positions, rope_tables
+    D = 64
+    q = _rand(B * N, H * D, seed=11)
+    k = _rand(B * Nk, H * D, seed=12)
+    v = _rand(B * Nk, H * D, seed=13)
+    o = torch.empty(B * N, H * D, device="cuda", dtype=torch.float16)
+    cos, sin = rope_tables(512, "cuda")
+    qpos = positions(B, 24, 32, "cuda")[:, :N].contiguous() if N <= 768 else None
+    kpos = positions(B, 24, 32, "cuda")
+    kpos = (kpos.flip(1) if cross else kpos)[:, :Nk].contiguous()
+    if not cross:
+        kpos = qpos
+    ops.attention([q], [k], [v], [o], B=B, Nq=N, Nk=Nk, H=H, q_stride=H * D, k_stride=H * D,
+                  v_stride=H * D, o_stride=H * D, qpos=[qpos], kpos=[kpos], rope=(cos, sin),
+                  scale=D ** -0.5)(_lib.stream())
+    Q = rope_ref(q.float().view(B, N, H, D).transpose(1, 2), qpos, cos, sin)
+    K = rope_ref(k.float().view(B, Nk, H, D).transpose(1, 2), kpos, cos, sin)
+    V = v.float().view(B, Nk, H, D).transpose(1, 2)
+    ref = ((Q @ K.transpose(-2, -1)) * D ** -0.5).softmax(-1) @ V
+    ref = ref.transpose(1, 2).reshape(B * N, H * D)
+    # Q/K rotated in fp16 and P rounded to fp16 before P.V: ~1e-3 relative
+    assert rel_err(o, ref) < 5e-3, rel_err(o, ref)
+
+
+def test_layernorm_vs_torch():
+    from splatt3r_amd import ops, _lib
+    for C in (1024, 768, 128):
+        x = _rand(300, C, dtype=torch.float32, seed=14) * 3 + 1
+        g = _rand(C, dtype=torch.float32, seed=15)
+        b = _rand(C, dtype=torch.float32, seed=16)
+        o16 = torch.empty(300, C, device="cuda", dtype=torch.float16)
+        o32 = torch.empty(300, C, device="cuda")
+        ops.layernorm([x], [g], [b], rows=300, C=C, ldx=C, eps=1e-6, out16=[o16], ld16=C,
+                      out32=[o32], ld32=C)(_lib.stream())
+        ref = F.layer_norm(x, (C,), g, b, eps=1e-6)
+        assert rel_err(o32, ref) < 1e-5
+        assert rel_err(o16, ref) < 1e-3
+
+
+@pytest.mark.parametrize("H,W,oh,ow", [(12, 16, 24, 32), (5, 7, 9, 14), (192, 256, 384, 512)])
+def test_upsample_align_corners_vs_torch(H, W, oh, ow):
+    from splatt3r_amd import ops, _lib
+    x = _rand(2, H, W, 128, seed=17)
+    out = torch.empty(2, oh, ow, 128, device="cuda", dtype=torch.float16)
+    ops.upsample2x([x], [out], B=2, H=H, W=W, C=128, oh=oh, ow=ow)(_lib.stream())
+    ref = F.interpolate(x.float().permute(0, 3, 1, 2), scale_factor=2, mode="bilinear",
+                        align_corners=True)[:, :, :oh, :ow].permute(0, 2, 3, 1)
+    assert rel_err(out, ref) < 1e-3
+
+
+def test_prng_fill_bitexact_vs_numpy():
+    from splatt3r_amd import ops
+    from splatt3r_amd.weights import prng_numpy, tensor_seed
+    t = torch.empty(100_003, device="cuda")
+    seed = tensor_seed(1234, "enc_blocks.0.attn.qkv.weight")
+    ops.prng_fill(t, seed, 0.0541, 0.0)
+    np.testing.assert_array_equal(t.cpu().numpy(), prng_numpy(seed, 100_003, 0.0541, 0.0))
+
+
+def test_gaussian_postprocess_vs_torch():
+    from splatt3r_amd import ops, _lib
+    n = 5000
+    pts = _rand(n, 16, dtype=torch.float32, seed=18)
+    feat = _rand(n, 25, dtype=torch.float32, seed=19)
+    gs = _rand(n, 16, dtype=torch.float32, seed=20)
+    out = {k: torch.empty(n, c, device="cuda").squeeze(-1) for k, c in
+           dict(pts3d=3, conf=1, desc=24, desc_conf=1, scales=3, rotations=4, sh=3,
+                opacities=1, means=3).items()}
+    ops.gaussian_postprocess(n, pts, 16, feat, gs, 16, True, out)(_lib.stream())
+    xyz = pts[:, :3]
+    d = xyz.norm(dim=-1, keepdim=True)
+    p3 = xyz / d.clip(min=1e-8) * torch.expm1(d)
+    off = gs[:, :3]
+    od = off.norm(dim=-1, keepdim=True)
+    offs = off / od.clip(min=1e-8) * (torch.exp(od - 6) - torch.exp(torch.zeros_like(od) - 6))
+    rot = gs[:, 6:10]
+    ref = dict(pts3d=p3, conf=1 + pts[:, 3].exp(), desc=feat[:, :24] / feat[:, :24].norm(dim=-1, keepdim=True),
+               desc_conf=1 + feat[:, 24].exp(), scales=gs[:, 3:6].exp(),
+               rotations=rot / (rot.norm(dim=-1, keepdim=True) + 1e-8), sh=gs[:, 10:13],
+               opacities=gs[:, 13].sigmoid(), means=p3 + offs)
+    for k, v in ref.items():
+        assert rel_err(out[k], v) < 1e-5, k
