@@ -210,9 +210,30 @@ def gen_net():
         H, Wd = 48, 64
         img1 = torch.rand(1, 3, H, Wd, generator=g) * 2 - 1
         img2 = torch.rand(1, 3, H, Wd, generator=g) * 2 - 1
+        # stage captures of head 1's pts DPT (NHWC) to localise divergences
+        cap = {}
+        dpt = model.downstream_head1.dpt
+        named = {"ap0": dpt.act_postprocess[0], "ap1": dpt.act_postprocess[1],
+                 "ap2": dpt.act_postprocess[2], "ap3": dpt.act_postprocess[3],
+                 "rn0": dpt.scratch.layer_rn[0], "rn1": dpt.scratch.layer_rn[1],
+                 "rn2": dpt.scratch.layer_rn[2], "rn3": dpt.scratch.layer_rn[3],
+                 "ref4": dpt.scratch.refinenet4, "ref3": dpt.scratch.refinenet3,
+                 "ref2": dpt.scratch.refinenet2, "ref1": dpt.scratch.refinenet1,
+                 "head0": dpt.head[0], "head3": dpt.head[3], "head4": dpt.head[4],
+                 "mlp": model.downstream_head1.head_local_features}
+        hooks = []
+        for k, m in named.items():
+            def fn(mod, inp, outp, k=k):
+                if k not in cap:
+                    cap[k] = outp.detach().clone()
+            hooks.append(m.register_forward_hook(fn))
         f1, f2, p1, dec1, dec2, r1, r2 = run_reference(model, img1, img2)
+        for hk_ in hooks:
+            hk_.remove()
         out = dict(img1=img1.numpy(), img2=img2.numpy(), feat1=f1.numpy(), feat2=f2.numpy(),
                    pos=p1.numpy())
+        for k, v in cap.items():
+            out["stage_" + k] = (v.permute(0, 2, 3, 1) if v.dim() == 4 else v).contiguous().numpy()
         for hk in cfg.hooks:
             out[f"dec1_{hk}"] = dec1[hk].numpy()
             out[f"dec2_{hk}"] = dec2[hk].numpy()

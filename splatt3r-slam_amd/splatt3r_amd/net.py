@@ -364,6 +364,7 @@ class PairPlan:
             rs.append(r)
         # refinenets 4 -> 1
         prev = None
+        self._ref_outs = {}
         for stage in (3, 2, 1, 0):
             blk = w.ref[stage]
             hh, ww = sizes[stage]
@@ -394,6 +395,7 @@ class PairPlan:
             up = e(4, Bp, oh, ow, Fd)
             P.add(ops.upsample2x(g4(oc), g4(up), B=Bp, H=hh, W=ww, C=Fd, oh=oh, ow=ow))
             prev = up
+            self._ref_outs[f"ref{stage + 1}"] = up[0]
         # head: conv3x3 256->128, up x2, conv3x3 128->128 + ReLU, conv1x1 -> 16
         hh, ww = 8 * ht, 8 * wt
         c1 = e(4, Bp, hh, ww, Fd // 2)
@@ -421,6 +423,11 @@ class PairPlan:
                                            desc16=self.desc16[hd]))
             self.res.append(out)
         self._head_bufs = (um, t0, l0, t1, l1, l2, t3, l3, rs, c1, c1u, c2)
+        # named stage outputs (group 0 = head 1 pts DPT), for parity diagnostics
+        self.stages = dict(ap0=l0[0], ap1=l1[0], ap2=l2[0], ap3=l3[0], rn0=rs[0][0], rn1=rs[1][0],
+                           rn2=rs[2][0], rn3=rs[3][0], head0=c1[0], head3=c2[0],
+                           head4=self.dpt_out[0].view(Bp, H, W, -1)[..., :4], mlp=self.feat25[0])
+        self.stages.update(self._ref_outs)
         return P
 
     @staticmethod

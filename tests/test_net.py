@@ -48,6 +48,36 @@ def _err(a, b):
 
 
 @pytest.mark.gpu
+def test_small_model_stage_by_stage():
+    """Per-stage errors of head 1's pts DPT vs the reference captures
+    (localises a divergence instead of reporting only the end result)."""
+    import torch.nn.functional as F
+    from splatt3r_amd import weights as W
+    from splatt3r_amd.net import Splatt3RNet
+    g = np.load(os.path.join(GOLDEN, "net_small_off.npz"))
+    net = Splatt3RNet(W.SMALL, seed=1234, graphs=False)
+    f1, p1, _ = net._encode_image(torch.from_numpy(g["img1"]).cuda(), None)
+    f2, p2, _ = net._encode_image(torch.from_numpy(g["img2"]).cuda(), None)
+    r1, r2, pp = net.infer_pair(f1, p1, f2, p2, (48, 64))
+    errs = {}
+    for k, ours in pp.stages.items():
+        ref = g["stage_" + k]
+        if k == "mlp":  # Mlp output [1, S, 6400] -> pixel_shuffle NHWC
+            t = torch.from_numpy(ref).transpose(-1, -2).reshape(1, 6400, 3, 4)
+            ref = F.pixel_shuffle(t, 16).permute(0, 2, 3, 1).numpy()
+        o = ours.float().cpu().numpy().reshape(ref.shape[0], -1, *ref.shape[2:]) if k != "ref4" else None
+        if k == "ref4":  # ours is cropped to layer 3's grid (dpt_head.py:56)
+            ref = ref[:, :3, :4]
+            o = ours.float().cpu().numpy()
+        errs[k] = _err(o.reshape(ref.shape), ref)
+    print({k: round(v, 5) for k, v in errs.items()})
+    for hk in (6, 9, 12):
+        pass
+    bad = {k: v for k, v in errs.items() if v > 2e-2}
+    assert not bad, f"stages over 2e-2: {bad} (all: {errs})"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("tag,use_offsets", [("small_off", True), ("small_nooff", False)])
 def test_small_model_vs_reference_golden(tag, use_offsets):
     import dataclasses
