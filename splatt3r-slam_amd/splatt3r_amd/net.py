@@ -350,7 +350,7 @@ class PairPlan:
         t3 = e(4, M, ld[3])
         h3, w3 = (ht + 1) // 2, (wt + 1) // 2
         l3 = e(4, Bp, h3, w3, ld[3])
-        P.add(ops.gemm(L3, g4(w.ap3a_w), g4(t3), M, ld[3], D, lda=D, bias=g4(w.ap3a_b)))
+        P.add(ops.gemm(L3, g4(w.ap3a_w), g4(t3), M, ld[3], D, lda=ED, bias=g4(w.ap3a_b)))
         P.add(self._conv(g4(t3), w.ap3b_w, g4(l3), Bp, ht, wt, ld[3], ld[3], 3, 2, 1,
                          bias=g4(w.ap3b_b)))
         # layer_rn: 3x3, no bias -> 256
@@ -468,7 +468,7 @@ class Splatt3RNet:
         self.w = PackedWeights(cfg, sd, self.device)
         del sd
         self.rope = rope_tables(512, self.device, cfg.rope_base)
-        self.graphs = graphs
+        self.graphs = graphs and ops.GRAPHS_ENABLED and not ops.DEBUG_SYNC
         self._enc: dict = {}
         self._pair: dict = {}
 

@@ -8,6 +8,7 @@ into a HIP graph.  No op has a torch fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Sequence
 
 import torch
@@ -69,6 +70,11 @@ _lib.register({
 })
 
 ACT = {"none": 0, "gelu": 1, "relu": 2}
+
+# S3_SYNC_DEBUG=1: run plans op by op with a device sync after each (fault
+# localisation); S3_GRAPHS=0 disables HIP-graph capture.
+DEBUG_SYNC = os.environ.get("S3_SYNC_DEBUG", "0") == "1"
+GRAPHS_ENABLED = os.environ.get("S3_GRAPHS", "1") != "0"
 
 
 def _ptr(x):
@@ -222,6 +228,13 @@ class Plan:
 
     def run(self, stream=None):
         st = stream if stream is not None else _lib.stream()
+        if DEBUG_SYNC:
+            for i, c in enumerate(self.calls):
+                print(f"[plan] op {i}/{len(self.calls)} {getattr(c, 'name', type(c).__name__)}",
+                      flush=True)
+                c(st)
+                torch.cuda.synchronize()
+            return
         for c in self.calls:
             c(st)
 
