@@ -1,0 +1,37 @@
+/*
+ * s3t.h — tracker Gauss-Newton step on the GPU (the per-iteration work of
+ * FrameTracker.opt_pose_ray_dist_sim3, splatt3r_slam/tracker.py:173-214,
+ * and FrameTracker.solve :156-171).
+ *
+ * One launch per GN iteration computes, for every correspondence i,
+ *   p  = T . Xf_i                          (geometry.act_Sim3, :45-52)
+ *   rd = (p/|p|, |p|), drd/dp              (geometry.point_to_ray_dist, :17-34)
+ *   r  = rd(Xk_i) - rd(p),  J = -drd/dp [I, -[p]x, p]
+ *   w  = sqrt_info * sqrt(huber(sqrt_info * r, k))   (nonlinear_optimizer.py:28-33)
+ *   A  = w J,  b = w r
+ * and reduces H = sum A^T A (upper triangle, 28), g = -sum A^T b (7),
+ * cost = 0.5 sum b^T b into out[36] = {H_upper(28, row-major), g(7), cost}.
+ * sqrt_info = (1/sigma_ray, x3; 1/sigma_dist) * valid_i * sqrt(Q_i).
+ * The pose T (Sim3, t q s) is a by-value argument so the host-driven loop
+ * needs no device upload per iteration.
+ */
+#ifndef S3T_H
+#define S3T_H
+#include "s3_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Workspace bytes for n correspondences (block partials). */
+size_t s3t_workspace_bytes(int64_t n);
+
+int s3t_ray_dist_normal_eqs(const float* T /* host [8] */, const float* Xf, const float* Xk,
+                            const float* Q, const uint8_t* valid, int64_t n,
+                            float sigma_ray, float sigma_dist, float huber_k,
+                            void* workspace, float* out36, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* S3T_H */

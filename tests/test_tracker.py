@@ -1,0 +1,115 @@
+"""Tracker Gauss-Newton (include/s3t.h, splatt3r_amd/tracker.py) vs the numpy
+oracle (oracle/tracker_ref.py, restating tracker.py:156-214).  The oracle's
+Jacobian is pinned by finite differences of its own residual under the left
+retraction Exp(d)*T (the parametrisation lietorch's retr uses)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import oracle.tracker_ref as TR
+
+CFG = dict(sigma_ray=0.003, sigma_dist=10.0, k=1.345)
+
+
+def _scene(n, seed, noise=0.0):
+    rng = np.random.default_rng(seed)
+    Xk = np.concatenate([rng.uniform(-1, 1, (n, 2)), rng.uniform(1, 4, (n, 1))], 1)
+    T_true = np.array([0.05, -0.02, 0.03, 0.02, -0.01, 0.015, 0.0, 1.02])
+    T_true[6] = np.sqrt(1 - np.sum(T_true[3:6] ** 2))
+    # Xf such that T_true . Xf = Xk
+    Tinv = oracle.sim3_inv(T_true.astype(np.float32)[None])[0].astype(np.float64)
+    Xf = TR.act_sim3(Tinv, Xk) + rng.normal(size=(n, 3)) * noise
+    Q = rng.uniform(1.0, 3.0, (n, 1))
+    valid = rng.uniform(size=(n, 1)) > 0.1
+    return (Xf.astype(np.float32), Xk.astype(np.float32), Q.astype(np.float32), valid,
+            T_true.astype(np.float32))
+
+
+def _residual(T, Xf, Xk):
+    return (TR.point_to_ray_dist(Xk.astype(np.float64)) -
+            TR.point_to_ray_dist(TR.act_sim3(T, Xf.astype(np.float64))))
+
+
+def test_oracle_jacobian_matches_finite_differences():
+    Xf, Xk, Q, valid, _ = _scene(64, 0, noise=0.01)
+    T = np.array([0.1, 0.0, -0.05, 0.0, 0.0, 0.0, 1.0, 1.1], np.float64)
+    p = TR.act_sim3(T, Xf.astype(np.float64))
+    dXdT = np.concatenate([np.broadcast_to(np.eye(3), (64, 3, 3)), -TR.skew(p), p[:, :, None]], -1)
+    _, D = TR.point_to_ray_dist(p, jacobian=True)
+    J = -D @ dXdT
+    eps = 1e-4
+    for j in range(7):
+        d = np.zeros((1, 7), np.float32)
+        d[0, j] = eps
+        Tp = oracle.sim3_retr(T.astype(np.float32)[None], d)[0].astype(np.float64)
+        d[0, j] = -eps
+        Tm = oracle.sim3_retr(T.astype(np.float32)[None], d)[0].astype(np.float64)
+        fd = (_residual(Tp, Xf, Xk) - _residual(Tm, Xf, Xk)) / (2 * eps)
+        np.testing.assert_allclose(J[:, :, j], fd, rtol=2e-2, atol=2e-3, err_msg=f"col {j}")
+
+
+def test_oracle_gn_recovers_pose():
+    Xf, Xk, Q, valid, T_true = _scene(2000, 1)
+    T = np.array([0, 0, 0, 0, 0, 0, 1, 1], np.float32)
+    for _ in range(20):
+        H, g, _ = TR.normal_equations(T, Xf, Xk, Q, valid, **CFG)
+        tau = np.linalg.solve(H, g)
+        T = oracle.sim3_retr(T[None], tau.astype(np.float32)[None])[0]
+    np.testing.assert_allclose(TR.act_sim3(T, Xf), Xk, atol=1e-4)
+
+
+def test_solve_normal_eqs_raises_like_cholesky():
+    from splatt3r_amd.tracker import CholeskyError, solve_normal_eqs
+    with pytest.raises(CholeskyError):
+        solve_normal_eqs(-np.eye(7), np.ones(7))
+    with pytest.raises(CholeskyError):
+        solve_normal_eqs(np.full((7, 7), np.nan), np.ones(7))
+    H = np.diag(np.arange(1.0, 8.0))
+    np.testing.assert_allclose(solve_normal_eqs(H, np.ones(7)), 1 / np.arange(1.0, 8.0))
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 1000, 196608])
+def test_normal_equations_gpu_vs_oracle(n):
+    from splatt3r_amd.tracker import NormalEquations
+    Xf, Xk, Q, valid, _ = _scene(n, 2, noise=0.02)
+    T = np.array([0.01, 0.02, -0.01, 0.01, 0.0, -0.01, 0.9999, 0.98], np.float32)
+    T[3:7] /= np.linalg.norm(T[3:7])
+    ne = NormalEquations("cuda")
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    H, g, cost = ne(T, d(Xf), d(Xk), d(Q), d(valid), CFG["sigma_ray"], CFG["sigma_dist"], CFG["k"])
+    Hr, gr, cr = TR.normal_equations(T, Xf, Xk, Q, valid, **CFG)
+    # fp32 per-point terms summed in fp32 per block / fp64 across blocks
+    scale = np.abs(Hr).max()
+    np.testing.assert_allclose(H, Hr, rtol=1e-3, atol=1e-5 * scale)
+    np.testing.assert_allclose(g, gr, rtol=1e-3, atol=1e-5 * np.abs(gr).max())
+    np.testing.assert_allclose(cost, cr, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_invalid_points_contribute_nothing():
+    from splatt3r_amd.tracker import NormalEquations
+    Xf, Xk, Q, valid, _ = _scene(4096, 3, noise=0.02)
+    valid[:] = False
+    ne = NormalEquations("cuda")
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    H, g, cost = ne(np.array([0, 0, 0, 0, 0, 0, 1, 1], np.float32), d(Xf), d(Xk), d(Q), d(valid),
+                    0.003, 10.0, 1.345)
+    assert np.all(H == 0) and np.all(g == 0) and cost == 0
+
+
+@pytest.mark.gpu
+def test_opt_pose_ray_dist_sim3_recovers_pose():
+    import lietorch
+    from splatt3r_amd.tracker import FrameTracker
+    Xf, Xk, Q, valid, T_true = _scene(196608, 4)
+    tr = FrameTracker(None, None, "cuda")
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    T_WCk = lietorch.Sim3.Identity(1, device="cuda")
+    T_WCf = lietorch.Sim3.Identity(1, device="cuda")
+    T_WCf_new, T_CkCf = tr.opt_pose_ray_dist_sim3(d(Xf), d(Xk), T_WCf, T_WCk, d(Q), d(valid))
+    got = T_CkCf.act(d(Xf)).cpu().numpy()
+    np.testing.assert_allclose(got, Xk, atol=2e-4)
+    assert 1 <= tr.last_iters < 50
