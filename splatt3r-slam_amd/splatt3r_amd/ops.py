@@ -100,7 +100,11 @@ class Call:
         self.name = name
         self.fn = getattr(_lib.lib(), name)
         self.args = args
-        self.keep = keep  # objects that must outlive the call (ctypes arrays, structs)
+        # Everything the call points into must outlive it: the ctypes
+        # arrays/structs AND the tensors behind the raw pointers (a plan
+        # buffer held only by pointer is freed, and torch.cuda.graph's
+        # empty_cache() then unmaps it under the captured kernels).
+        self.keep = keep
 
     def __call__(self, stream):
         st = self.fn(*self.args, stream)
@@ -151,7 +155,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         mode, sH, sW, s, cout = store
         a.store_mode = {"convt": 1, "pixshuf": 2}[mode]
         a.sH, a.sW, a.sS, a.sCout = sH, sW, s, cout
-    return Call("s3n_gemm", ctypes.byref(a), keep=(a,))
+    return Call("s3n_gemm", ctypes.byref(a), keep=(a, A, B, C, bias, R1, R2, C2))
 
 
 def attention(Q, K, V, O, *, B, Nq, Nk, H, q_stride, k_stride, v_stride, o_stride, qpos=None,
@@ -168,7 +172,7 @@ def attention(Q, K, V, O, *, B, Nq, Nk, H, q_stride, k_stride, v_stride, o_strid
         a.rope_cos, a.rope_sin = rope[0].data_ptr(), rope[1].data_ptr()
         a.rope_maxpos = rope[0].shape[0]
     a.scale = scale
-    return Call("s3n_attention", ctypes.byref(a), keep=(a,))
+    return Call("s3n_attention", ctypes.byref(a), keep=(a, Q, K, V, O, qpos, kpos, rope))
 
 
 def layernorm(x, gamma, beta, *, rows, C, ldx, eps=1e-6, out16=None, ld16=0, out32=None,
@@ -180,17 +184,17 @@ def layernorm(x, gamma, beta, *, rows, C, ldx, eps=1e-6, out16=None, ld16=0, out
                 ctypes.cast(gs, _PP), ctypes.cast(bs, _PP), ctypes.c_float(eps),
                 ctypes.cast(o16, _PP) if o16 is not None else None, ld16,
                 ctypes.cast(o32, _PP) if o32 is not None else None, ld32,
-                keep=(xs, gs, bs, o16, o32))
+                keep=(xs, gs, bs, o16, o32, x, gamma, beta, out16, out32))
 
 
 def upsample2x(inp, out, *, B, H, W, C, oh=None, ow=None) -> Call:
     i, o = _parr(inp), _parr(out)
     return Call("s3n_upsample2x", len(inp), ctypes.cast(i, _PP), ctypes.cast(o, _PP), B, H, W, C,
-                oh or 2 * H, ow or 2 * W, keep=(i, o))
+                oh or 2 * H, ow or 2 * W, keep=(i, o, inp, out))
 
 
 def patch_im2col(img, A, *, B, H, W, p) -> Call:
-    return Call("s3n_patch_im2col", _ptr(img), B, H, W, p, _ptr(A))
+    return Call("s3n_patch_im2col", _ptr(img), B, H, W, p, _ptr(A), keep=(img, A))
 
 
 def gaussian_postprocess(n, pts, ld_pts, feat, gauss, ld_g, use_offsets, out: dict,
@@ -199,7 +203,7 @@ def gaussian_postprocess(n, pts, ld_pts, feat, gauss, ld_g, use_offsets, out: di
                 int(use_offsets), _ptr(out["pts3d"]), _ptr(out["conf"]), _ptr(out["desc"]),
                 _ptr(desc16), _ptr(out["desc_conf"]), _ptr(out["scales"]),
                 _ptr(out["rotations"]), _ptr(out["sh"]), _ptr(out["opacities"]),
-                _ptr(out["means"]))
+                _ptr(out["means"]), keep=(pts, feat, gauss, out, desc16))
 
 
 def prng_fill(out: torch.Tensor, seed: int, a: float, c: float) -> None:
@@ -209,7 +213,7 @@ def prng_fill(out: torch.Tensor, seed: int, a: float, c: float) -> None:
 
 def cast_f16(x, out, *, rows, cols, ld_in, ld_out) -> Call:
     """fp32 [rows, cols] (row stride ld_in) -> fp16 (row stride ld_out)."""
-    return Call("s3n_cast_f16", _ptr(x), ld_in, _ptr(out), ld_out, rows, cols)
+    return Call("s3n_cast_f16", _ptr(x), ld_in, _ptr(out), ld_out, rows, cols, keep=(x, out))
 
 
 class Plan:

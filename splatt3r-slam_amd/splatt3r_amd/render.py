@@ -125,12 +125,14 @@ def render_cuda(extrinsics, intrinsics, near, far, image_shape, background_color
     return torch.stack(images)
 
 
-def pack_splats(views, image_scale):
+def pack_splats(views, image_scale, img_chw_normalized=False):
     """Fused HIP packing of per-view head outputs into rasterizer inputs.
 
     views: list of dicts with means [hw,3], scales [hw,3], rotations [hw,4]
            (xyzw), sh [hw,3,1] (network residual), opacities [hw,1] and
-           img [hw,3] in [0,1] (the RGB2SH residual source), all f32 cuda.
+           img [hw,3] in [0,1] (the RGB2SH residual source), all f32 cuda;
+           with img_chw_normalized, img is the frame's [1,3,H,W] ImgNorm
+           tensor (converted with clamp(x*0.5+0.5, 0, 1) in the kernel).
     image_scale: the scale-invariant factor s (means * s, cov * s^2).
     Returns (means3D [P,3], cov6 [P,6], shs [P,1,3], opac [P,1]) with
     P = sum(hw), in view order (view 0 first), as render_cuda receives them.
@@ -151,7 +153,8 @@ def pack_splats(views, image_scale):
                                                    "opacities", "img")]
         if ts[3].shape[-1] != 1:
             raise NotImplementedError("pack_splats: sh_degree 0 (one SH coefficient) only")
-        _lib.call("s3r_pack_splats", *[t.data_ptr() for t in ts], n, 1, float(image_scale), 0,
+        _lib.call("s3r_pack_splats", *[t.data_ptr() for t in ts], n, 1, float(image_scale),
+                  int(img_chw_normalized),
                   means[off:].data_ptr(), cov6[off:].data_ptr(), shs[off:].data_ptr(),
                   opac[off:].data_ptr(), stream)
         off += n

@@ -1,0 +1,329 @@
+"""Inference / matching / rendering entry points of the SLAM frontend with the
+reference's names and contracts (splatt3r_slam/splatt3r_utils.py).
+
+Differences in HOW, not WHAT:
+  * `decoder()` runs the fused pair plan (grouped decoder branches + both
+    heads, HIP-graph replay) instead of `_decoder` + 2 x `_downstream_head`;
+    the result dicts carry the same keys/shapes (:92-99).
+  * `splatt3r_render()` feeds `render.pack_splats` (one HIP kernel for
+    build_covariance + RGB2SH residual + scale-invariant rescale + triu)
+    into the HIP rasterizer, instead of ~20 torch ops + render_cuda; same
+    camera math (:332-432 -> decoder_splatting_cuda.py:30-83).
+  * `gaussians_to_world()` keeps the reference's torch formulation
+    (:180-328); its fusion into HIP kernels is §8(f) f2.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+import lietorch
+from splatt3r_amd import matching
+from splatt3r_amd.config import config
+from splatt3r_amd.render import (DecoderSplattingCUDA, camera_settings, normalize_intrinsics,
+                                 pack_splats)
+
+C0 = 0.28209479177387814
+
+
+# ----------------------------------------------------------------- model ---
+class Splatt3RModel:
+    """What load_splatt3r returns (MAST3RGaussians, splatt3r_core/main.py:44-124):
+    `.encoder` exposes _encode_image/_decoder/_downstream_head, `.decoder`
+    is the splatting decoder."""
+
+    def __init__(self, encoder, decoder):
+        self.encoder = encoder
+        self.decoder = decoder
+
+    def eval(self):
+        return self
+
+    def share_memory(self):
+        return self
+
+    def to(self, *a, **k):
+        return self
+
+
+def load_splatt3r(path=None, device="cuda", cfg=None, seed: int = 1234, graphs: bool = True):
+    """splatt3r_utils.py:31-66.  `path`: a local Lightning ckpt / safetensors
+    with the reference's state_dict keys (loaded with weights_only=True).  No
+    path and no local checkpoints/epoch=19-step=1200.ckpt -> portable-PRNG
+    weights of the same architecture (there is no download path offline)."""
+    from splatt3r_amd.net import Splatt3RNet
+    from splatt3r_amd.weights import FULL, load_state_dict_file
+    cfg = cfg or FULL
+    sd = None
+    if path is None:
+        local = os.path.join(os.getcwd(), "checkpoints", "epoch=19-step=1200.ckpt")
+        path = local if os.path.exists(local) else None
+    if path is not None:
+        print(f"Loading Splatt3R model from {path}")
+        sd = {k: v.to(device) for k, v in load_state_dict_file(path).items()}
+    net = Splatt3RNet(cfg, state_dict=sd, seed=seed, device=device, graphs=graphs)
+    return Splatt3RModel(net, DecoderSplattingCUDA([0.0, 0.0, 0.0]).to(device))
+
+
+# ------------------------------------------------------------- inference ---
+@torch.inference_mode()
+def decoder(model, feat1, feat2, pos1, pos2, shape1, shape2):
+    """splatt3r_utils.py:92-99 (fused).  Returns (res1, res2) dicts of
+    [B,H,W,...] tensors; they are views of the plan's static buffers and
+    stay valid until the next decoder() call of the same shape."""
+    H, W = _hw(shape1)
+    res1, res2, _ = model.encoder.infer_pair(feat1, pos1, feat2, pos2, (H, W))
+    return res1, res2
+
+
+def _hw(shape):
+    if torch.is_tensor(shape):
+        s = shape.reshape(-1, 2)[0].tolist()
+        return int(s[0]), int(s[1])
+    s = np.asarray(shape).reshape(-1, 2)[0]
+    return int(s[0]), int(s[1])
+
+
+def downsample(X, C, D, Q):
+    """splatt3r_utils.py:102-112."""
+    ds = config["dataset"]["img_downsample"]
+    if ds > 1:
+        X = X[..., ::ds, ::ds, :].contiguous()
+        C = C[..., ::ds, ::ds].contiguous()
+        D = D[..., ::ds, ::ds, :].contiguous()
+        Q = Q[..., ::ds, ::ds].contiguous()
+    return X, C, D, Q
+
+
+def _extract_gaussian_params(res):
+    """splatt3r_utils.py:120-137 (clones: the plan buffers are reused)."""
+    d = {k: res[k].clone() for k in ("means", "scales", "rotations", "sh", "opacities")}
+    if "conf" in res:
+        d["conf"] = res["conf"].clone()
+    return d
+
+
+def _ensure_encoded(model, frame):
+    if frame.feat is None:
+        frame.feat, frame.pos, _ = model.encoder._encode_image(frame.img, frame.img_true_shape)
+
+
+def _stack_outputs(res):
+    X = torch.stack([r["pts3d"][0] for r in res])
+    C = torch.stack([r["conf"][0] for r in res])
+    D = torch.stack([r["desc"][0] for r in res])
+    Q = torch.stack([r["desc_conf"][0] for r in res])
+    return downsample(X, C, D, Q)
+
+
+@torch.inference_mode()
+def splatt3r_inference_mono(model, frame):
+    """splatt3r_utils.py:503-536."""
+    _ensure_encoded(model, frame)
+    res11, res21 = decoder(model, frame.feat, frame.feat, frame.pos, frame.pos,
+                           frame.img_true_shape, frame.img_true_shape)
+    frame.gaussian_pred = _extract_gaussian_params(res11)
+    frame.gaussian_pred_cross = _extract_gaussian_params(res21)
+    X, C, _, _ = _stack_outputs([res11, res21])
+    Xii = X[0].reshape(1, -1, 3)
+    Cii = C[0].reshape(1, -1, 1)
+    return Xii[0], Cii[0]
+
+
+@torch.inference_mode()
+def splatt3r_asymmetric_inference(model, frame_i, frame_j):
+    """splatt3r_utils.py:580-607."""
+    _ensure_encoded(model, frame_i)
+    _ensure_encoded(model, frame_j)
+    res11, res21 = decoder(model, frame_i.feat, frame_j.feat, frame_i.pos, frame_j.pos,
+                           frame_i.img_true_shape, frame_j.img_true_shape)
+    X, C, D, Q = _stack_outputs([res11, res21])
+    return X, C, D, Q, (res11, res21)
+
+
+def splatt3r_match_asymmetric(model, frame_i, frame_j, idx_i2j_init=None):
+    """splatt3r_utils.py:610-644."""
+    X, C, D, Q, (res_self, res_cross) = splatt3r_asymmetric_inference(model, frame_i, frame_j)
+    frame_i.gaussian_pred = _extract_gaussian_params(res_self)
+    frame_i.gaussian_pred_cross = _extract_gaussian_params(res_cross)
+    b = X.shape[0] // 2
+    idx_i2j, valid_match_j = matching.match(X[:b], X[b:], D[:b], D[b:],
+                                            idx_1_to_2_init=idx_i2j_init)
+    Xii, Xji = X.reshape(2 * b, -1, 3)[:b], X.reshape(2 * b, -1, 3)[b:]
+    Cii, Cji = C.reshape(2 * b, -1, 1)[:b], C.reshape(2 * b, -1, 1)[b:]
+    Qii, Qji = Q.reshape(2 * b, -1, 1)[:b], Q.reshape(2 * b, -1, 1)[b:]
+    # the reference unpacks the b=1 batch dim with einops (:638-641)
+    return idx_i2j, valid_match_j, Xii[0], Cii[0], Qii[0], Xji[0], Cji[0], Qji[0]
+
+
+@torch.inference_mode()
+def splatt3r_decode_symmetric_batch(model, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
+    """splatt3r_utils.py:466-499, batched: one fused pair plan over the b
+    pairs in each order (the reference loops pairs one at a time)."""
+    b = feat_i.shape[0]
+    H, W = _hw(shape_i)
+    r11, r21, _ = model.encoder.infer_pair(feat_i, pos_i, feat_j, pos_j, (H, W))
+    Xa = [r11["pts3d"].clone(), r21["pts3d"].clone()]
+    Ca = [r11["conf"].clone(), r21["conf"].clone()]
+    Da = [r11["desc"].clone(), r21["desc"].clone()]
+    Qa = [r11["desc_conf"].clone(), r21["desc_conf"].clone()]
+    r22, r12, _ = model.encoder.infer_pair(feat_j, pos_j, feat_i, pos_i, (H, W))
+    Xa += [r22["pts3d"], r12["pts3d"]]
+    Ca += [r22["conf"], r12["conf"]]
+    Da += [r22["desc"], r12["desc"]]
+    Qa += [r22["desc_conf"], r12["desc_conf"]]
+    # ordering 4 x b x h x w x c : [ii, ji, jj, ij]
+    X, C, D, Q = (torch.stack(t, 0) for t in (Xa, Ca, Da, Qa))
+    return downsample(X, C, D, Q)
+
+
+def splatt3r_match_symmetric(model, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
+    """splatt3r_utils.py:539-576."""
+    X, C, D, Q = splatt3r_decode_symmetric_batch(model, feat_i, pos_i, feat_j, pos_j,
+                                                 shape_i, shape_j)
+    b = X.shape[1]
+    Xii, Xji, Xjj, Xij = X
+    Dii, Dji, Djj, Dij = D
+    Qii, Qji, Qjj, Qij = Q
+    idx, valid = matching.match(torch.cat((Xii, Xjj)), torch.cat((Xji, Xij)),
+                                torch.cat((Dii, Djj)), torch.cat((Dji, Dij)))
+    return (idx[:b], idx[b:], valid[:b], valid[b:], Qii.reshape(b, -1, 1),
+            Qjj.reshape(b, -1, 1), Qji.reshape(b, -1, 1), Qij.reshape(b, -1, 1))
+
+
+# ------------------------------------------------------------- rendering ---
+def _sim3_to_4x4(T_sim3):
+    """splatt3r_utils.py:153-165: [sR | t; 0 0 0 1] (float32)."""
+    data = T_sim3.data.detach()
+    if data.dim() == 1:
+        data = data.unsqueeze(0)
+    return lietorch.Sim3(data.reshape(-1, 8)).matrix().to(torch.float32)
+
+
+def _estimate_default_intrinsics(h, w, device="cuda"):
+    """splatt3r_utils.py:168-176."""
+    f = float(max(h, w))
+    return torch.tensor([[f, 0, w / 2.0], [0, f, h / 2.0], [0, 0, 1]], device=device,
+                        dtype=torch.float32)
+
+
+@torch.inference_mode()
+def splatt3r_render(model, frame, ref_frame, K=None, target_T_WC=None):
+    """splatt3r_utils.py:332-432 -> [1,1,3,H,W]."""
+    if frame.gaussian_pred is None or frame.gaussian_pred_cross is None:
+        print("[splatt3r_render] No Gaussian predictions available – skipping.")
+        return None
+    g1, g2 = frame.gaussian_pred, frame.gaussian_pred_cross
+    dev = g1["means"].device
+    _, h, w, _ = g1["means"].shape
+    context = _sim3_to_4x4(frame.T_WC).to(dev)
+    target = context.clone() if target_T_WC is None else _sim3_to_4x4(target_T_WC).to(dev)
+    K_use = (_estimate_default_intrinsics(h, w, dev) if K is None
+             else K.clone().to(device=dev, dtype=torch.float32))
+    if K_use.dim() == 2:
+        K_use = K_use.unsqueeze(0)
+    # decoder_splatting_cuda.py:36-55
+    extr = torch.inverse(context) @ target
+    intr = normalize_intrinsics(K_use, (h, w))[..., :3, :3]
+    near = torch.full((1,), 0.1, device=dev)
+    far = torch.full((1,), 1000.0, device=dev)
+    bg = model.decoder.background_color.to(dev)[None]
+    settings, scale = camera_settings(extr, intr, near, far, (h, w), bg, 0)
+    views = []
+    for g, img in ((g1, frame.img), (g2, ref_frame.img)):
+        views.append(dict(means=g["means"].reshape(-1, 3), scales=g["scales"].reshape(-1, 3),
+                          rotations=g["rotations"].reshape(-1, 4), sh=g["sh"].reshape(-1, 3, 1),
+                          opacities=g["opacities"].reshape(-1, 1),
+                          img=img.to(dev)))
+    means, cov6, shs, opac = pack_splats(views, float(scale[0]), img_chw_normalized=True)
+    from diff_gaussian_rasterization import GaussianRasterizer
+    means2D = torch.zeros_like(means)
+    image, _ = GaussianRasterizer(settings[0])(means3D=means, means2D=means2D, shs=shs,
+                                               colors_precomp=None, opacities=opac,
+                                               cov3D_precomp=cov6)
+    return image[None, None]
+
+
+@torch.inference_mode()
+def gaussians_to_world(frame, include_cross=True, spatial_stride=1, depth_min=0.05,
+                       depth_max_percentile=0.98, max_scale=0.5, min_confidence=1.5):
+    """splatt3r_utils.py:180-328 -> (means_world, cov_triu, colors, opacities)."""
+    if frame.gaussian_pred is None:
+        return None
+    M = _sim3_to_4x4(frame.T_WC)[0]
+    R, t = M[:3, :3].to(frame.gaussian_pred["means"].device), M[:3, 3]
+    preds = [frame.gaussian_pred]
+    if include_cross and frame.gaussian_pred_cross is not None:
+        preds.append(frame.gaussian_pred_cross)
+    s = max(1, int(spatial_stride))
+    row, col = torch.triu_indices(3, 3)
+    outs = []
+    for pred in preds:
+        means = pred["means"][:, ::s, ::s, :].reshape(-1, 3)
+        scales = pred["scales"][:, ::s, ::s, :].reshape(-1, 3)
+        rots = pred["rotations"][:, ::s, ::s, :].reshape(-1, 4)
+        sh0 = pred["sh"][:, ::s, ::s, :, 0].reshape(-1, 3)
+        opas = pred["opacities"][:, ::s, ::s, :].reshape(-1)
+        conf = pred["conf"][:, ::s, ::s].reshape(-1) if "conf" in pred else None
+        img = (frame.img * 0.5 + 0.5).clamp(0, 1)[:, :, ::s, ::s]
+        sh0 = sh0 + (img[0].permute(1, 2, 0).reshape(-1, 3) - 0.5) / C0   # RGB2SH
+        z = means[:, 2]
+        valid = z > depth_min
+        if bool(valid.any()) and depth_max_percentile < 1.0:
+            valid = valid & (z <= torch.quantile(z[valid], depth_max_percentile))
+        valid = valid & (scales.max(dim=-1).values < max_scale)
+        if conf is not None and min_confidence > 0:
+            valid = valid & (conf >= min_confidence)
+        means, scales, rots, sh0, opas = (x[valid] for x in (means, scales, rots, sh0, opas))
+        if means.shape[0] == 0:
+            continue
+        Rq = _quat_to_matrix(rots)
+        cov = Rq @ torch.diag_embed(scales ** 2) @ Rq.transpose(-1, -2)
+        cov_w = R @ cov @ R.T
+        outs.append(((R @ means.T).T + t, cov_w[:, row, col], (sh0 * C0 + 0.5).clamp(0, 1), opas))
+    if not outs:
+        return None
+    return tuple(torch.cat(x, 0) for x in zip(*outs))
+
+
+def _quat_to_matrix(q, eps: float = 1e-8):
+    """utils/geometry.py:24-49 (xyzw, with the 2/(|q|^2+eps) factor)."""
+    i, j, k, r = q.unbind(-1)
+    two_s = 2 / ((q * q).sum(-1) + eps)
+    o = torch.stack((1 - two_s * (j * j + k * k), two_s * (i * j - k * r), two_s * (i * k + j * r),
+                     two_s * (i * j + k * r), 1 - two_s * (i * i + k * k), two_s * (j * k - i * r),
+                     two_s * (i * k - j * r), two_s * (j * k + i * r), 1 - two_s * (i * i + j * j)),
+                    -1)
+    return o.reshape(*q.shape[:-1], 3, 3)
+
+
+# ------------------------------------------------------------ host input ---
+def resize_img(img, size, square_ok=False, return_transformation=False):
+    """splatt3r_utils.py:658-693 (PIL resize + centre crop, ImgNorm)."""
+    import PIL.Image
+    assert size in (224, 512)
+    pil = PIL.Image.fromarray(np.uint8(img * 255))
+    W1, H1 = pil.size
+    long_edge = round(size * max(W1 / H1, H1 / W1)) if size == 224 else size
+    S = max(pil.size)
+    interp = PIL.Image.LANCZOS if S > long_edge else PIL.Image.BICUBIC
+    pil = pil.resize(tuple(int(round(x * long_edge / S)) for x in pil.size), interp)
+    W, H = pil.size
+    cx, cy = W // 2, H // 2
+    if size == 224:
+        half = min(cx, cy)
+        pil = pil.crop((cx - half, cy - half, cx + half, cy + half))
+    else:
+        halfw, halfh = ((2 * cx) // 16) * 8, ((2 * cy) // 16) * 8
+        if not square_ok and W == H:
+            halfh = 3 * halfw / 4
+        pil = pil.crop((cx - halfw, cy - halfh, cx + halfw, cy + halfh))
+    arr = np.asarray(pil)
+    t = torch.from_numpy(arr.astype(np.float32) / 255.0).permute(2, 0, 1)
+    res = dict(img=((t - 0.5) / 0.5)[None], true_shape=np.int32([pil.size[::-1]]),
+               unnormalized_img=arr)
+    if return_transformation:
+        return res, (W1 / W, H1 / H, (W - pil.size[0]) / 2, (H - pil.size[1]) / 2)
+    return res
