@@ -34,7 +34,7 @@ import math
 import torch
 
 from splatt3r_amd import ops
-from splatt3r_amd.weights import FULL, NetConfig, check_state_dict, prng_state_dict
+from splatt3r_amd.weights import FULL, NetConfig, check_state_dict, prng_state_dict, tie_symmetric
 
 F16 = torch.float16
 F32 = torch.float32
@@ -460,10 +460,12 @@ class Splatt3RNet:
     (dust3r/dust3r/model.py:121-193) plus fused fast paths."""
 
     def __init__(self, cfg: NetConfig = FULL, state_dict=None, seed: int = 1234, device="cuda",
-                 graphs: bool = True):
+                 graphs: bool = True, symmetric: bool = False):
         self.cfg = cfg
         self.device = torch.device(device)
         sd = state_dict if state_dict is not None else prng_state_dict(cfg, seed, self.device)
+        if symmetric:
+            sd = tie_symmetric(dict(sd))
         check_state_dict(cfg, sd)
         self.w = PackedWeights(cfg, sd, self.device)
         del sd
@@ -471,12 +473,38 @@ class Splatt3RNet:
         self.graphs = graphs and ops.GRAPHS_ENABLED and not ops.DEBUG_SYNC
         self._enc: dict = {}
         self._pair: dict = {}
+        # bench.py sets a list here to collect (tag, start, end) HIP events
+        # around every encoder / pair-plan replay on the launch stream
+        self.events = None
+
+    def _timed(self, tag, fn, *a):
+        if self.events is None:
+            return fn(*a)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn(*a)
+        e1.record()
+        self.events.append((tag, e0, e1))
+        return out
+
+    def plans(self):
+        """Every built plan (for per-kernel profiling)."""
+        for ep in self._enc.values():
+            yield ep.plan
+        for pp in self._pair.values():
+            yield pp.decoder_plan
+            yield pp.head_plan
 
     # ---------------------------------------------------------- plans ----
     def encoder_plan(self, B, H, W) -> EncoderPlan:
         key = (B, H, W)
         if key not in self._enc:
-            ep = EncoderPlan(self, B, H, W)
+            # plan buffers are ordinary tensors even when the first call
+            # comes from inside torch.inference_mode (they are re-filled
+            # in place by later calls made outside it)
+            with torch.inference_mode(False):
+                ep = EncoderPlan(self, B, H, W)
             if self.graphs:
                 ep.plan.capture()
             self._enc[key] = ep
@@ -485,7 +513,8 @@ class Splatt3RNet:
     def pair_plan(self, Bp, H, W, keep_tokens=False) -> PairPlan:
         key = (Bp, H, W, keep_tokens)
         if key not in self._pair:
-            pp = PairPlan(self, Bp, H, W, keep_tokens)
+            with torch.inference_mode(False):
+                pp = PairPlan(self, Bp, H, W, keep_tokens)
             if self.graphs and not keep_tokens:
                 pp.decoder_plan.capture()
                 pp.head_plan.capture()
@@ -499,7 +528,7 @@ class Splatt3RNet:
             raise NotImplementedError("portrait input: transpose to landscape first "
                                       "(ManyAR_PatchEmbed asserts W >= H)")
         ep = self.encoder_plan(B, H, W)
-        feat, pos = ep(image.to(device=self.device, dtype=F32))
+        feat, pos = self._timed("encoder", ep, image.to(device=self.device, dtype=F32))
         return feat.clone(), pos.clone(), None
 
     def infer_pair(self, feat1, pos1, feat2, pos2, hw):
@@ -510,7 +539,7 @@ class Splatt3RNet:
         H, W = hw
         pp = self.pair_plan(Bp, H, W)
         self._load_pair_inputs(pp, feat1, pos1, feat2, pos2)
-        pp.run()
+        self._timed("pair", pp.run)
         return pp.res[0], pp.res[1], pp
 
     def _load_pair_inputs(self, pp, feat1, pos1, feat2, pos2):

@@ -94,10 +94,12 @@ def _parr(items: Sequence, n=G):
 
 class Call:
     """A prebuilt library call: fn(*args) with status check."""
-    __slots__ = ("fn", "args", "name", "keep")
+    __slots__ = ("fn", "args", "name", "keep", "kind", "flops")
 
-    def __init__(self, name, *args, keep=()):
+    def __init__(self, name, *args, keep=(), kind=None, flops=0):
         self.name = name
+        self.kind = kind or name     # roofline bucket (bench.py)
+        self.flops = flops           # algorithmic flops of one launch
         self.fn = getattr(_lib.lib(), name)
         self.args = args
         # Everything the call points into must outlive it: the ctypes
@@ -155,7 +157,9 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         mode, sH, sW, s, cout = store
         a.store_mode = {"convt": 1, "pixshuf": 2}[mode]
         a.sH, a.sW, a.sS, a.sCout = sH, sW, s, cout
-    return Call("s3n_gemm", ctypes.byref(a), keep=(a, A, B, C, bias, R1, R2, C2))
+    return Call("s3n_gemm", ctypes.byref(a), keep=(a, A, B, C, bias, R1, R2, C2),
+                kind="gemm.conv" if conv is not None else "gemm.dense",
+                flops=2 * int(M) * int(N) * int(K) * groups)
 
 
 def attention(Q, K, V, O, *, B, Nq, Nk, H, q_stride, k_stride, v_stride, o_stride, qpos=None,
@@ -172,7 +176,8 @@ def attention(Q, K, V, O, *, B, Nq, Nk, H, q_stride, k_stride, v_stride, o_strid
         a.rope_cos, a.rope_sin = rope[0].data_ptr(), rope[1].data_ptr()
         a.rope_maxpos = rope[0].shape[0]
     a.scale = scale
-    return Call("s3n_attention", ctypes.byref(a), keep=(a, Q, K, V, O, qpos, kpos, rope))
+    return Call("s3n_attention", ctypes.byref(a), keep=(a, Q, K, V, O, qpos, kpos, rope),
+                flops=4 * B * H * Nq * Nk * 64 * len(Q))
 
 
 def layernorm(x, gamma, beta, *, rows, C, ldx, eps=1e-6, out16=None, ld16=0, out32=None,
@@ -241,6 +246,21 @@ class Plan:
             return
         for c in self.calls:
             c(st)
+
+    def run_timed(self, stream=None):
+        """Eager run with a HIP event pair around every call on the launch
+        stream; returns [(kind, flops, start_event, end_event)]."""
+        st = stream if stream is not None else _lib.stream()
+        ts = torch.cuda.current_stream()
+        out = []
+        for c in self.calls:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(ts)
+            c(st)
+            e1.record(ts)
+            out.append((getattr(c, "kind", type(c).__name__), getattr(c, "flops", 0), e0, e1))
+        return out
 
     def capture(self):
         """Capture the plan into a HIP graph (torch.cuda.CUDAGraph)."""

@@ -48,7 +48,8 @@ class Splatt3RModel:
         return self
 
 
-def load_splatt3r(path=None, device="cuda", cfg=None, seed: int = 1234, graphs: bool = True):
+def load_splatt3r(path=None, device="cuda", cfg=None, seed: int = 1234, graphs: bool = True,
+                  symmetric: bool = False):
     """splatt3r_utils.py:31-66.  `path`: a local Lightning ckpt / safetensors
     with the reference's state_dict keys (loaded with weights_only=True).  No
     path and no local checkpoints/epoch=19-step=1200.ckpt -> portable-PRNG
@@ -63,7 +64,8 @@ def load_splatt3r(path=None, device="cuda", cfg=None, seed: int = 1234, graphs: 
     if path is not None:
         print(f"Loading Splatt3R model from {path}")
         sd = {k: v.to(device) for k, v in load_state_dict_file(path).items()}
-    net = Splatt3RNet(cfg, state_dict=sd, seed=seed, device=device, graphs=graphs)
+    net = Splatt3RNet(cfg, state_dict=sd, seed=seed, device=device, graphs=graphs,
+                      symmetric=symmetric)
     return Splatt3RModel(net, DecoderSplattingCUDA([0.0, 0.0, 0.0]).to(device))
 
 

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -28,6 +29,7 @@ _lib.register({
 })
 
 _TRIU = [(a, b) for a in range(7) for b in range(a, 7)]
+_DEBUG = os.environ.get("S3_TRACK_DEBUG", "0") == "1"
 
 
 class CholeskyError(RuntimeError):
@@ -172,6 +174,12 @@ class FrameTracker:
         for step in range(cfg["max_iters"]):
             H, g, new_cost = self.normal_eqs(T, Xf, Xk, Q, valid, cfg["sigma_ray"],
                                              cfg["sigma_dist"], cfg["huber"])
+            if _DEBUG:
+                print(f"[gn] step {step} n={Xf.shape[0]} valid={int(valid.sum())} cost={new_cost:.4g} "
+                      f"Hdiag={np.diag(H)} g={g} T={T} "
+                      f"finite Xf={bool(torch.isfinite(Xf).all())} Xk={bool(torch.isfinite(Xk).all())} "
+                      f"Q={bool(torch.isfinite(Q).all())} |Xf|min={float(Xf.norm(dim=-1).min()):.3g} "
+                      f"|Xk|min={float(Xk.norm(dim=-1).min()):.3g}", flush=True)
             tau = solve_normal_eqs(H, g)
             T = _retr_host(T, tau)
             self.last_iters = step + 1

@@ -294,3 +294,19 @@ def check_state_dict(cfg: NetConfig, sd: dict) -> None:
            if n in sd and tuple(sd[n].shape) != tuple(s)]
     if missing or bad:
         raise ValueError(f"state_dict mismatch: missing={missing[:5]}... bad={bad[:5]}")
+
+
+def tie_symmetric(sd: dict) -> dict:
+    """Make the two decoder branches and the two heads share weights
+    (dec_blocks2 := dec_blocks, downstream_head2 := downstream_head1).
+
+    Same architecture and the same compute; used by bench.py so that, with
+    portable-PRNG weights, the cross prediction of a view agrees with the
+    self prediction of a nearby view (as trained weights make it) and the
+    tracker's matching/GN run with realistic trip counts.  Parity tests use
+    the untied weights."""
+    for name in list(sd):
+        for a, b in (("dec_blocks2.", "dec_blocks."), ("downstream_head2.", "downstream_head1.")):
+            if name.startswith(a):
+                sd[name] = sd[b + name[len(a):]]
+    return sd
