@@ -26,6 +26,30 @@ def shard(pairs, ws: int, rank: int):
     return pairs[rank::ws]
 
 
+def gather_map(recs: torch.Tensor, ws: int) -> torch.Tensor:
+    """The map exchange: every rank contributes its [n_r, 13] world records,
+    every rank receives all of them in rank order (one all-gather; shards
+    of unequal size are padded to the largest and trimmed after)."""
+    if ws == 1:
+        return recs
+    dev = recs.device
+    n = torch.tensor([recs.shape[0]], device=dev, dtype=torch.int64)
+    ns = [torch.zeros_like(n) for _ in range(ws)]
+    dist.all_gather(ns, n)
+    ns = [int(x) for x in ns]
+    nmax = max(ns)
+    buf = torch.zeros(nmax, recs.shape[1], device=dev, dtype=recs.dtype)
+    buf[:recs.shape[0]] = recs
+    if dist.get_backend() == "nccl":
+        out = torch.empty(ws * nmax, recs.shape[1], device=dev, dtype=recs.dtype)
+        dist.all_gather_into_tensor(out, buf)
+        parts = out.split(nmax)
+    else:
+        parts = [torch.empty_like(buf) for _ in range(ws)]
+        dist.all_gather(parts, buf)
+    return torch.cat([p[:k] for p, k in zip(parts, ns)])
+
+
 def world_gaussians(res, T_WC: torch.Tensor, img: torch.Tensor) -> torch.Tensor:
     """Per-pixel Gaussians of one predicted view -> [n, 13] world records
     (means, cov triu, RGB colour, opacity), the transform gaussians_to_world
@@ -94,7 +118,6 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
     process_shard(model, feats, poss, poses, imgs, mine, shape)   # build + capture plans
     torch.cuda.synchronize()
     n_local = len(mine) * H * W   # the jj self-prediction of every local pair
-    gathered = torch.empty(ws, n_local, GAUSS_FLOATS, device=dev)
     times, t_gather = [], []
     for _ in range(reps):
         if ws > 1:
@@ -104,10 +127,7 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
         _, recs = process_shard(model, feats, poss, poses, imgs, mine, shape)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        if ws > 1:
-            dist.all_gather_into_tensor(gathered, recs.reshape(n_local, GAUSS_FLOATS))
-        else:
-            gathered[0].copy_(recs.reshape(n_local, GAUSS_FLOATS))
+        gathered = gather_map(recs, ws)
         torch.cuda.synchronize()
         if ws > 1:
             dist.barrier()
@@ -122,4 +142,4 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
     return dict(kf_pairs_per_s=total / t, pairs=total, pairs_per_rank=len(mine),
                 ms_per_batch=t * 1e3, allgather_ms=sorted(t_gather)[len(t_gather) // 2] * 1e3,
                 allgather_MB_per_rank=n_local * GAUSS_FLOATS * 4 / 1e6,
-                map_gaussians=ws * n_local)
+                map_gaussians=int(gathered.shape[0]))
