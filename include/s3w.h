@@ -1,0 +1,51 @@
+/*
+ * s3w.h — camera-space Gaussian predictions -> filtered world-space records
+ * (SURVEY §8 A11 / §8(f) f2).
+ *
+ * Replaces the torch body of gaussians_to_world
+ * (splatt3r_slam/splatt3r_utils.py:180-328) for one predicted view:
+ *   stride-s subsample (:259-270), RGB2SH residual on the DC band (:277-281,
+ *   utils/sh_utils.py:114-115), the three splash filters (:296-312):
+ *     z > depth_min, z <= quantile(z[z > depth_min], q) (torch.quantile,
+ *     linear interpolation), max(scale) < max_scale, conf >= min_confidence,
+ *   then means_w = M x + t, cov_w = M (R S S^T R^T) M^T (build_covariance,
+ *   utils/geometry.py:24-62) packed triu (xx,xy,xz,yy,yz,zz), colour =
+ *   clamp(sh0 * C0 + 0.5, 0, 1), opacity.  M = s R of the Sim3 T_WC.
+ * Output records keep the reference's order (row-major over the strided
+ * grid, the order of torch boolean indexing): out[k] = 13 floats
+ *   {means_w[3], cov_triu[6], colour[3], opacity}.
+ */
+#ifndef S3W_H
+#define S3W_H
+#include "s3_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  const float* means;      /* [H, W, 3] camera space */
+  const float* scales;     /* [H, W, 3] */
+  const float* rotations;  /* [H, W, 4] xyzw */
+  const float* sh;         /* [H, W, 3, d_sh] (DC = index 0) */
+  const float* opacities;  /* [H, W] */
+  const float* conf;       /* [H, W] or NULL (no confidence filter) */
+  const float* img;        /* [3, H, W] ImgNorm-normalised frame image */
+  int H, W, d_sh, stride;
+} s3w_view;
+
+/* Workspace for n = ceil(H/stride) * ceil(W/stride) Gaussians. */
+size_t s3w_workspace_bytes(int64_t n);
+
+/* T_WC: host float[12] = row-major 3x3 (s R) then t.  depth_max_percentile
+ * >= 1 disables the quantile bound, min_confidence <= 0 the confidence
+ * filter.  out: [n, 13] device; *count_dev (device int64) receives the
+ * number of records written.  Stream-ordered, no host sync. */
+int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, float depth_min,
+                           float depth_max_percentile, float max_scale, float min_confidence,
+                           void* workspace, float* out, int64_t* count_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* S3W_H */

@@ -37,6 +37,7 @@ SOURCES = {
     "tracker.hip": STRICT,
     "raster.hip": STRICT,
     "splat_pack.hip": STRICT,
+    "gaussians.hip": STRICT,
     "net_gemm.hip": FAST,
     "net_attn.hip": FAST,
     "net_ops.hip": STRICT,

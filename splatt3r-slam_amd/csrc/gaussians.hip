@@ -1,0 +1,210 @@
+// gaussians_to_world for one predicted view (include/s3w.h).
+//
+// k_prep    strided gather of z, "z > depth_min" keys (+inf otherwise) and
+//           the valid count
+// sort      hipcub radix sort of the keys (the quantile's order statistic)
+// k_flags   torch.quantile (linear) bound + scale / confidence filters
+// scan      hipcub exclusive sum of the flags (stable compaction order)
+// k_emit    world transform, covariance, colour, opacity -> 13-float records
+// All stream-ordered; the only host-visible result is *count_dev.
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+#include "s3w.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr float kC0 = 0.28209479177387814f;
+
+struct Ws {
+  float* keys_in;
+  float* keys_out;
+  uint32_t* flags;
+  uint32_t* offsets;
+  uint32_t* n_valid0;
+  void* sort_tmp;
+  size_t sort_bytes;
+  void* scan_tmp;
+  size_t scan_bytes;
+};
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+size_t sort_bytes(int64_t n) {
+  size_t b = 0;
+  hipcub::DeviceRadixSort::SortKeys(nullptr, b, (float*)nullptr, (float*)nullptr, (int)n);
+  return b;
+}
+
+size_t scan_bytes(int64_t n) {
+  size_t b = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  return b;
+}
+
+Ws carve(void* base, int64_t n) {
+  char* p = static_cast<char*>(base);
+  Ws w;
+  w.keys_in = (float*)p;  p += align256(sizeof(float) * n);
+  w.keys_out = (float*)p; p += align256(sizeof(float) * n);
+  w.flags = (uint32_t*)p; p += align256(sizeof(uint32_t) * n);
+  w.offsets = (uint32_t*)p; p += align256(sizeof(uint32_t) * n);
+  w.n_valid0 = (uint32_t*)p; p += 256;
+  w.sort_bytes = sort_bytes(n);
+  w.sort_tmp = p; p += align256(w.sort_bytes);
+  w.scan_bytes = scan_bytes(n);
+  w.scan_tmp = p;
+  return w;
+}
+
+struct Grid {
+  int H, W, s, ws;
+  __device__ int64_t pix(int64_t i) const {
+    const int64_t y = (i / ws) * s, x = (i % ws) * s;
+    return y * W + x;
+  }
+};
+
+__global__ void __launch_bounds__(kThreads)
+k_prep(int64_t n, Grid g, const float* __restrict__ means, float depth_min,
+       float* __restrict__ keys, uint32_t* __restrict__ n_valid0) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const float z = means[g.pix(i) * 3 + 2];
+  const bool v = z > depth_min;
+  keys[i] = v ? z : INFINITY;
+  if (v) atomicAdd(n_valid0, 1u);
+}
+
+// torch.quantile(sorted[:n], q), interpolation='linear' (aten Sorting.cpp:
+// ranks = q * (n - 1); below = long(ranks); above = ceil(ranks);
+// lerp(v_below, v_above, ranks - below) with torch's two-sided lerp).
+__device__ float quantile_linear(const float* sorted, uint32_t n, float q) {
+  const float ranks = q * (float)(n - 1);
+  const int64_t lo = (int64_t)ranks;
+  const int64_t hi = (int64_t)ceilf(ranks);
+  const float w = ranks - (float)lo;
+  const float a = sorted[lo], b = sorted[hi];
+  return fabsf(w) < 0.5f ? a + w * (b - a) : b - (b - a) * (1.0f - w);
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_flags(int64_t n, Grid g, const float* __restrict__ means, const float* __restrict__ scales,
+        const float* __restrict__ conf, float depth_min, float q, float max_scale, float min_conf,
+        const float* __restrict__ sorted, const uint32_t* __restrict__ n_valid0,
+        uint32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = g.pix(i);
+  const float z = means[p * 3 + 2];
+  bool v = z > depth_min;
+  const uint32_t n0 = *n_valid0;
+  if (n0 > 0 && q < 1.0f) v = v && (z <= quantile_linear(sorted, n0, q));
+  // torch max propagates NaN
+  float m = scales[p * 3 + 0];
+  const float s1 = scales[p * 3 + 1], s2 = scales[p * 3 + 2];
+  if (!(s1 <= m) && !isnan(m)) m = s1;
+  if (!(s2 <= m) && !isnan(m)) m = s2;
+  v = v && (m < max_scale);
+  if (conf && min_conf > 0.0f) v = v && (conf[p] >= min_conf);
+  flags[i] = v ? 1u : 0u;
+}
+
+struct Pose {
+  float m[12];
+};
+
+__global__ void __launch_bounds__(kThreads)
+k_emit(int64_t n, Grid g, s3w_view v, Pose T, const uint32_t* __restrict__ flags,
+       const uint32_t* __restrict__ offsets, float* __restrict__ out, int64_t* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  if (i == n - 1) *count = (int64_t)offsets[i] + flags[i];
+  if (!flags[i]) return;
+  const int64_t p = g.pix(i);
+  const float* M = T.m;
+  const float x = v.means[p * 3 + 0], y = v.means[p * 3 + 1], z = v.means[p * 3 + 2];
+  float* o = out + (int64_t)offsets[i] * 13;
+  for (int r = 0; r < 3; ++r) o[r] = (M[r * 3 + 0] * x + M[r * 3 + 1] * y + M[r * 3 + 2] * z) + M[9 + r];
+  // quaternion_to_matrix (xyzw, two_s = 2 / (|q|^2 + 1e-8)), utils/geometry.py:24-49
+  const float qi = v.rotations[p * 4 + 0], qj = v.rotations[p * 4 + 1];
+  const float qk = v.rotations[p * 4 + 2], qr = v.rotations[p * 4 + 3];
+  const float two_s = 2.0f / ((qi * qi + qj * qj + qk * qk + qr * qr) + 1e-8f);
+  const float R[9] = {1 - two_s * (qj * qj + qk * qk), two_s * (qi * qj - qk * qr),
+                      two_s * (qi * qk + qj * qr),     two_s * (qi * qj + qk * qr),
+                      1 - two_s * (qi * qi + qk * qk), two_s * (qj * qk - qi * qr),
+                      two_s * (qi * qk - qj * qr),     two_s * (qj * qk + qi * qr),
+                      1 - two_s * (qi * qi + qj * qj)};
+  const float s[3] = {v.scales[p * 3 + 0], v.scales[p * 3 + 1], v.scales[p * 3 + 2]};
+  float RS[9], C[9], MC[9], W[9];
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) RS[a * 3 + b] = (R[a * 3 + b] * s[b]) * s[b];
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b)
+      C[a * 3 + b] = RS[a * 3 + 0] * R[b * 3 + 0] + RS[a * 3 + 1] * R[b * 3 + 1] + RS[a * 3 + 2] * R[b * 3 + 2];
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b)
+      MC[a * 3 + b] = M[a * 3 + 0] * C[0 * 3 + b] + M[a * 3 + 1] * C[1 * 3 + b] + M[a * 3 + 2] * C[2 * 3 + b];
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b)
+      W[a * 3 + b] = MC[a * 3 + 0] * M[b * 3 + 0] + MC[a * 3 + 1] * M[b * 3 + 1] + MC[a * 3 + 2] * M[b * 3 + 2];
+  o[3] = W[0]; o[4] = W[1]; o[5] = W[2]; o[6] = W[4]; o[7] = W[5]; o[8] = W[8];
+  // colour: SH2RGB(sh0 + RGB2SH(clamp(img*0.5+0.5)))  (:277-281, :315-318)
+  const int64_t hw = (int64_t)g.H * g.W;
+  for (int c = 0; c < 3; ++c) {
+    float rgb = v.img[c * hw + p] * 0.5f + 0.5f;
+    rgb = fminf(fmaxf(rgb, 0.0f), 1.0f);
+    const float sh0 = v.sh[(p * 3 + c) * v.d_sh] + (rgb - 0.5f) / kC0;
+    o[9 + c] = fminf(fmaxf(sh0 * kC0 + 0.5f, 0.0f), 1.0f);
+  }
+  o[12] = v.opacities[p];
+}
+
+int64_t count_for(const s3w_view* v) {
+  return s3::cdiv(v->H, v->stride) * s3::cdiv(v->W, v->stride);
+}
+
+}  // namespace
+
+extern "C" size_t s3w_workspace_bytes(int64_t n) {
+  if (n <= 0) return 256;
+  return 4 * align256(sizeof(float) * n) + 256 + align256(sort_bytes(n)) + scan_bytes(n);
+}
+
+extern "C" int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, float depth_min,
+                                      float depth_max_percentile, float max_scale,
+                                      float min_confidence, void* workspace, float* out,
+                                      int64_t* count_dev, void* stream) {
+  S3_REQUIRE(v && T_WC && workspace && out && count_dev, "s3w_gaussians_to_world: null argument");
+  S3_REQUIRE(v->H > 0 && v->W > 0 && v->stride >= 1 && v->d_sh >= 1,
+             "s3w_gaussians_to_world: bad view shape");
+  S3_REQUIRE(v->means && v->scales && v->rotations && v->sh && v->opacities && v->img,
+             "s3w_gaussians_to_world: null view tensor");
+  hipStream_t st = s3::as_stream(stream);
+  const int64_t n = count_for(v);
+  S3_REQUIRE(n < (int64_t)1 << 31, "s3w_gaussians_to_world: too many Gaussians");
+  Ws w = carve(workspace, n);
+  Grid g{v->H, v->W, v->stride, (int)s3::cdiv(v->W, v->stride)};
+  Pose T;
+  for (int k = 0; k < 12; ++k) T.m[k] = T_WC[k];
+  const int blocks = (int)s3::cdiv(n, kThreads);
+  S3_HIP(hipMemsetAsync(w.n_valid0, 0, sizeof(uint32_t), st));
+  k_prep<<<blocks, kThreads, 0, st>>>(n, g, v->means, depth_min, w.keys_in, w.n_valid0);
+  S3_LAUNCH_CHECK();
+  const bool use_q = depth_max_percentile < 1.0f;
+  if (use_q) {
+    size_t tb = w.sort_bytes;
+    S3_HIP(hipcub::DeviceRadixSort::SortKeys(w.sort_tmp, tb, w.keys_in, w.keys_out, (int)n, 0,
+                                             32, st));
+  }
+  k_flags<<<blocks, kThreads, 0, st>>>(n, g, v->means, v->scales, v->conf, depth_min,
+                                       use_q ? depth_max_percentile : 1.0f, max_scale,
+                                       min_confidence, w.keys_out, w.n_valid0, w.flags);
+  S3_LAUNCH_CHECK();
+  size_t sb = w.scan_bytes;
+  S3_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, sb, w.flags, w.offsets, (int)n, st));
+  k_emit<<<blocks, kThreads, 0, st>>>(n, g, *v, T, w.flags, w.offsets, out, count_dev);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}

@@ -94,12 +94,18 @@ k_normal_eqs(Pose T, const float* __restrict__ Xf, const float* __restrict__ Xk,
         (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
-__global__ void k_finalize(const float* __restrict__ partial, int nblocks, float* __restrict__ out) {
-  const int k = threadIdx.x;
-  if (k >= NV) return;
+// One workgroup per output value; fixed-order fp64 tree (deterministic).
+__global__ void __launch_bounds__(kThreads)
+k_finalize(const float* __restrict__ partial, int nblocks, float* __restrict__ out) {
+  const int k = blockIdx.x;
   double s = 0.0;
-  for (int b = 0; b < nblocks; ++b) s += (double)partial[b * NV + k];
-  out[k] = (float)s;
+  for (int b = threadIdx.x; b < nblocks; b += kThreads) s += (double)partial[b * NV + k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  __shared__ double red[kThreads / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[k] = (float)((red[0] + red[1]) + (red[2] + red[3]));
 }
 
 int blocks_for(int64_t n) {
@@ -127,7 +133,7 @@ extern "C" int s3t_ray_dist_normal_eqs(const float* T, const float* Xf, const fl
   k_normal_eqs<<<nb, kThreads, 0, st>>>(pose, Xf, Xk, Q, valid, n, 1.0f / sigma_ray,
                                        1.0f / sigma_dist, huber_k, partial);
   S3_LAUNCH_CHECK();
-  k_finalize<<<1, 64, 0, st>>>(partial, nb, out36);
+  k_finalize<<<NV, kThreads, 0, st>>>(partial, nb, out36);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

@@ -94,9 +94,10 @@ def _parr(items: Sequence, n=G):
 
 class Call:
     """A prebuilt library call: fn(*args) with status check."""
-    __slots__ = ("fn", "args", "name", "keep", "kind", "flops")
+    __slots__ = ("fn", "args", "name", "keep", "kind", "flops", "desc")
 
-    def __init__(self, name, *args, keep=(), kind=None, flops=0):
+    def __init__(self, name, *args, keep=(), kind=None, flops=0, desc=""):
+        self.desc = desc             # shape string for per-launch profiles
         self.name = name
         self.kind = kind or name     # roofline bucket (bench.py)
         self.flops = flops           # algorithmic flops of one launch
@@ -159,7 +160,11 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         a.sH, a.sW, a.sS, a.sCout = sH, sW, s, cout
     return Call("s3n_gemm", ctypes.byref(a), keep=(a, A, B, C, bias, R1, R2, C2),
                 kind="gemm.conv" if conv is not None else "gemm.dense",
-                flops=2 * int(M) * int(N) * int(K) * groups)
+                flops=2 * int(M) * int(N) * int(K) * groups,
+                desc=f"gemm{'.conv' if conv is not None else ''} {M}x{N}x{K} g{groups}"
+                     + (f" k{conv['k']}s{conv['stride']}" if conv is not None else "")
+                     + (f" {act}" if act != "none" else "") + (" R1" if R1 else "")
+                     + (f" st={store[0]}" if store else ""))
 
 
 def attention(Q, K, V, O, *, B, Nq, Nk, H, q_stride, k_stride, v_stride, o_stride, qpos=None,
@@ -177,7 +182,8 @@ def attention(Q, K, V, O, *, B, Nq, Nk, H, q_stride, k_stride, v_stride, o_strid
         a.rope_maxpos = rope[0].shape[0]
     a.scale = scale
     return Call("s3n_attention", ctypes.byref(a), keep=(a, Q, K, V, O, qpos, kpos, rope),
-                flops=4 * B * H * Nq * Nk * 64 * len(Q))
+                flops=4 * B * H * Nq * Nk * 64 * len(Q),
+                desc=f"attn B{B} H{H} {Nq}x{Nk} g{len(Q)}")
 
 
 def layernorm(x, gamma, beta, *, rows, C, ldx, eps=1e-6, out16=None, ld16=0, out32=None,
@@ -259,7 +265,8 @@ class Plan:
             e0.record(ts)
             c(st)
             e1.record(ts)
-            out.append((getattr(c, "kind", type(c).__name__), getattr(c, "flops", 0), e0, e1))
+            out.append((getattr(c, "kind", type(c).__name__), getattr(c, "flops", 0), e0, e1,
+                        getattr(c, "desc", "")))
         return out
 
     def capture(self):

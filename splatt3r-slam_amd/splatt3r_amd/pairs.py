@@ -16,7 +16,7 @@ import time
 import torch
 import torch.distributed as dist
 
-from splatt3r_amd.splatt3r_utils import _quat_to_matrix, C0, splatt3r_match_symmetric
+from splatt3r_amd.splatt3r_utils import pose_host12, splatt3r_match_symmetric, world_records
 
 GAUSS_FLOATS = 13   # means 3 + cov_triu 6 + colour 3 + opacity 1 (52 B)
 
@@ -51,22 +51,14 @@ def gather_map(recs: torch.Tensor, ws: int) -> torch.Tensor:
 
 
 def world_gaussians(res, T_WC: torch.Tensor, img: torch.Tensor) -> torch.Tensor:
-    """Per-pixel Gaussians of one predicted view -> [n, 13] world records
-    (means, cov triu, RGB colour, opacity), the transform gaussians_to_world
-    applies (splatt3r_utils.py:290-312) without its filters (stride 1)."""
+    """Per-pixel Gaussians of one predicted view ([H,W,...] dict) -> [h*w, 13]
+    world records (means, cov triu, RGB colour, opacity): the transform of
+    gaussians_to_world (splatt3r_utils.py:290-318) at stride 1 with its
+    filters off, as one HIP pass (include/s3w.h)."""
     from lietorch import Sim3
     M = Sim3(T_WC.reshape(1, 8)).matrix()[0]
-    R, t = M[:3, :3], M[:3, 3]
-    means = res["means"].reshape(-1, 3)
-    sc = res["scales"].reshape(-1, 3)
-    Rq = _quat_to_matrix(res["rotations"].reshape(-1, 4))
-    cov = (Rq * (sc * sc)[:, None, :]) @ Rq.transpose(-1, -2)
-    cov_w = R @ cov @ R.T
-    iu = torch.triu_indices(3, 3, device=means.device)
-    rgb = (img[0] * 0.5 + 0.5).clamp(0, 1).permute(1, 2, 0).reshape(-1, 3)
-    sh0 = res["sh"].reshape(-1, 3) + (rgb - 0.5) / C0
-    return torch.cat([means @ R.T + t, cov_w[:, iu[0], iu[1]], (sh0 * C0 + 0.5).clamp(0, 1),
-                      res["opacities"].reshape(-1, 1)], 1)
+    out, _ = world_records(res, img[0] if img.dim() == 4 else img, pose_host12(M))
+    return out
 
 
 @torch.inference_mode()

@@ -9,18 +9,20 @@ Differences in HOW, not WHAT:
     build_covariance + RGB2SH residual + scale-invariant rescale + triu)
     into the HIP rasterizer, instead of ~20 torch ops + render_cuda; same
     camera math (:332-432 -> decoder_splatting_cuda.py:30-83).
-  * `gaussians_to_world()` keeps the reference's torch formulation
-    (:180-328); its fusion into HIP kernels is §8(f) f2.
+  * `gaussians_to_world()` is one HIP pass per view (include/s3w.h:
+    strided gather, torch.quantile-exact depth bound, filters, stable
+    compaction, world transform) instead of ~40 torch ops (:180-328).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
 import torch
 
 import lietorch
-from splatt3r_amd import matching
+from splatt3r_amd import _lib, matching
 from splatt3r_amd.config import config
 from splatt3r_amd.render import (DecoderSplattingCUDA, camera_settings, normalize_intrinsics,
                                  pack_splats)
@@ -248,46 +250,92 @@ def splatt3r_render(model, frame, ref_frame, K=None, target_T_WC=None):
     return image[None, None]
 
 
+class S3wView(ctypes.Structure):
+    _fields_ = [("means", ctypes.c_void_p), ("scales", ctypes.c_void_p),
+                ("rotations", ctypes.c_void_p), ("sh", ctypes.c_void_p),
+                ("opacities", ctypes.c_void_p), ("conf", ctypes.c_void_p),
+                ("img", ctypes.c_void_p), ("H", ctypes.c_int), ("W", ctypes.c_int),
+                ("d_sh", ctypes.c_int), ("stride", ctypes.c_int)]
+
+
+_P = ctypes.c_void_p
+_lib.register({
+    "s3w_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "s3w_gaussians_to_world": (ctypes.c_int, [ctypes.POINTER(S3wView), _P, ctypes.c_float,
+                                              ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                              _P, _P, _P, _P]),
+})
+_WS: dict = {}
+
+
+def _workspace(dev, n):
+    need = _lib.lib().s3w_workspace_bytes(n)
+    ws = _WS.get(dev)
+    if ws is None or ws.numel() < need:
+        ws = _WS[dev] = torch.empty(need, dtype=torch.uint8, device=dev)
+    return ws
+
+
+def world_records(view, img, T, stride=1, depth_min=float("-inf"), depth_max_percentile=1.0,
+                  max_scale=float("inf"), min_confidence=0.0):
+    """One predicted view ([H,W,...] tensors: means, scales, rotations, sh,
+    opacities[, conf]) + its [3,H,W] ImgNorm image -> ([n,13] world records,
+    device int64 count), stream-ordered (include/s3w.h).  T: host float[12]
+    (s R row-major, t).  Defaults disable every filter."""
+    H, W, _ = view["means"].shape
+    d_sh = view["sh"].shape[-1]
+    n = -(-H // stride) * -(-W // stride)
+    t = {k: view[k].float().contiguous() for k in
+         ("means", "scales", "rotations", "sh", "opacities")}
+    conf = view["conf"].float().contiguous() if view.get("conf") is not None else None
+    im = img.float().contiguous()
+    _lib.require_cuda(*t.values(), im)
+    v = S3wView(t["means"].data_ptr(), t["scales"].data_ptr(), t["rotations"].data_ptr(),
+                t["sh"].data_ptr(), t["opacities"].data_ptr(),
+                conf.data_ptr() if conf is not None else None, im.data_ptr(), H, W, d_sh, stride)
+    out = torch.empty(n, 13, device=im.device)
+    cnt = torch.empty(1, dtype=torch.int64, device=im.device)
+    ws = _workspace(im.device, n)
+    _lib.call("s3w_gaussians_to_world", ctypes.byref(v), T, float(depth_min),
+              float(depth_max_percentile), float(max_scale), float(min_confidence),
+              ws.data_ptr(), out.data_ptr(), cnt.data_ptr(), _lib.stream(im.device))
+    return out, cnt
+
+
+def pose_host12(M):
+    """[4,4] (s R | t) -> ctypes float[12] for world_records."""
+    M = M.detach().float().cpu()
+    return (ctypes.c_float * 12)(*M[:3, :3].reshape(-1).tolist(), *M[:3, 3].tolist())
+
+
 @torch.inference_mode()
 def gaussians_to_world(frame, include_cross=True, spatial_stride=1, depth_min=0.05,
                        depth_max_percentile=0.98, max_scale=0.5, min_confidence=1.5):
-    """splatt3r_utils.py:180-328 -> (means_world, cov_triu, colors, opacities)."""
+    """splatt3r_utils.py:180-328 -> (means_world [G,3], cov_triu [G,6],
+    colors [G,3], opacities [G]); one HIP pass per view (include/s3w.h)
+    and a single host sync for the record counts."""
     if frame.gaussian_pred is None:
         return None
-    M = _sim3_to_4x4(frame.T_WC)[0]
-    R, t = M[:3, :3].to(frame.gaussian_pred["means"].device), M[:3, 3]
+    T = pose_host12(_sim3_to_4x4(frame.T_WC)[0])
     preds = [frame.gaussian_pred]
     if include_cross and frame.gaussian_pred_cross is not None:
         preds.append(frame.gaussian_pred_cross)
     s = max(1, int(spatial_stride))
-    row, col = torch.triu_indices(3, 3)
-    outs = []
+    img = frame.img
+    outs, counts = [], []
     for pred in preds:
-        means = pred["means"][:, ::s, ::s, :].reshape(-1, 3)
-        scales = pred["scales"][:, ::s, ::s, :].reshape(-1, 3)
-        rots = pred["rotations"][:, ::s, ::s, :].reshape(-1, 4)
-        sh0 = pred["sh"][:, ::s, ::s, :, 0].reshape(-1, 3)
-        opas = pred["opacities"][:, ::s, ::s, :].reshape(-1)
-        conf = pred["conf"][:, ::s, ::s].reshape(-1) if "conf" in pred else None
-        img = (frame.img * 0.5 + 0.5).clamp(0, 1)[:, :, ::s, ::s]
-        sh0 = sh0 + (img[0].permute(1, 2, 0).reshape(-1, 3) - 0.5) / C0   # RGB2SH
-        z = means[:, 2]
-        valid = z > depth_min
-        if bool(valid.any()) and depth_max_percentile < 1.0:
-            valid = valid & (z <= torch.quantile(z[valid], depth_max_percentile))
-        valid = valid & (scales.max(dim=-1).values < max_scale)
-        if conf is not None and min_confidence > 0:
-            valid = valid & (conf >= min_confidence)
-        means, scales, rots, sh0, opas = (x[valid] for x in (means, scales, rots, sh0, opas))
-        if means.shape[0] == 0:
-            continue
-        Rq = _quat_to_matrix(rots)
-        cov = Rq @ torch.diag_embed(scales ** 2) @ Rq.transpose(-1, -2)
-        cov_w = R @ cov @ R.T
-        outs.append(((R @ means.T).T + t, cov_w[:, row, col], (sh0 * C0 + 0.5).clamp(0, 1), opas))
-    if not outs:
+        for b in range(pred["means"].shape[0]):
+            view = {k: v[b] for k, v in pred.items()}
+            out, cnt = world_records(view, img[min(b, img.shape[0] - 1)], T, s, depth_min,
+                                     depth_max_percentile, max_scale, min_confidence)
+            outs.append(out)
+            counts.append(cnt)
+    counts = torch.cat(counts).tolist()
+    recs = torch.cat([o[:c] for o, c in zip(outs, counts)]) if sum(counts) else None
+    if recs is None:
         return None
-    return tuple(torch.cat(x, 0) for x in zip(*outs))
+    return (recs[:, 0:3].contiguous(), recs[:, 3:9].contiguous(), recs[:, 9:12].contiguous(),
+            recs[:, 12].contiguous())
 
 
 def _quat_to_matrix(q, eps: float = 1e-8):

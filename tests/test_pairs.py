@@ -56,6 +56,7 @@ def test_gather_map_world_size_2_gloo():
         np.testing.assert_array_equal(res[r], want)
 
 
+@pytest.mark.gpu
 def test_world_gaussians_matches_numpy():
     from splatt3r_amd.pairs import world_gaussians
     rng = np.random.default_rng(0)
@@ -69,7 +70,8 @@ def test_world_gaussians_matches_numpy():
                opacities=torch.from_numpy(rng.uniform(size=(1, h, w, 1)).astype(np.float32)))
     T = torch.tensor([0.1, -0.2, 0.3, 0.0, 0.0, np.sin(0.2), np.cos(0.2), 1.5])
     img = torch.from_numpy(rng.uniform(-1, 1, (1, 3, h, w)).astype(np.float32))
-    out = world_gaussians(res, T, img).numpy()
+    out = world_gaussians({k: v[0].cuda() for k, v in res.items()}, T.cuda(), img.cuda())
+    out = out.cpu().numpy()
     # numpy restatement of splatt3r_utils.py:290-312
     c, s_ = np.cos(0.4), np.sin(0.4)
     R = np.array([[c, -s_, 0], [s_, c, 0], [0, 0, 1]]) * 1.5
