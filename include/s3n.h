@@ -72,8 +72,28 @@ typedef struct {
   int cH, cW, cC, ksize, stride, pad, oH, oW, relu_in;
   /* scatter stores: token grid sH x sW, factor s, output channels sCout */
   int sH, sW, sS, sCout;
+  /* split-K: split_k > 1 partitions the K tiles over split_k workgroups per
+   * output tile; fp32 partials go to `workspace` (s3n_gemm_workspace_bytes)
+   * and a second launch sums them in split order (deterministic) and
+   * applies the epilogue.  tile: 0 = auto, 1 = 64x64, 2 = 64x128,
+   * 3 = 128x128. */
+  int split_k;
+  int tile;
+  void* workspace;
+  /* RoPE2D epilogue (pos_embed.py:142-159, head_dim 64): when rope_pos[g]
+   * is set, output columns [0, rope_ncols) are treated as heads of 64 and
+   * rotated after the bias, with row positions rope_pos[g][row] = (y, x)
+   * (int64) and tables cos/sin [rope_maxpos, 16] (dims [0,32) of a head use
+   * y, [32,64) use x; d pairs with d+16 inside each half).  Requires
+   * split_k <= 1, rope_ncols % 64 == 0. */
+  const float* rope_cos;
+  const float* rope_sin;
+  int rope_maxpos;
+  int rope_ncols;
+  const int64_t* rope_pos[S3N_MAX_GROUPS];
 } s3n_gemm_args;
 
+size_t s3n_gemm_workspace_bytes(const s3n_gemm_args* args);
 int s3n_gemm(const s3n_gemm_args* args, void* stream);
 
 /* Fused multi-head attention softmax(Q K^T * scale) V with 2-D RoPE

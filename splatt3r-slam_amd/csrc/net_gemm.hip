@@ -43,6 +43,13 @@ struct GemmP {
   int cH, cW, cC, ks, st, pad, oH, oW, relu_in;
   int sH, sW, sS, sCout;
   int tiles_m, tiles_n;
+  int split_k, kt_per_split;
+  float* ws;
+  int col_major;   // tile order: 1 = M fastest (each XCD owns a band of N)
+  const float* rope_cos;
+  const float* rope_sin;
+  int rope_ncols;
+  const int64_t* rope_pos[S3N_MAX_GROUPS];
 };
 
 __device__ __forceinline__ int swz(int row, int kc) { return (kc ^ ((row >> 1) & 7)); }
@@ -57,101 +64,173 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
 }
 
-template <int BM, int BN, int AMODE>
+// A operand modes of the kernel template (AMODE): dense rows, implicit-im2col
+// conv, implicit-im2col conv with ReLU applied to the A fragments.
+constexpr int kDense = 0, kConv = 1, kConvRelu = 2;
+
+// Zero source for out-of-range LDS-DMA lanes (padding taps, M/N/K tails).
+__device__ __attribute__((aligned(64))) f16 g_zero[64];
+
+#define S3_GLDS(gptr, lptr)                                                          \
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(gptr), \
+                                   (__attribute__((address_space(3))) void*)(lptr), 16, 0, 0)
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// bias -> act -> + R1 -> + R2 -> store (plain / ConvT / pixel-shuffle
+// scatter) -> optional fp16 copy, for one output element.
+template <bool kBias = true>
+__device__ __forceinline__ void epilogue(const GemmP& p, int g, int row, int col, float v) {
+  const float* __restrict__ bias = p.bias[g];
+  const void* R1 = p.R1[g];
+  const void* R2 = p.R2[g];
+  void* C = p.C[g];
+  f16* C2 = p.C2[g];
+  if (kBias && bias) v += bias[col];
+  if (p.act == S3N_ACT_GELU) v = gelu(v);
+  else if (p.act == S3N_ACT_RELU) v = fmaxf(v, 0.0f);
+  if (R1) {
+    const int64_t o = (int64_t)row * p.ldr1 + col;
+    v += p.r1_f16 ? (float)reinterpret_cast<const f16*>(R1)[o] : reinterpret_cast<const float*>(R1)[o];
+  }
+  if (R2) {
+    const int64_t o = (int64_t)row * p.ldr2 + col;
+    v += p.r2_f16 ? (float)reinterpret_cast<const f16*>(R2)[o] : reinterpret_cast<const float*>(R2)[o];
+  }
+  int64_t off;
+  if (p.store_mode == S3N_STORE_PLAIN) {
+    off = (int64_t)row * p.ldc + col;
+  } else {
+    // row = token (b, ty, tx) on an sH x sW grid; col -> (i, j, co)
+    const int tx = row % p.sW, t = row / p.sW, ty = t % p.sH, b = t / p.sH;
+    int i, j, co;
+    if (p.store_mode == S3N_STORE_CONVT) {
+      co = col % p.sCout;
+      const int ij = col / p.sCout;
+      i = ij / p.sS;
+      j = ij % p.sS;
+    } else {
+      co = col / (p.sS * p.sS);
+      const int ij = col % (p.sS * p.sS);
+      i = ij / p.sS;
+      j = ij % p.sS;
+    }
+    const int64_t oy = (int64_t)ty * p.sS + i, ox = (int64_t)tx * p.sS + j;
+    off = (((int64_t)b * p.sH * p.sS + oy) * ((int64_t)p.sW * p.sS) + ox) * p.sCout + co;
+  }
+  if (p.c_f16) reinterpret_cast<f16*>(C)[off] = (f16)v;
+  else reinterpret_cast<float*>(C)[off] = v;
+  if (C2) C2[(int64_t)row * p.ldc2 + col] = (f16)v;
+}
+
+template <int BM, int BN, int AMODE, int kStages>
 __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int FM = WM / 32, FN = WN / 32;
-  constexpr int AC = BM / 32, BC = BN / 32;  // 16-B chunks per thread per tile
-  __shared__ __attribute__((aligned(16))) f16 smem[2 * (BM + BN) * BK];
+  // One LDS-DMA wave instruction moves 64 lanes x 16 B = 8 rows of the
+  // 128-B (BK = 64 fp16) tile rows.  Each wave issues AW + BW per K tile.
+  constexpr int AW = BM / 8 / 4, BW = BN / 8 / 4;
+  constexpr int PERW = AW + BW;
+  constexpr int STAGE = (BM + BN) * BK;
+  __shared__ __attribute__((aligned(1024))) f16 smem[kStages * STAGE];
 
   const int g = blockIdx.z;
   const int nwg = p.tiles_m * p.tiles_n;
   const int tile = xcd_remap(blockIdx.x, nwg);
-  const int tm = tile / p.tiles_n, tn = tile % p.tiles_n;
+  // xcd_remap gives each XCD a contiguous run of tile ids; the order makes
+  // that run share the larger operand (its slice stays in the XCD's L2).
+  const int tm = p.col_major ? tile % p.tiles_m : tile / p.tiles_n;
+  const int tn = p.col_major ? tile / p.tiles_m : tile % p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int M = p.M, N = p.N, K = p.K;
   const f16* __restrict__ A = p.A[g];
   const f16* __restrict__ B = p.B[g];
+  const int KT_all = (K + BK - 1) / BK;
+  const int kt_begin = blockIdx.y * p.kt_per_split;
+  const int kt_end = min(KT_all, kt_begin + p.kt_per_split);
 
-  // Per-thread staging rows are fixed across K tiles.
-  int a_row[AC], a_kc[AC];
-  const f16* a_base[AC];
-  int a_iy0[AC], a_ix0[AC];
-  bool a_ok[AC];
+  // Lane -> (row within its 8-row group, LDS chunk); the global k chunk is
+  // pre-swizzled so the LDS image is the XOR-swizzled layout the fragment
+  // reads expect (swz is an involution).
+  const int lrow = lane >> 3, lchunk = lane & 7;
+  const f16* a_src[AW];
+  int a_iy0[AW], a_ix0[AW];
+  bool a_ok[AW];
+  int a_kc[AW];
+  // conv: per-row (tap, ci, ky, kx) of the lane's current k, advanced by BK
+  // per issued tile (no integer division in the K loop)
+  int c_ci[AW], c_ky[AW], c_kx[AW];
 #pragma unroll
-  for (int i = 0; i < AC; ++i) {
-    const int c = tid + i * kThreads;
-    a_row[i] = c >> 3;
-    a_kc[i] = c & 7;
-    const int m = m0 + a_row[i];
-    a_ok[i] = m < M;
-    if constexpr (AMODE == S3N_A_DENSE) {
-      a_base[i] = A + (int64_t)(a_ok[i] ? m : 0) * p.lda;
-      a_iy0[i] = a_ix0[i] = 0;
+  for (int j = 0; j < AW; ++j) {
+    const int r = (wave * AW + j) * 8 + lrow;
+    a_kc[j] = swz(r, lchunk);
+    const int m = m0 + r;
+    a_ok[j] = m < M;
+    const int mm = a_ok[j] ? m : 0;
+    if constexpr (AMODE == kDense) {
+      a_src[j] = A + (int64_t)mm * p.lda + a_kc[j] * 8;
+      a_iy0[j] = a_ix0[j] = 0;
     } else {
-      const int mm = a_ok[i] ? m : 0;
       const int ox = mm % p.oW, t = mm / p.oW, oy = t % p.oH, b = t / p.oH;
-      a_base[i] = A + (int64_t)b * p.cH * p.cW * p.cC;
-      a_iy0[i] = oy * p.st - p.pad;
-      a_ix0[i] = ox * p.st - p.pad;
+      a_src[j] = A + (int64_t)b * p.cH * p.cW * p.cC;
+      a_iy0[j] = oy * p.st - p.pad;
+      a_ix0[j] = ox * p.st - p.pad;
+      const int k = kt_begin * BK + a_kc[j] * 8, tap = k / p.cC;
+      c_ci[j] = k - tap * p.cC;
+      c_ky[j] = tap / p.ks;
+      c_kx[j] = tap - c_ky[j] * p.ks;
     }
   }
-  int b_row[BC], b_kc[BC];
-  bool b_ok[BC];
+  const f16* b_src[BW];
+  bool b_ok[BW];
+  int b_kc[BW];
 #pragma unroll
-  for (int i = 0; i < BC; ++i) {
-    const int c = tid + i * kThreads;
-    b_row[i] = c >> 3;
-    b_kc[i] = c & 7;
-    b_ok[i] = (n0 + b_row[i]) < N;
+  for (int j = 0; j < BW; ++j) {
+    const int r = (wave * BW + j) * 8 + lrow;
+    b_kc[j] = swz(r, lchunk);
+    b_ok[j] = (n0 + r) < N;
+    b_src[j] = B + (int64_t)(b_ok[j] ? n0 + r : 0) * p.ldb + b_kc[j] * 8;
   }
 
-  f16x8 ra[AC], rb[BC];
-  const f16x8 zero8 = {};
-
-  auto gload = [&](int k0) {
+  // Issue the LDS-DMA loads of K tile kt into stage st (tiles are issued in
+  // order kt = 0, 1, 2, ...: the conv state advances one tile per call).
+  auto issue = [&](int kt, int st) {
+    f16* As = smem + st * STAGE;
+    f16* Bs = As + BM * BK;
+    const int k0 = kt * BK;
 #pragma unroll
-    for (int i = 0; i < AC; ++i) {
-      const int k = k0 + a_kc[i] * 8;
-      f16x8 v = zero8;
-      if (a_ok[i] && k < K) {
-        if constexpr (AMODE == S3N_A_DENSE) {
-          v = *reinterpret_cast<const f16x8*>(a_base[i] + k);
-        } else {
-          const int tap = k / p.cC, ci = k - tap * p.cC;
-          const int ky = tap / p.ks, kx = tap - ky * p.ks;
-          const int iy = a_iy0[i] + ky, ix = a_ix0[i] + kx;
-          if (iy >= 0 && iy < p.cH && ix >= 0 && ix < p.cW) {
-            v = *reinterpret_cast<const f16x8*>(a_base[i] + ((int64_t)iy * p.cW + ix) * p.cC + ci);
-            if (p.relu_in) {
-#pragma unroll
-              for (int j = 0; j < 8; ++j) v[j] = v[j] > (f16)0 ? v[j] : (f16)0;
-            }
-          }
+    for (int j = 0; j < AW; ++j) {
+      const int k = k0 + a_kc[j] * 8;
+      const f16* src = g_zero;
+      if constexpr (AMODE == kDense) {
+        if (a_ok[j] && k < K) src = a_src[j] + k0;
+      } else {
+        if (a_ok[j] && k < K) {
+          const int iy = a_iy0[j] + c_ky[j], ix = a_ix0[j] + c_kx[j];
+          if (iy >= 0 && iy < p.cH && ix >= 0 && ix < p.cW)
+            src = a_src[j] + ((int64_t)iy * p.cW + ix) * p.cC + c_ci[j];
+        }
+        c_ci[j] += BK;
+        while (c_ci[j] >= p.cC) {
+          c_ci[j] -= p.cC;
+          if (++c_kx[j] == p.ks) { c_kx[j] = 0; ++c_ky[j]; }
         }
       }
-      ra[i] = v;
+      S3_GLDS(src, As + (wave * AW + j) * 512);
     }
 #pragma unroll
-    for (int i = 0; i < BC; ++i) {
-      const int k = k0 + b_kc[i] * 8;
-      f16x8 v = zero8;
-      if (b_ok[i] && k < K)
-        v = *reinterpret_cast<const f16x8*>(B + (int64_t)(n0 + b_row[i]) * p.ldb + k);
-      rb[i] = v;
+    for (int j = 0; j < BW; ++j) {
+      const int k = k0 + b_kc[j] * 8;
+      const f16* src = (b_ok[j] && k < K) ? b_src[j] + k0 : g_zero;
+      S3_GLDS(src, Bs + (wave * BW + j) * 512);
     }
-  };
-  auto sstore = [&](int buf) {
-    f16* As = smem + buf * (BM + BN) * BK;
-    f16* Bs = As + BM * BK;
-#pragma unroll
-    for (int i = 0; i < AC; ++i)
-      *reinterpret_cast<f16x8*>(As + a_row[i] * BK + swz(a_row[i], a_kc[i]) * 8) = ra[i];
-#pragma unroll
-    for (int i = 0; i < BC; ++i)
-      *reinterpret_cast<f16x8*>(Bs + b_row[i] * BK + swz(b_row[i], b_kc[i]) * 8) = rb[i];
   };
 
   f32x16 acc[FM][FN];
@@ -162,14 +241,26 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  const int KT = (K + BK - 1) / BK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
+  // kStages-deep ring: tiles kt+1 .. kt+kStages-2 stay in flight while
+  // tile kt is consumed; one raw barrier per K tile.
+  constexpr int AHEAD = kStages - 1;
+  const int KT = kt_end - kt_begin;   // this workgroup's K tiles
+#pragma unroll
+  for (int i = 0; i < AHEAD; ++i)
+    if (i < KT) issue(kt_begin + i, i);
   for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) gload((kt + 1) * BK);
-    const f16* As = smem + cur * (BM + BN) * BK;
+    // Tile kt has landed once at most AHEAD-1 newer tiles are in flight.
+    if constexpr (AHEAD == 2) {
+      if (kt + 1 < KT) wait_vmcnt<PERW>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    // Everyone's DMA for tile kt is visible, and everyone finished reading
+    // the stage that tile kt+AHEAD overwrites (read during iteration kt-1).
+    __builtin_amdgcn_s_barrier();
+    if (kt + AHEAD < KT) issue(kt_begin + kt + AHEAD, (kt + AHEAD) % kStages);
+    const f16* As = smem + (kt % kStages) * STAGE;
     const f16* Bs = As + BM * BK;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
@@ -179,6 +270,10 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
       for (int fm = 0; fm < FM; ++fm) {
         const int row = wm * WM + fm * 32 + (lane & 31);
         af[fm] = *reinterpret_cast<const f16x8*>(As + row * BK + swz(row, kc) * 8);
+        if constexpr (AMODE == kConvRelu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) af[fm][e] = af[fm][e] > (f16)0 ? af[fm][e] : (f16)0;
+        }
       }
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
@@ -191,81 +286,103 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
         for (int fn = 0; fn < FN; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
     }
-    if (kt + 1 < KT) sstore(cur ^ 1);
-    __syncthreads();
   }
 
   // ---- epilogue ----
-  const float* __restrict__ bias = p.bias[g];
-  const void* R1 = p.R1[g];
-  const void* R2 = p.R2[g];
-  void* C = p.C[g];
-  f16* C2 = p.C2[g];
+  const int s_idx = blockIdx.y;
+  if (p.rope_pos[g]) {
+    // bias, then RoPE: the partner column (col ^ 16, same rows) sits in lane
+    // ^ 16 of the same 32x32 accumulator, so one xor-shuffle fetches it.
+    const int64_t* __restrict__ pos = p.rope_pos[g];
+    const float* __restrict__ bias = p.bias[g];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int col = n0 + wn * WN + fn * 32 + (lane & 31);
+        const float bv = (bias && col < N) ? bias[col] : 0.0f;
+        const int d = col & 63, j = col & 15;
+        const bool lo = (col & 31) < 16, rot = col < p.rope_ncols;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * WM + fm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          float x = acc[fm][fn][r] + bv;
+          const float xp = __shfl_xor(x, 16, 64);
+          if (row >= M || col >= N) continue;
+          if (rot) {
+            const int64_t ps = pos[(int64_t)row * 2 + (d >> 5)];
+            const float cs = p.rope_cos[ps * 16 + j], sn = p.rope_sin[ps * 16 + j];
+            x = lo ? x * cs - xp * sn : x * cs + xp * sn;
+          }
+          epilogue<false>(p, g, row, col, x);
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       const int col = n0 + wn * WN + fn * 32 + (lane & 31);
       if (col >= N) continue;
-      const float bv = bias ? bias[col] : 0.0f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * WM + fm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (row >= M) continue;
-        float v = acc[fm][fn][r] + bv;
-        if (p.act == S3N_ACT_GELU) v = gelu(v);
-        else if (p.act == S3N_ACT_RELU) v = fmaxf(v, 0.0f);
-        if (R1) {
-          const int64_t o = (int64_t)row * p.ldr1 + col;
-          v += p.r1_f16 ? (float)reinterpret_cast<const f16*>(R1)[o] : reinterpret_cast<const float*>(R1)[o];
-        }
-        if (R2) {
-          const int64_t o = (int64_t)row * p.ldr2 + col;
-          v += p.r2_f16 ? (float)reinterpret_cast<const f16*>(R2)[o] : reinterpret_cast<const float*>(R2)[o];
-        }
-        int64_t off;
-        if (p.store_mode == S3N_STORE_PLAIN) {
-          off = (int64_t)row * p.ldc + col;
-        } else {
-          // row = token (b, ty, tx) on an sH x sW grid; col -> (i, j, co)
-          const int tx = row % p.sW, t = row / p.sW, ty = t % p.sH, b = t / p.sH;
-          int i, j, co;
-          if (p.store_mode == S3N_STORE_CONVT) {
-            co = col % p.sCout;
-            const int ij = col / p.sCout;
-            i = ij / p.sS;
-            j = ij % p.sS;
-          } else {
-            co = col / (p.sS * p.sS);
-            const int ij = col % (p.sS * p.sS);
-            i = ij / p.sS;
-            j = ij % p.sS;
-          }
-          const int64_t oy = (int64_t)ty * p.sS + i, ox = (int64_t)tx * p.sS + j;
-          off = (((int64_t)b * p.sH * p.sS + oy) * ((int64_t)p.sW * p.sS) + ox) * p.sCout + co;
-        }
-        if (p.c_f16) reinterpret_cast<f16*>(C)[off] = (f16)v;
-        else reinterpret_cast<float*>(C)[off] = v;
-        if (C2) C2[(int64_t)row * p.ldc2 + col] = (f16)v;
+        if (p.split_k > 1)
+          p.ws[(((int64_t)g * p.split_k + s_idx) * M + row) * N + col] = acc[fm][fn][r];
+        else
+          epilogue(p, g, row, col, acc[fm][fn][r]);
       }
     }
 }
 
-template <int BM, int BN>
+// Split-K combine: sum the partial planes in split order, then the epilogue.
+__global__ void __launch_bounds__(kThreads) k_splitk_reduce(GemmP p) {
+  const int g = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t MN = (int64_t)p.M * p.N;
+  if (i >= MN) return;
+  const float* w = p.ws + (int64_t)g * p.split_k * MN + i;
+  float v = w[0];
+  for (int s = 1; s < p.split_k; ++s) v += w[s * MN];
+  epilogue(p, g, (int)(i / p.N), (int)(i % p.N), v);
+}
+
+template <int BM, int BN, int S>
 int launch(const GemmP& p, hipStream_t st) {
   GemmP q = p;
   q.tiles_m = (p.M + BM - 1) / BM;
   q.tiles_n = (p.N + BN - 1) / BN;
-  dim3 grid(q.tiles_m * q.tiles_n, 1, p.groups);
+  const int KT = (p.K + BK - 1) / BK;
+  q.split_k = p.split_k > 1 ? p.split_k : 1;
+  q.kt_per_split = (KT + q.split_k - 1) / q.split_k;
+  q.split_k = (KT + q.kt_per_split - 1) / q.kt_per_split;   // no empty splits
+  const int64_t a_bytes = p.a_mode == S3N_A_DENSE ? (int64_t)p.M * p.K
+                                                  : (int64_t)p.M / (p.oH * p.oW) * p.cH * p.cW * p.cC;
+  q.col_major = (int64_t)p.N * p.K > a_bytes;
+  dim3 grid(q.tiles_m * q.tiles_n, q.split_k, p.groups);
   if (p.a_mode == S3N_A_DENSE)
-    k_gemm<BM, BN, S3N_A_DENSE><<<grid, kThreads, 0, st>>>(q);
+    k_gemm<BM, BN, kDense, S><<<grid, kThreads, 0, st>>>(q);
+  else if (p.relu_in)
+    k_gemm<BM, BN, kConvRelu, S><<<grid, kThreads, 0, st>>>(q);
   else
-    k_gemm<BM, BN, S3N_A_CONV><<<grid, kThreads, 0, st>>>(q);
+    k_gemm<BM, BN, kConv, S><<<grid, kThreads, 0, st>>>(q);
   S3_LAUNCH_CHECK();
+  if (q.split_k > 1) {
+    dim3 rg((unsigned)s3::cdiv((int64_t)p.M * p.N, kThreads), p.groups);
+    k_splitk_reduce<<<rg, kThreads, 0, st>>>(q);
+    S3_LAUNCH_CHECK();
+  }
   return S3_OK;
 }
 
 }  // namespace
+
+extern "C" size_t s3n_gemm_workspace_bytes(const s3n_gemm_args* a) {
+  if (!a || a->split_k <= 1) return 0;
+  return sizeof(float) * (size_t)a->groups * a->split_k * (size_t)a->M * a->N;
+}
 
 extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   S3_REQUIRE(a && a->M >= 0 && a->N > 0 && a->K > 0, "s3n_gemm: bad sizes");
@@ -299,12 +416,36 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   p.cH = a->cH; p.cW = a->cW; p.cC = a->cC; p.ks = a->ksize; p.st = a->stride; p.pad = a->pad;
   p.oH = a->oH; p.oW = a->oW; p.relu_in = a->relu_in;
   p.sH = a->sH; p.sW = a->sW; p.sS = a->sS; p.sCout = a->sCout;
+  p.split_k = a->split_k > 1 ? a->split_k : 1;
+  p.rope_cos = a->rope_cos;
+  p.rope_sin = a->rope_sin;
+  p.rope_ncols = a->rope_ncols;
+  bool any_rope = false;
+  for (int g = 0; g < S3N_MAX_GROUPS; ++g) {
+    p.rope_pos[g] = g < a->groups ? a->rope_pos[g] : nullptr;
+    any_rope = any_rope || p.rope_pos[g];
+  }
+  if (any_rope) {
+    S3_REQUIRE(p.split_k == 1 && a->rope_cos && a->rope_sin && a->rope_ncols % 64 == 0 &&
+                   a->rope_ncols <= a->N && a->store_mode == S3N_STORE_PLAIN,
+               "s3n_gemm: RoPE epilogue needs split_k 1, tables, ncols %% 64 == 0, plain store");
+    for (int g = 0; g < a->groups; ++g)
+      S3_REQUIRE(a->rope_pos[g], "s3n_gemm: RoPE positions missing for group %d", g);
+  }
+  p.ws = static_cast<float*>(a->workspace);
+  if (p.split_k > 1)
+    S3_REQUIRE(p.ws, "s3n_gemm: split_k > 1 needs a workspace (s3n_gemm_workspace_bytes)");
   hipStream_t st = s3::as_stream(stream);
+  if (a->tile == 1) return launch<64, 64, 3>(p, st);
+  if (a->tile == 2) return launch<64, 128, 3>(p, st);
+  if (a->tile == 3) return launch<128, 128, 2>(p, st);
   // Tile choice: fill the 256 CUs before growing the tile.
   auto tiles = [&](int bm, int bn) {
     return (int64_t)a->groups * ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
   };
-  if (tiles(128, 128) >= 240) return launch<128, 128>(p, st);
-  if (tiles(64, 128) >= 200 && a->N >= 128) return launch<64, 128>(p, st);
-  return launch<64, 64>(p, st);
+  // LDS: 128x128 x 2 stages = 64 KB (2 WG/CU), 64x128 x 3 = 72 KB (2),
+  // 64x64 x 3 = 48 KB (3).
+  if (tiles(128, 128) >= 512) return launch<128, 128, 2>(p, st);
+  if (tiles(64, 128) >= 384 && a->N >= 128) return launch<64, 128, 3>(p, st);
+  return launch<64, 64, 3>(p, st);
 }

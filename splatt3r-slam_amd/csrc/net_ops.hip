@@ -34,14 +34,21 @@ __global__ void __launch_bounds__(kThreads) k_layernorm(LnP p) {
   const int lane = threadIdx.x & 63;
   if (row >= p.rows) return;
   const float* x = p.x[g] + (int64_t)row * p.ldx;
-  f32x4 v[VPL];
+  const float* gm = p.gamma[g];
+  const float* bt = p.beta[g];
+  f32x4 v[VPL], gg[VPL], bb[VPL];
   float s = 0.f;
+  // gamma/beta are issued with x so their latency overlaps the reductions
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = (i * 64 + lane) * 4;
-    v[i] = c < p.C ? *reinterpret_cast<const f32x4*>(x + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+    const bool in = c < p.C;
+    v[i] = in ? *reinterpret_cast<const f32x4*>(x + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    gg[i] = in ? *reinterpret_cast<const f32x4*>(gm + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bb[i] = in ? *reinterpret_cast<const f32x4*>(bt + c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   const float mean = s / p.C;
@@ -59,23 +66,20 @@ __global__ void __launch_bounds__(kThreads) k_layernorm(LnP p) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
   const float rstd = rsqrtf(q / p.C + p.eps);
-  const float* gm = p.gamma[g];
-  const float* bt = p.beta[g];
   f16* o16 = p.o16[g];
   float* o32 = p.o32[g];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = (i * 64 + lane) * 4;
     if (c >= p.C) continue;
-    const f32x4 gg = *reinterpret_cast<const f32x4*>(gm + c);
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(bt + c);
     f32x4 y;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) y[j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
+    for (int j = 0; j < 4; ++j) y[j] = (v[i][j] - mean) * rstd * gg[i][j] + bb[i][j];
     if (o32) *reinterpret_cast<f32x4*>(o32 + (int64_t)row * p.ld32 + c) = y;
     if (o16) {
-      f16* d = o16 + (int64_t)row * p.ld16 + c;
-      d[0] = (f16)y[0]; d[1] = (f16)y[1]; d[2] = (f16)y[2]; d[3] = (f16)y[3];
+      typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+      const f16x4 h = {(f16)y[0], (f16)y[1], (f16)y[2], (f16)y[3]};
+      *reinterpret_cast<f16x4*>(o16 + (int64_t)row * p.ld16 + c) = h;
     }
   }
 }
@@ -222,7 +226,8 @@ int s3n_layernorm(int rows, int C, int groups, const float* const* x, int64_t ld
                   void* stream) {
   S3_REQUIRE(rows >= 0 && C > 0 && C % 4 == 0 && C <= 2048, "s3n_layernorm: C must be 4..2048, %%4");
   S3_REQUIRE(groups >= 1 && groups <= S3N_MAX_GROUPS, "s3n_layernorm: groups 1..4");
-  S3_REQUIRE(ldx % 4 == 0 && (!out32 || ld32 % 4 == 0), "s3n_layernorm: fp32 strides %% 4");
+  S3_REQUIRE(ldx % 4 == 0 && (!out32 || ld32 % 4 == 0) && (!out16 || ld16 % 4 == 0),
+             "s3n_layernorm: strides must be multiples of 4");
   if (rows == 0) return S3_OK;
   LnP p;
   p.rows = rows; p.C = C; p.ldx = ldx; p.eps = eps; p.ld16 = ld16; p.ld32 = ld32;

@@ -196,10 +196,11 @@ class EncoderPlan:
         for blk in w.enc:
             P.add(ops.layernorm([x], [blk["n1w"]], [blk["n1b"]], rows=M, C=E, ldx=E, eps=cfg.ln_eps,
                                 out16=[h], ld16=E))
-            P.add(ops.gemm([h], [blk["qkv_w"]], [qkv], M, 3 * E, E, lda=E, bias=[blk["qkv_b"]]))
+            # q, k rotated in the GEMM epilogue (RoPE2D on columns [0, 2E))
+            P.add(ops.gemm([h], [blk["qkv_w"]], [qkv], M, 3 * E, E, lda=E, bias=[blk["qkv_b"]],
+                           rope=net.rope, rope_pos=[self.pos], rope_ncols=2 * E))
             P.add(ops.attention([qkv], [qkv[:, E:]], [qkv[:, 2 * E:]], [ao], B=B, Nq=N, Nk=N, H=H_,
                                 q_stride=3 * E, k_stride=3 * E, v_stride=3 * E, o_stride=E,
-                                qpos=[self.pos], kpos=[self.pos], rope=net.rope,
                                 scale=(E // H_) ** -0.5))
             P.add(ops.gemm([ao], [blk["proj_w"]], [x], M, E, E, lda=E, bias=[blk["proj_b"]],
                            R1=[x], ldr1=E))
@@ -271,21 +272,25 @@ class PairPlan:
             # self attention
             P.add(ops.layernorm(g2(X), g2(blk["n1w"]), g2(blk["n1b"]), rows=M, C=D, ldx=D,
                                 eps=cfg.ln_eps, out16=g2(h), ld16=D))
-            P.add(ops.gemm(g2(h), g2(blk["qkv_w"]), g2(qkv), M, 3 * D, D, lda=D, bias=g2(blk["qkv_b"])))
+            P.add(ops.gemm(g2(h), g2(blk["qkv_w"]), g2(qkv), M, 3 * D, D, lda=D, bias=g2(blk["qkv_b"]),
+                           rope=net.rope, rope_pos=pos, rope_ncols=2 * D))
             P.add(ops.attention(g2(qkv), [qkv[0][:, D:], qkv[1][:, D:]],
                                 [qkv[0][:, 2 * D:], qkv[1][:, 2 * D:]], g2(ao), B=Bp, Nq=N, Nk=N, H=Hd,
                                 q_stride=3 * D, k_stride=3 * D, v_stride=3 * D, o_stride=D,
-                                qpos=pos, kpos=pos, rope=net.rope, scale=sc))
+                                scale=sc))
             P.add(ops.gemm(g2(ao), g2(blk["proj_w"]), g2(X), M, D, D, lda=D, bias=g2(blk["proj_b"]),
                            R1=g2(X), ldr1=D))
             # cross attention: q from norm2(x), k/v from norm_y(y)
             P.add(ops.layernorm(g2(X), g2(blk["n2w"]), g2(blk["n2b"]), rows=M, C=D, ldx=D,
                                 eps=cfg.ln_eps, out16=g2(h), ld16=D))
-            P.add(ops.gemm(g2(h), g2(blk["q_w"]), g2(q), M, D, D, lda=D, bias=g2(blk["q_b"])))
-            P.add(ops.gemm(g2(yh), g2(blk["kv_w"]), g2(kv), M, 2 * D, D, lda=D, bias=g2(blk["kv_b"])))
+            P.add(ops.gemm(g2(h), g2(blk["q_w"]), g2(q), M, D, D, lda=D, bias=g2(blk["q_b"]),
+                           rope=net.rope, rope_pos=pos, rope_ncols=D))
+            # keys come from the other branch: its positions
+            P.add(ops.gemm(g2(yh), g2(blk["kv_w"]), g2(kv), M, 2 * D, D, lda=D, bias=g2(blk["kv_b"]),
+                           rope=net.rope, rope_pos=[pos[1], pos[0]], rope_ncols=D))
             P.add(ops.attention(g2(q), g2(kv), [kv[0][:, D:], kv[1][:, D:]], g2(ao), B=Bp, Nq=N, Nk=N,
                                 H=Hd, q_stride=D, k_stride=2 * D, v_stride=2 * D, o_stride=D,
-                                qpos=pos, kpos=[pos[1], pos[0]], rope=net.rope, scale=sc))
+                                scale=sc))
             P.add(ops.gemm(g2(ao), g2(blk["cp_w"]), g2(X), M, D, D, lda=D, bias=g2(blk["cp_b"]),
                            R1=g2(X), ldr1=D))
             # MLP (+ fp16 copy of the block output when it is a DPT hook)

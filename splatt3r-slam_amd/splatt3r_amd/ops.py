@@ -35,6 +35,9 @@ class GemmArgs(ctypes.Structure):
         ("stride", ctypes.c_int), ("pad", ctypes.c_int), ("oH", ctypes.c_int), ("oW", ctypes.c_int),
         ("relu_in", ctypes.c_int),
         ("sH", ctypes.c_int), ("sW", ctypes.c_int), ("sS", ctypes.c_int), ("sCout", ctypes.c_int),
+        ("split_k", ctypes.c_int), ("tile", ctypes.c_int), ("workspace", P),
+        ("rope_cos", P), ("rope_sin", P), ("rope_maxpos", ctypes.c_int),
+        ("rope_ncols", ctypes.c_int), ("rope_pos", P * G),
     ]
 
 
@@ -56,6 +59,7 @@ _AP = ctypes.POINTER(AttnArgs)
 _PP = ctypes.POINTER(P)
 _lib.register({
     "s3n_gemm": (ctypes.c_int, [_GP, P]),
+    "s3n_gemm_workspace_bytes": (ctypes.c_size_t, [_GP]),
     "s3n_attention": (ctypes.c_int, [_AP, P]),
     "s3n_layernorm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _PP, I64, _PP, _PP,
                                      ctypes.c_float, _PP, I64, _PP, I64, P]),
@@ -115,8 +119,19 @@ class Call:
             _lib.check(st, self.name)
 
 
+def auto_split_k(M, N, K, groups) -> int:
+    """Split K when the 64x64 tile grid cannot fill the chip (M = 768-token
+    GEMMs, small DPT levels): aim at ~512 workgroups, >= 4 K tiles each."""
+    tiles64 = groups * -(-M // 64) * -(-N // 64)
+    if tiles64 >= 384:
+        return 1
+    kt = -(-K // 64)
+    return max(1, min(kt // 4, -(-512 // tiles64)))
+
+
 def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1=None,
-         ldr1=0, R2=None, ldr2=0, C2=None, ldc2=0, conv=None, store=None) -> Call:
+         ldr1=0, R2=None, ldr2=0, C2=None, ldc2=0, conv=None, store=None, split_k=None,
+         tile=0, rope=None, rope_pos=None, rope_ncols=0) -> Call:
     """Grouped GEMM: A, B, C, bias, R1, R2, C2 are lists (one entry per group)
     of tensors / raw pointers.  conv = dict(H, W, C, k, stride, pad, oH, oW,
     relu_in) switches A to implicit im2col of an NHWC image.  store =
@@ -158,13 +173,30 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         mode, sH, sW, s, cout = store
         a.store_mode = {"convt": 1, "pixshuf": 2}[mode]
         a.sH, a.sW, a.sS, a.sCout = sH, sW, s, cout
-    return Call("s3n_gemm", ctypes.byref(a), keep=(a, A, B, C, bias, R1, R2, C2),
+    if rope_pos is not None:   # fused RoPE2D epilogue on the first rope_ncols columns
+        a.rope_cos, a.rope_sin = rope[0].data_ptr(), rope[1].data_ptr()
+        a.rope_maxpos = rope[0].shape[0]
+        a.rope_ncols = int(rope_ncols)
+        a.rope_pos = _parr(rope_pos)
+        split_k = 1
+    a.split_k = int(auto_split_k(M, N, K, groups) if split_k is None else split_k)
+    a.tile = int(tile)
+    ws = None
+    if a.split_k > 1:
+        nbytes = _lib.lib().s3n_gemm_workspace_bytes(ctypes.byref(a))
+        dev = next(t.device for t in (*A, *C) if isinstance(t, torch.Tensor))
+        ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+        a.workspace = ws.data_ptr()
+    return Call("s3n_gemm", ctypes.byref(a), keep=(a, A, B, C, bias, R1, R2, C2, ws, rope,
+                                                    rope_pos),
                 kind="gemm.conv" if conv is not None else "gemm.dense",
                 flops=2 * int(M) * int(N) * int(K) * groups,
                 desc=f"gemm{'.conv' if conv is not None else ''} {M}x{N}x{K} g{groups}"
                      + (f" k{conv['k']}s{conv['stride']}" if conv is not None else "")
                      + (f" {act}" if act != "none" else "") + (" R1" if R1 else "")
-                     + (f" st={store[0]}" if store else ""))
+                     + (f" st={store[0]}" if store else "")
+                     + (f" sk{a.split_k}" if a.split_k > 1 else "")
+                     + (" rope" if rope_pos is not None else ""))
 
 
 def attention(Q, K, V, O, *, B, Nq, Nk, H, q_stride, k_stride, v_stride, o_stride, qpos=None,

@@ -37,6 +37,54 @@ def test_gemm_dense_bias_residual(M, N, K, groups):
         assert rel_err(C[g], ref) < 1e-5, (g, rel_err(C[g], ref))
 
 
+@pytest.mark.parametrize("M,N,K,groups,split,tile", [
+    (768, 1024, 4096, 1, 3, 0), (768, 768, 768, 2, 2, 1), (200, 96, 200, 2, 5, 0),
+    (130, 300, 1000, 1, 7, 2), (300, 256, 2304, 4, 4, 3), (768, 1024, 1024, 1, 1, 3)])
+def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
+    """Split-K partials + ordered reduce + the full epilogue (bias, GELU,
+    fp32 residual, fp16 out + fp16 copy) for every tile shape."""
+    from splatt3r_amd import ops, _lib
+    A = [_rand(M, K, seed=g) for g in range(groups)]
+    W = [_rand(N, K, scale=K ** -0.5, seed=10 + g) for g in range(groups)]
+    b = [_rand(N, dtype=torch.float32, seed=20 + g) for g in range(groups)]
+    R = [_rand(M, N, dtype=torch.float32, seed=30 + g) for g in range(groups)]
+    C = [torch.empty(M, N, device="cuda", dtype=torch.float16) for _ in range(groups)]
+    C2 = [torch.empty(M, N, device="cuda", dtype=torch.float16) for _ in range(groups)]
+    ops.gemm(A, W, C, M, N, K, lda=K, bias=b, act="gelu", R1=R, ldr1=N, C2=C2, ldc2=N,
+             split_k=split, tile=tile)(_lib.stream())
+    for g in range(groups):
+        ref = F.gelu(A[g].float() @ W[g].float().T + b[g]) + R[g]
+        assert rel_err(C[g], ref) < 2e-3, (g, rel_err(C[g], ref))
+        assert torch.equal(C[g], C2[g])
+
+
+@pytest.mark.parametrize("split,tile", [(3, 1), (9, 0), (2, 3)])
+def test_gemm_implicit_conv_split_k(split, tile):
+    from splatt3r_amd import ops, _lib
+    B, H, W, Cin, Cout, k, stride, pad = 1, 12, 16, 768, 256, 3, 1, 1
+    x = _rand(B, H, W, Cin, seed=13)
+    w = _rand(Cout, Cin, k, k, scale=(Cin * k * k) ** -0.5, seed=14)
+    out = torch.empty(B, H, W, Cout, device="cuda")
+    wk = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous()
+    conv = dict(H=H, W=W, C=Cin, k=k, stride=stride, pad=pad, oH=H, oW=W, relu_in=True)
+    ops.gemm([x], [wk], [out], B * H * W, Cout, k * k * Cin, lda=0, conv=conv, split_k=split,
+             tile=tile)(_lib.stream())
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2).clamp_min(0), w.float(), padding=pad)
+    assert rel_err(out, ref.permute(0, 2, 3, 1)) < 1e-5
+
+
+def test_gemm_split_k_is_deterministic():
+    from splatt3r_amd import ops, _lib
+    M, N, K = 768, 1024, 4096
+    A, W = _rand(M, K), _rand(N, K, scale=K ** -0.5, seed=1)
+    outs = []
+    for _ in range(3):
+        C = torch.empty(M, N, device="cuda")
+        ops.gemm([A], [W], [C], M, N, K, lda=K, split_k=4)(_lib.stream())
+        outs.append(C)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+
+
 def test_gemm_gelu_fp16_out_and_copy():
     from splatt3r_amd import ops, _lib
     M, N, K = 300, 512, 256
@@ -124,6 +172,37 @@ def rope_ref(t, pos, cos, sin):
 
     y, xx = t.chunk(2, dim=-1)
     return torch.cat((r1d(y, pos[:, :, 0]), r1d(xx, pos[:, :, 1])), -1)
+
+
+@pytest.mark.parametrize("B,ht,wt,heads,ncol_heads,groups", [(1, 24, 32, 16, 32, 1), (2, 6, 8, 12, 12, 2),
+                                                            (1, 5, 7, 2, 4, 2)])
+def test_gemm_rope_epilogue_vs_torch(B, ht, wt, heads, ncol_heads, groups):
+    """QKV projection with RoPE2D fused into the epilogue == linear then
+    pos_embed.py's rope on each head of the first rope_ncols columns."""
+    from splatt3r_amd import ops, _lib
+    from splatt3r_amd.net import positions, rope_tables
+    N_tok = ht * wt
+    M, K = B * N_tok, 128
+    Nout = heads * 64 + 64 * 2          # rotated heads + 2 untouched heads
+    ncols = ncol_heads * 64 if ncol_heads <= heads else heads * 64
+    ncols = min(ncols, heads * 64)
+    cos, sin = rope_tables(64, "cuda")
+    pos = [positions(B, ht, wt, "cuda") for _ in range(groups)]
+    if groups > 1:
+        pos[1] = pos[1].flip(1).contiguous()     # different positions per group
+    A = [_rand(M, K, seed=40 + g) for g in range(groups)]
+    W = [_rand(Nout, K, scale=K ** -0.5, seed=50 + g) for g in range(groups)]
+    b = [_rand(Nout, dtype=torch.float32, seed=60 + g) for g in range(groups)]
+    C = [torch.empty(M, Nout, device="cuda") for _ in range(groups)]
+    ops.gemm(A, W, C, M, Nout, K, lda=K, bias=b, rope=(cos, sin), rope_pos=pos,
+             rope_ncols=ncols)(_lib.stream())
+    for g in range(groups):
+        lin = A[g].float() @ W[g].float().T + b[g]
+        ref = lin.clone()
+        hr = ncols // 64
+        t = lin[:, :ncols].view(B, N_tok, hr, 64).transpose(1, 2)
+        ref[:, :ncols] = rope_ref(t, pos[g], cos, sin).transpose(1, 2).reshape(M, ncols)
+        assert rel_err(C[g], ref) < 1e-5, (g, rel_err(C[g], ref))
 
 
 @pytest.mark.parametrize("B,N,Nk,H,cross", [(1, 768, 768, 16, False), (2, 12, 12, 2, False),
