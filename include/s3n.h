@@ -76,7 +76,7 @@ typedef struct {
    * output tile; fp32 partials go to `workspace` (s3n_gemm_workspace_bytes)
    * and a second launch sums them in split order (deterministic) and
    * applies the epilogue.  tile: 0 = auto, 1 = 64x64, 2 = 64x128,
-   * 3 = 128x128. */
+   * 3 = 128x128 (4 waves), 4 = 256x128 (8 waves), 5 = 128x128 (8 waves). */
   int split_k;
   int tile;
   void* workspace;

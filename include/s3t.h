@@ -12,8 +12,9 @@
  * and reduces H = sum A^T A (upper triangle, 28), g = -sum A^T b (7),
  * cost = 0.5 sum b^T b into out[36] = {H_upper(28, row-major), g(7), cost}.
  * sqrt_info = (1/sigma_ray, x3; 1/sigma_dist) * valid_i * sqrt(Q_i).
- * The pose T (Sim3, t q s) is a by-value argument so the host-driven loop
- * needs no device upload per iteration.
+ * The pose T (Sim3, t q s) is read from device memory, so the first
+ * iteration can be queued before the host knows the pose (the host loop
+ * uploads later poses asynchronously, stream-ordered).
  */
 #ifndef S3T_H
 #define S3T_H
@@ -26,7 +27,7 @@ extern "C" {
 /* Workspace bytes for n correspondences (block partials). */
 size_t s3t_workspace_bytes(int64_t n);
 
-int s3t_ray_dist_normal_eqs(const float* T /* host [8] */, const float* Xf, const float* Xk,
+int s3t_ray_dist_normal_eqs(const float* T /* device [8] */, const float* Xf, const float* Xk,
                             const float* Q, const uint8_t* valid, int64_t n,
                             float sigma_ray, float sigma_dist, float huber_k,
                             void* workspace, float* out36, void* stream);

@@ -37,7 +37,8 @@ typedef struct {
 /* Workspace for n = ceil(H/stride) * ceil(W/stride) Gaussians. */
 size_t s3w_workspace_bytes(int64_t n);
 
-/* T_WC: host float[12] = row-major 3x3 (s R) then t.  depth_max_percentile
+/* T_WC: device float[16], the row-major 4x4 [s R | t; 0 0 0 1] (as
+ * lietorch Sim3.matrix() returns it).  depth_max_percentile
  * >= 1 disables the quantile bound, min_confidence <= 0 the confidence
  * filter.  out: [n, 13] device; *count_dev (device int64) receives the
  * number of records written.  Stream-ordered, no host sync. */

@@ -111,19 +111,22 @@ k_flags(int64_t n, Grid g, const float* __restrict__ means, const float* __restr
   flags[i] = v ? 1u : 0u;
 }
 
-struct Pose {
-  float m[12];
-};
-
 __global__ void __launch_bounds__(kThreads)
-k_emit(int64_t n, Grid g, s3w_view v, Pose T, const uint32_t* __restrict__ flags,
+k_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44, const uint32_t* __restrict__ flags,
        const uint32_t* __restrict__ offsets, float* __restrict__ out, int64_t* __restrict__ count) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   if (i == n - 1) *count = (int64_t)offsets[i] + flags[i];
   if (!flags[i]) return;
   const int64_t p = g.pix(i);
-  const float* M = T.m;
+  // T44: row-major [4,4] (s R | t); M[0..8] = s R, M[9..11] = t
+  float M[12];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) M[r * 3 + c] = T44[r * 4 + c];
+    M[9 + r] = T44[r * 4 + 3];
+  }
   const float x = v.means[p * 3 + 0], y = v.means[p * 3 + 1], z = v.means[p * 3 + 2];
   float* o = out + (int64_t)offsets[i] * 13;
   for (int r = 0; r < 3; ++r) o[r] = (M[r * 3 + 0] * x + M[r * 3 + 1] * y + M[r * 3 + 2] * z) + M[9 + r];
@@ -186,8 +189,6 @@ extern "C" int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, floa
   S3_REQUIRE(n < (int64_t)1 << 31, "s3w_gaussians_to_world: too many Gaussians");
   Ws w = carve(workspace, n);
   Grid g{v->H, v->W, v->stride, (int)s3::cdiv(v->W, v->stride)};
-  Pose T;
-  for (int k = 0; k < 12; ++k) T.m[k] = T_WC[k];
   const int blocks = (int)s3::cdiv(n, kThreads);
   S3_HIP(hipMemsetAsync(w.n_valid0, 0, sizeof(uint32_t), st));
   k_prep<<<blocks, kThreads, 0, st>>>(n, g, v->means, depth_min, w.keys_in, w.n_valid0);
@@ -204,7 +205,7 @@ extern "C" int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, floa
   S3_LAUNCH_CHECK();
   size_t sb = w.scan_bytes;
   S3_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, sb, w.flags, w.offsets, (int)n, st));
-  k_emit<<<blocks, kThreads, 0, st>>>(n, g, *v, T, w.flags, w.offsets, out, count_dev);
+  k_emit<<<blocks, kThreads, 0, st>>>(n, g, *v, T_WC, w.flags, w.offsets, out, count_dev);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

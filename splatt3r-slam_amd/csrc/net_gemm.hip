@@ -68,17 +68,37 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // conv, implicit-im2col conv with ReLU applied to the A fragments.
 constexpr int kDense = 0, kConv = 1, kConvRelu = 2;
 
-// Zero source for out-of-range LDS-DMA lanes (padding taps, M/N/K tails).
-__device__ __attribute__((aligned(64))) f16 g_zero[64];
+// 16-B LDS-DMA through a raw buffer resource: voffset per lane (bytes),
+// soffset uniform (bytes); offsets at or past num_records read as zero,
+// which implements every M/N/K tail and conv padding tap.
+#define S3_BLDS(rsrc, lptr, voff, soff)                                               \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(                                          \
+      (rsrc), (__attribute__((address_space(3))) void*)(lptr), 16, (int)(voff), (int)(soff), 0, 0)
 
-#define S3_GLDS(gptr, lptr)                                                          \
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(gptr), \
-                                   (__attribute__((address_space(3))) void*)(lptr), 16, 0, 0)
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
+  const int64_t lim = bytes < 0x7fffffff ? bytes : 0x7fffffff;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)lim,
+                                           0x00020000);
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until <= min(after, MAXA) * PERW loads remain (after: tiles issued
+// behind the one being waited for; wave-uniform)
+template <int PERW, int MAXA>
+__device__ __forceinline__ void wait_tiles(int after) {
+  if constexpr (MAXA <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (after >= MAXA) wait_vmcnt<PERW * MAXA>();
+    else wait_tiles<PERW, MAXA - 1>(after);
+  }
 }
 
 // bias -> act -> + R1 -> + R2 -> store (plain / ConvT / pixel-shuffle
@@ -127,13 +147,18 @@ __device__ __forceinline__ void epilogue(const GemmP& p, int g, int row, int col
   if (C2) C2[(int64_t)row * p.ldc2 + col] = (f16)v;
 }
 
-template <int BM, int BN, int AMODE, int kStages>
-__global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+// NWM x NWN waves, each owning a (BM/NWM) x (BN/NWN) block of 32x32
+// accumulators.
+template <int BM, int BN, int NWM, int NWN, int AMODE, int kStages>
+__global__ void __launch_bounds__(64 * NWM * NWN) k_gemm(GemmP p) {
+  constexpr int NW = NWM * NWN;
+  constexpr int WM = BM / NWM, WN = BN / NWN;
   constexpr int FM = WM / 32, FN = WN / 32;
   // One LDS-DMA wave instruction moves 64 lanes x 16 B = 8 rows of the
   // 128-B (BK = 64 fp16) tile rows.  Each wave issues AW + BW per K tile.
-  constexpr int AW = BM / 8 / 4, BW = BN / 8 / 4;
+  constexpr int AW = BM / 8 / NW, BW = BN / 8 / NW;
+  static_assert(AW * 8 * NW == BM && BW * 8 * NW == BN, "LDS-DMA rows must split over waves");
+  static_assert(WM % 32 == 0 && WN % 32 == 0, "32x32 accumulator blocks");
   constexpr int PERW = AW + BW;
   constexpr int STAGE = (BM + BN) * BK;
   __shared__ __attribute__((aligned(1024))) f16 smem[kStages * STAGE];
@@ -148,7 +173,7 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / NWN, wn = wave % NWN;
   const int M = p.M, N = p.N, K = p.K;
   const f16* __restrict__ A = p.A[g];
   const f16* __restrict__ B = p.B[g];
@@ -160,7 +185,8 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
   // pre-swizzled so the LDS image is the XOR-swizzled layout the fragment
   // reads expect (swz is an involution).
   const int lrow = lane >> 3, lchunk = lane & 7;
-  const f16* a_src[AW];
+  uint32_t a_off[AW];   // dense: byte offset of the lane's row chunk at k = 0
+  int64_t a_img[AW];    // conv: element offset of the lane's image
   int a_iy0[AW], a_ix0[AW];
   bool a_ok[AW];
   int a_kc[AW];
@@ -175,11 +201,13 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
     a_ok[j] = m < M;
     const int mm = a_ok[j] ? m : 0;
     if constexpr (AMODE == kDense) {
-      a_src[j] = A + (int64_t)mm * p.lda + a_kc[j] * 8;
+      a_off[j] = a_ok[j] ? (uint32_t)(((int64_t)mm * p.lda + a_kc[j] * 8) * 2) : kOOB;
       a_iy0[j] = a_ix0[j] = 0;
+      a_img[j] = 0;
     } else {
       const int ox = mm % p.oW, t = mm / p.oW, oy = t % p.oH, b = t / p.oH;
-      a_src[j] = A + (int64_t)b * p.cH * p.cW * p.cC;
+      a_off[j] = 0;
+      a_img[j] = (int64_t)b * p.cH * p.cW * p.cC;
       a_iy0[j] = oy * p.st - p.pad;
       a_ix0[j] = ox * p.st - p.pad;
       const int k = kt_begin * BK + a_kc[j] * 8, tap = k / p.cC;
@@ -188,7 +216,7 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
       c_kx[j] = tap - c_ky[j] * p.ks;
     }
   }
-  const f16* b_src[BW];
+  uint32_t b_off[BW];
   bool b_ok[BW];
   int b_kc[BW];
 #pragma unroll
@@ -196,8 +224,16 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
     const int r = (wave * BW + j) * 8 + lrow;
     b_kc[j] = swz(r, lchunk);
     b_ok[j] = (n0 + r) < N;
-    b_src[j] = B + (int64_t)(b_ok[j] ? n0 + r : 0) * p.ldb + b_kc[j] * 8;
+    b_off[j] = b_ok[j] ? (uint32_t)(((int64_t)(n0 + r) * p.ldb + b_kc[j] * 8) * 2) : kOOB;
   }
+
+  // Buffer resources: operand extents bound the reads (tails read zero).
+  const int Bn = AMODE == kDense ? 0 : M / (p.oH * p.oW);
+  const __amdgpu_buffer_rsrc_t ra =
+      AMODE == kDense ? make_rsrc(A, ((int64_t)(M - 1) * p.lda + K) * 2)
+                      : make_rsrc(A, (int64_t)Bn * p.cH * p.cW * p.cC * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B, ((int64_t)(N - 1) * p.ldb + K) * 2);
+  const bool k_tail = (K % BK) != 0;
 
   // Issue the LDS-DMA loads of K tile kt into stage st (tiles are issued in
   // order kt = 0, 1, 2, ...: the conv state advances one tile per call).
@@ -205,31 +241,33 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
     f16* As = smem + st * STAGE;
     f16* Bs = As + BM * BK;
     const int k0 = kt * BK;
+    const bool tail = k_tail && (k0 + BK > K);   // wave-uniform
 #pragma unroll
     for (int j = 0; j < AW; ++j) {
-      const int k = k0 + a_kc[j] * 8;
-      const f16* src = g_zero;
+      uint32_t off;
       if constexpr (AMODE == kDense) {
-        if (a_ok[j] && k < K) src = a_src[j] + k0;
+        off = a_off[j];
+        if (tail && k0 + a_kc[j] * 8 >= K) off = kOOB;
+        S3_BLDS(ra, As + (wave * AW + j) * 512, off, k0 * 2);
       } else {
-        if (a_ok[j] && k < K) {
-          const int iy = a_iy0[j] + c_ky[j], ix = a_ix0[j] + c_kx[j];
-          if (iy >= 0 && iy < p.cH && ix >= 0 && ix < p.cW)
-            src = a_src[j] + ((int64_t)iy * p.cW + ix) * p.cC + c_ci[j];
-        }
+        off = kOOB;
+        const int iy = a_iy0[j] + c_ky[j], ix = a_ix0[j] + c_kx[j];
+        if (a_ok[j] && !(tail && k0 + a_kc[j] * 8 >= K) && iy >= 0 && iy < p.cH && ix >= 0 &&
+            ix < p.cW)
+          off = (uint32_t)((a_img[j] + ((int64_t)iy * p.cW + ix) * p.cC + c_ci[j]) * 2);
         c_ci[j] += BK;
         while (c_ci[j] >= p.cC) {
           c_ci[j] -= p.cC;
           if (++c_kx[j] == p.ks) { c_kx[j] = 0; ++c_ky[j]; }
         }
+        S3_BLDS(ra, As + (wave * AW + j) * 512, off, 0);
       }
-      S3_GLDS(src, As + (wave * AW + j) * 512);
     }
 #pragma unroll
     for (int j = 0; j < BW; ++j) {
-      const int k = k0 + b_kc[j] * 8;
-      const f16* src = (b_ok[j] && k < K) ? b_src[j] + k0 : g_zero;
-      S3_GLDS(src, Bs + (wave * BW + j) * 512);
+      uint32_t off = b_off[j];
+      if (tail && k0 + b_kc[j] * 8 >= K) off = kOOB;
+      S3_BLDS(rb, Bs + (wave * BW + j) * 512, off, k0 * 2);
     }
   };
 
@@ -249,42 +287,46 @@ __global__ void __launch_bounds__(kThreads) k_gemm(GemmP p) {
   for (int i = 0; i < AHEAD; ++i)
     if (i < KT) issue(kt_begin + i, i);
   for (int kt = 0; kt < KT; ++kt) {
-    // Tile kt has landed once at most AHEAD-1 newer tiles are in flight.
-    if constexpr (AHEAD == 2) {
-      if (kt + 1 < KT) wait_vmcnt<PERW>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
+    // Tile kt has landed once at most (tiles issued after it) x PERW DMA
+    // instructions of this wave are still outstanding.
+    wait_tiles<PERW, AHEAD - 1>(KT - 1 - kt);
     // Everyone's DMA for tile kt is visible, and everyone finished reading
     // the stage that tile kt+AHEAD overwrites (read during iteration kt-1).
     __builtin_amdgcn_s_barrier();
-    if (kt + AHEAD < KT) issue(kt_begin + kt + AHEAD, (kt + AHEAD) % kStages);
     const f16* As = smem + (kt % kStages) * STAGE;
     const f16* Bs = As + BM * BK;
+    // All fragments of this K tile first (their LDS latency overlaps the
+    // next tile's DMA issue below), then the MFMA chain.
+    f16x8 af[BK / 16][FM], bf[BK / 16][FN];
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       const int kc = 2 * ks + (lane >> 5);
-      f16x8 af[FM], bf[FN];
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm) {
         const int row = wm * WM + fm * 32 + (lane & 31);
-        af[fm] = *reinterpret_cast<const f16x8*>(As + row * BK + swz(row, kc) * 8);
-        if constexpr (AMODE == kConvRelu) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) af[fm][e] = af[fm][e] > (f16)0 ? af[fm][e] : (f16)0;
-        }
+        af[ks][fm] = *reinterpret_cast<const f16x8*>(As + row * BK + swz(row, kc) * 8);
       }
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const int row = wn * WN + fn * 32 + (lane & 31);
-        bf[fn] = *reinterpret_cast<const f16x8*>(Bs + row * BK + swz(row, kc) * 8);
+        bf[ks][fn] = *reinterpret_cast<const f16x8*>(Bs + row * BK + swz(row, kc) * 8);
+      }
+    }
+    if (kt + AHEAD < KT) issue(kt_begin + kt + AHEAD, (kt + AHEAD) % kStages);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      if constexpr (AMODE == kConvRelu) {
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            af[ks][fm][e] = af[ks][fm][e] > (f16)0 ? af[ks][fm][e] : (f16)0;
       }
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[ks][fm], bf[ks][fn], acc[fm][fn], 0, 0, 0);
     }
   }
 
@@ -349,8 +391,9 @@ __global__ void __launch_bounds__(kThreads) k_splitk_reduce(GemmP p) {
   epilogue(p, g, (int)(i / p.N), (int)(i % p.N), v);
 }
 
-template <int BM, int BN, int S>
+template <int BM, int BN, int S, int NWM = 2, int NWN = 2>
 int launch(const GemmP& p, hipStream_t st) {
+  constexpr int NT = 64 * NWM * NWN;
   GemmP q = p;
   q.tiles_m = (p.M + BM - 1) / BM;
   q.tiles_n = (p.N + BN - 1) / BN;
@@ -363,11 +406,11 @@ int launch(const GemmP& p, hipStream_t st) {
   q.col_major = (int64_t)p.N * p.K > a_bytes;
   dim3 grid(q.tiles_m * q.tiles_n, q.split_k, p.groups);
   if (p.a_mode == S3N_A_DENSE)
-    k_gemm<BM, BN, kDense, S><<<grid, kThreads, 0, st>>>(q);
+    k_gemm<BM, BN, NWM, NWN, kDense, S><<<grid, NT, 0, st>>>(q);
   else if (p.relu_in)
-    k_gemm<BM, BN, kConvRelu, S><<<grid, kThreads, 0, st>>>(q);
+    k_gemm<BM, BN, NWM, NWN, kConvRelu, S><<<grid, NT, 0, st>>>(q);
   else
-    k_gemm<BM, BN, kConv, S><<<grid, kThreads, 0, st>>>(q);
+    k_gemm<BM, BN, NWM, NWN, kConv, S><<<grid, NT, 0, st>>>(q);
   S3_LAUNCH_CHECK();
   if (q.split_k > 1) {
     dim3 rg((unsigned)s3::cdiv((int64_t)p.M * p.N, kThreads), p.groups);
@@ -439,13 +482,19 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   if (a->tile == 1) return launch<64, 64, 3>(p, st);
   if (a->tile == 2) return launch<64, 128, 3>(p, st);
   if (a->tile == 3) return launch<128, 128, 2>(p, st);
+  if (a->tile == 4) return launch<256, 128, 3, 4, 2>(p, st);
+  if (a->tile == 5) return launch<128, 128, 3, 2, 4>(p, st);
+  if (a->tile == 6) return launch<64, 64, 4>(p, st);
+  if (a->tile == 7) return launch<64, 64, 5>(p, st);
+  if (a->tile == 8) return launch<64, 128, 4>(p, st);
   // Tile choice: fill the 256 CUs before growing the tile.
   auto tiles = [&](int bm, int bn) {
     return (int64_t)a->groups * ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
   };
-  // LDS: 128x128 x 2 stages = 64 KB (2 WG/CU), 64x128 x 3 = 72 KB (2),
-  // 64x64 x 3 = 48 KB (3).
-  if (tiles(128, 128) >= 512) return launch<128, 128, 2>(p, st);
-  if (tiles(64, 128) >= 384 && a->N >= 128) return launch<64, 128, 3>(p, st);
+  // LDS: 64x64 x 3 stages = 48 KB (3 WG/CU), 64x128 x 3 = 72 KB (2),
+  // 128x128 x 2 = 64 KB (2).  Measured on the network's shapes
+  // (splatt3r_amd/bench_gemm.py): 64x64 wins up to ~2k tiles (the
+  // 768-token GEMMs), 64x128 beyond (head MLP, DPT convs).
+  if (tiles(64, 64) > 2048 && a->N >= 128) return launch<64, 128, 3>(p, st);
   return launch<64, 64, 3>(p, st);
 }

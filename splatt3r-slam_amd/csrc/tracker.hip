@@ -14,14 +14,13 @@ constexpr int kThreads = 256;
 constexpr int kMaxBlocks = 1024;
 constexpr int NV = 36;  // 28 (H upper) + 7 (g) + 1 (cost)
 
-struct Pose {
-  float v[8];
-};
-
 __global__ void __launch_bounds__(kThreads)
-k_normal_eqs(Pose T, const float* __restrict__ Xf, const float* __restrict__ Xk,
+k_normal_eqs(const float* __restrict__ Tdev, const float* __restrict__ Xf, const float* __restrict__ Xk,
              const float* __restrict__ Q, const uint8_t* __restrict__ valid, int64_t n,
              float inv_sr, float inv_sd, float hk, float* __restrict__ partial) {
+  float T[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) T[k] = Tdev[k];
   float acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.f;
@@ -29,7 +28,7 @@ k_normal_eqs(Pose T, const float* __restrict__ Xf, const float* __restrict__ Xk,
        i += (int64_t)gridDim.x * blockDim.x) {
     float x[3] = {Xf[i * 3 + 0], Xf[i * 3 + 1], Xf[i * 3 + 2]};
     float p[3];
-    s3lie::act_sim3(T.v, x, p);
+    s3lie::act_sim3(T, x, p);
     const float d = sqrtf(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
     const float di = 1.0f / d;
     const float rf[3] = {di * p[0], di * p[1], di * p[2]};
@@ -125,12 +124,10 @@ extern "C" int s3t_ray_dist_normal_eqs(const float* T, const float* Xf, const fl
                                        void* workspace, float* out36, void* stream) {
   S3_REQUIRE(T && n >= 0 && workspace && out36, "s3t_ray_dist_normal_eqs: bad arguments");
   hipStream_t st = s3::as_stream(stream);
-  Pose pose;
-  for (int k = 0; k < 8; ++k) pose.v[k] = T[k];
   const int nb = blocks_for(n);
   float* partial = static_cast<float*>(workspace);
   // reference: sqrt_info = 1 / sigma * valid * sqrt(Q)  (tracker.py:175-176)
-  k_normal_eqs<<<nb, kThreads, 0, st>>>(pose, Xf, Xk, Q, valid, n, 1.0f / sigma_ray,
+  k_normal_eqs<<<nb, kThreads, 0, st>>>(T, Xf, Xk, Q, valid, n, 1.0f / sigma_ray,
                                        1.0f / sigma_dist, huber_k, partial);
   S3_LAUNCH_CHECK();
   k_finalize<<<NV, kThreads, 0, st>>>(partial, nb, out36);

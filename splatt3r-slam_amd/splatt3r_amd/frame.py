@@ -114,12 +114,14 @@ def create_frame(i, img, T_WC=None, img_size=512, device="cuda:0"):
     if torch.is_tensor(img) and img.dim() == 4:
         rgb = img.to(device)
         H, W = rgb.shape[-2:]
-        true_shape = torch.tensor([[H, W]], device=device, dtype=torch.int32)
+        true_shape = torch.tensor([[H, W]], dtype=torch.int32)
         uimg = None
     else:
         r = resize_img(img, img_size)
         rgb = r["img"].to(device)
-        true_shape = torch.tensor(r["true_shape"], device=device)
+        # kept on the host (the reference puts it on the device): it is
+        # shape metadata, read by the host glue every frame
+        true_shape = torch.tensor(r["true_shape"])
         uimg = torch.from_numpy(r["unnormalized_img"].copy()) / 255.0
     img_shape = true_shape.clone()
     ds = config["dataset"]["img_downsample"]

@@ -120,13 +120,15 @@ class Call:
 
 
 def auto_split_k(M, N, K, groups) -> int:
-    """Split K when the 64x64 tile grid cannot fill the chip (M = 768-token
-    GEMMs, small DPT levels): aim at ~512 workgroups, >= 4 K tiles each."""
+    """Split K only when the 64x64 tile grid is far too small for the chip
+    (the 12x16 / 24x32 DPT levels): ~256 workgroups, >= 4 K tiles each."""
     tiles64 = groups * -(-M // 64) * -(-N // 64)
-    if tiles64 >= 384:
-        return 1
     kt = -(-K // 64)
-    return max(1, min(kt // 4, -(-512 // tiles64)))
+    if tiles64 < 256 and kt >= 32:   # e.g. the encoder fc2 (768x1024x4096): 2 halves
+        return 2
+    if tiles64 >= 128:      # the combine launch costs more than it saves
+        return 1
+    return max(1, min(kt // 4, -(-256 // tiles64)))
 
 
 def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1=None,

@@ -16,7 +16,7 @@ import time
 import torch
 import torch.distributed as dist
 
-from splatt3r_amd.splatt3r_utils import pose_host12, splatt3r_match_symmetric, world_records
+from splatt3r_amd.splatt3r_utils import splatt3r_match_symmetric, world_records
 
 GAUSS_FLOATS = 13   # means 3 + cov_triu 6 + colour 3 + opacity 1 (52 B)
 
@@ -57,7 +57,7 @@ def world_gaussians(res, T_WC: torch.Tensor, img: torch.Tensor) -> torch.Tensor:
     filters off, as one HIP pass (include/s3w.h)."""
     from lietorch import Sim3
     M = Sim3(T_WC.reshape(1, 8)).matrix()[0]
-    out, _ = world_records(res, img[0] if img.dim() == 4 else img, pose_host12(M))
+    out, _ = world_records(res, img[0] if img.dim() == 4 else img, M)
     return out
 
 

@@ -74,9 +74,14 @@ def camera_settings(extrinsics, intrinsics, near, far, image_shape, background_c
                     sh_degree, scale_invariant=True):
     """The per-view settings render_cuda builds (cuda_splatting.py:67-113),
     for a batch of views.  Returns (list[GaussianRasterizationSettings], scale)."""
+    # Intrinsics-only quantities (fov, projection) are computed wherever the
+    # intrinsics live: pass CPU intrinsics/near/far to avoid a device->host
+    # sync for the tanfov floats; the pose-dependent part stays on the
+    # extrinsics' device.
+    dev = extrinsics.device
     scale = 1 / near if scale_invariant else torch.ones_like(near)
     extrinsics = extrinsics.clone()
-    extrinsics[..., :3, 3] = extrinsics[..., :3, 3] * scale[:, None]
+    extrinsics[..., :3, 3] = extrinsics[..., :3, 3] * scale.to(dev)[:, None]
     near = near * scale
     far = far * scale
     h, w = image_shape
@@ -84,7 +89,9 @@ def camera_settings(extrinsics, intrinsics, near, far, image_shape, background_c
     tan_fov_x = (0.5 * fov_x).tan()
     tan_fov_y = (0.5 * fov_y).tan()
     projection_matrix = get_projection_matrix(near, far, fov_x, fov_y).transpose(1, 2)
-    view_matrix = extrinsics.inverse().transpose(1, 2)
+    if projection_matrix.device != dev:
+        projection_matrix = projection_matrix.pin_memory().to(dev, non_blocking=True)
+    view_matrix = torch.linalg.inv_ex(extrinsics)[0].transpose(1, 2)
     full_projection = view_matrix @ projection_matrix
     tx = tan_fov_x.tolist()
     ty = tan_fov_y.tolist()

@@ -224,15 +224,16 @@ def splatt3r_render(model, frame, ref_frame, K=None, target_T_WC=None):
     _, h, w, _ = g1["means"].shape
     context = _sim3_to_4x4(frame.T_WC).to(dev)
     target = context.clone() if target_T_WC is None else _sim3_to_4x4(target_T_WC).to(dev)
-    K_use = (_estimate_default_intrinsics(h, w, dev) if K is None
-             else K.clone().to(device=dev, dtype=torch.float32))
+    # intrinsics-only math on the host (no device sync for the fov floats)
+    K_use = (_estimate_default_intrinsics(h, w, "cpu") if K is None
+             else K.detach().to(device="cpu", dtype=torch.float32).clone())
     if K_use.dim() == 2:
         K_use = K_use.unsqueeze(0)
     # decoder_splatting_cuda.py:36-55
-    extr = torch.inverse(context) @ target
+    extr = torch.linalg.inv_ex(context)[0] @ target   # inv_ex: no host-side error check
     intr = normalize_intrinsics(K_use, (h, w))[..., :3, :3]
-    near = torch.full((1,), 0.1, device=dev)
-    far = torch.full((1,), 1000.0, device=dev)
+    near = torch.full((1,), 0.1)
+    far = torch.full((1,), 1000.0)
     bg = model.decoder.background_color.to(dev)[None]
     settings, scale = camera_settings(extr, intr, near, far, (h, w), bg, 0)
     views = []
@@ -280,8 +281,8 @@ def world_records(view, img, T, stride=1, depth_min=float("-inf"), depth_max_per
                   max_scale=float("inf"), min_confidence=0.0):
     """One predicted view ([H,W,...] tensors: means, scales, rotations, sh,
     opacities[, conf]) + its [3,H,W] ImgNorm image -> ([n,13] world records,
-    device int64 count), stream-ordered (include/s3w.h).  T: host float[12]
-    (s R row-major, t).  Defaults disable every filter."""
+    device int64 count), stream-ordered (include/s3w.h).  T: device [4,4]
+    (s R | t) float32.  Defaults disable every filter."""
     H, W, _ = view["means"].shape
     d_sh = view["sh"].shape[-1]
     n = -(-H // stride) * -(-W // stride)
@@ -289,23 +290,18 @@ def world_records(view, img, T, stride=1, depth_min=float("-inf"), depth_max_per
          ("means", "scales", "rotations", "sh", "opacities")}
     conf = view["conf"].float().contiguous() if view.get("conf") is not None else None
     im = img.float().contiguous()
-    _lib.require_cuda(*t.values(), im)
+    T = T.float().contiguous()
+    _lib.require_cuda(*t.values(), im, T)
     v = S3wView(t["means"].data_ptr(), t["scales"].data_ptr(), t["rotations"].data_ptr(),
                 t["sh"].data_ptr(), t["opacities"].data_ptr(),
                 conf.data_ptr() if conf is not None else None, im.data_ptr(), H, W, d_sh, stride)
     out = torch.empty(n, 13, device=im.device)
     cnt = torch.empty(1, dtype=torch.int64, device=im.device)
     ws = _workspace(im.device, n)
-    _lib.call("s3w_gaussians_to_world", ctypes.byref(v), T, float(depth_min),
+    _lib.call("s3w_gaussians_to_world", ctypes.byref(v), T.data_ptr(), float(depth_min),
               float(depth_max_percentile), float(max_scale), float(min_confidence),
               ws.data_ptr(), out.data_ptr(), cnt.data_ptr(), _lib.stream(im.device))
     return out, cnt
-
-
-def pose_host12(M):
-    """[4,4] (s R | t) -> ctypes float[12] for world_records."""
-    M = M.detach().float().cpu()
-    return (ctypes.c_float * 12)(*M[:3, :3].reshape(-1).tolist(), *M[:3, 3].tolist())
 
 
 @torch.inference_mode()
@@ -316,7 +312,7 @@ def gaussians_to_world(frame, include_cross=True, spatial_stride=1, depth_min=0.
     and a single host sync for the record counts."""
     if frame.gaussian_pred is None:
         return None
-    T = pose_host12(_sim3_to_4x4(frame.T_WC)[0])
+    T = _sim3_to_4x4(frame.T_WC)[0].to(frame.img.device)
     preds = [frame.gaussian_pred]
     if include_cross and frame.gaussian_pred_cross is not None:
         preds.append(frame.gaussian_pred_cross)

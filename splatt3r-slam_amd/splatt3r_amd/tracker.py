@@ -44,35 +44,51 @@ def check_convergence(it, rel_error_threshold, delta_norm_threshold, old_cost, n
 
 
 class NormalEquations:
-    """Device workspace + pinned host buffer for the fused GN reduction."""
+    """Device workspace, pose slot and pinned host buffers for the fused GN
+    reduction.  `launch` queues one iteration (pose read from the device
+    slot); `fetch` waits for it and returns (H, g, cost) on the host."""
 
     def __init__(self, device):
         self.device = torch.device(device)
         self.ws = None
         self.out = torch.empty(36, device=self.device)
         self.host = torch.empty(36, pin_memory=True)
-        self.pose = (ctypes.c_float * 8)()
+        self.pose = torch.empty(8, device=self.device)
+        self.pose_host = torch.empty(8, pin_memory=True)
 
-    def __call__(self, T: np.ndarray, Xf, Xk, Q, valid, sigma_ray, sigma_dist, huber_k):
+    def set_pose_host(self, T: np.ndarray):
+        """Stream-ordered upload of a host pose into the device slot."""
+        self.pose_host.numpy()[:] = T
+        self.pose.copy_(self.pose_host, non_blocking=True)
+
+    def launch(self, Xf, Xk, Q, valid, sigma_ray, sigma_dist, huber_k):
         n = Xf.shape[0]
         _lib.require_cuda(Xf, Xk, Q, valid)
         _lib.require_contig("s3t_ray_dist_normal_eqs", Xf, Xk, Q, valid)
         need = _lib.lib().s3t_workspace_bytes(n)
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-        for k in range(8):
-            self.pose[k] = float(T[k])
-        st = _lib.stream(self.device)
-        _lib.call("s3t_ray_dist_normal_eqs", ctypes.addressof(self.pose), Xf.data_ptr(),
-                  Xk.data_ptr(), Q.data_ptr(), valid.data_ptr(), n, sigma_ray, sigma_dist,
-                  huber_k, self.ws.data_ptr(), self.out.data_ptr(), st)
+        _lib.call("s3t_ray_dist_normal_eqs", self.pose.data_ptr(), Xf.data_ptr(), Xk.data_ptr(),
+                  Q.data_ptr(), valid.data_ptr(), n, sigma_ray, sigma_dist, huber_k,
+                  self.ws.data_ptr(), self.out.data_ptr(), _lib.stream(self.device))
         self.host.copy_(self.out, non_blocking=True)
+
+    def fetch(self):
         torch.cuda.current_stream(self.device).synchronize()
-        v = self.host.numpy().astype(np.float64)
+        return self.unpack(self.host.numpy())
+
+    @staticmethod
+    def unpack(v):
+        v = v.astype(np.float64)
         H = np.empty((7, 7))
         for q, (a, b) in enumerate(_TRIU):
             H[a, b] = H[b, a] = v[q]
         return H, v[28:35].copy(), float(v[35])
+
+    def __call__(self, T: np.ndarray, Xf, Xk, Q, valid, sigma_ray, sigma_dist, huber_k):
+        self.set_pose_host(T)
+        self.launch(Xf, Xk, Q, valid, sigma_ray, sigma_dist, huber_k)
+        return self.fetch()
 
 
 def solve_normal_eqs(H, g):
@@ -130,13 +146,36 @@ class FrameTracker:
         valid_Q = Qk > self.cfg["Q_conf"]
         valid_opt = valid_match_k & valid_Cf & valid_Ck & valid_Q
         valid_kf = valid_match_k & valid_Q
+        n = valid_opt.numel()
+        # unique(idx_f2k[valid_match_k]) counted without a host sync:
+        # mark the hit keyframe pixels, then count them
+        hit = torch.zeros(idx_f2k.shape[0], dtype=torch.uint8, device=idx_f2k.device)
+        hit.scatter_reduce_(0, idx_f2k, valid_match_k[:, 0].to(torch.uint8), "amax")
+        stats = torch.stack([valid_opt.sum(), valid_kf.sum(), hit.sum()]).to(torch.float64)
+        stats_host = torch.empty(3, dtype=torch.float64, pin_memory=True)
+        stats_host.copy_(stats, non_blocking=True)
+        # queue GN iteration 0 at the device-side relative pose before syncing
+        T_CkCf = T_WCk.inv() * T_WCf
+        Xf = Xf.float().contiguous()
+        Xk = Xk.float().contiguous()
+        Q = Qk.float().contiguous()
+        valid_c = valid_opt.contiguous()
+        ne = self.normal_eqs
+        ne.pose.copy_(T_CkCf.data.reshape(8))
+        pose_host = torch.empty(8, pin_memory=True)
+        pose_host.copy_(ne.pose, non_blocking=True)
+        ne.launch(Xf, Xk, Q, valid_c, self.cfg["sigma_ray"], self.cfg["sigma_dist"],
+                  self.cfg["huber"])
+        first = ne.fetch()            # the one sync for stats + pose + iteration 0
+        n_opt, n_kf, n_unique = stats_host.tolist()
 
-        match_frac = float(valid_opt.sum()) / valid_opt.numel()
-        if match_frac < self.cfg["min_match_frac"]:
+        if n_opt / n < self.cfg["min_match_frac"]:
             print(f"Skipped frame {frame.frame_id}")
             return False, [], True
         try:
-            T_WCf, T_CkCf = self.opt_pose_ray_dist_sim3(Xf, Xk, T_WCf, T_WCk, Qk, valid_opt)
+            T_WCf, T_CkCf = self.opt_pose_ray_dist_sim3(
+                Xf, Xk, T_WCf, T_WCk, Q, valid_c,
+                _first=(pose_host.numpy().copy(), first))
         except CholeskyError:
             print(f"Cholesky failed {frame.frame_id}")
             return False, [], True
@@ -146,8 +185,8 @@ class FrameTracker:
         keyframe.update_pointmap(Xkk, Ckf)
         self.keyframes[len(self.keyframes) - 1] = keyframe
 
-        match_frac_k = float(valid_kf.sum()) / valid_kf.numel()
-        unique_frac_f = torch.unique(idx_f2k[valid_match_k[:, 0]]).shape[0] / valid_kf.numel()
+        match_frac_k = n_kf / n
+        unique_frac_f = n_unique / n
         new_kf = min(match_frac_k, unique_frac_f) < self.cfg["match_frac_thresh"]
         if new_kf:
             self.reset_idx_f2k()
@@ -161,25 +200,30 @@ class FrameTracker:
         return (frame.X_canon[idx_f2k], keyframe.X_canon, frame.T_WC, keyframe.T_WC,
                 Cf[idx_f2k], Ck)
 
-    def opt_pose_ray_dist_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid):
-        """tracker.py:173-214 with the per-iteration work fused on the GPU."""
+    def opt_pose_ray_dist_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid, _first=None):
+        """tracker.py:173-214 with the per-iteration work fused on the GPU.
+        `_first` = (T, (H, g, cost)) when iteration 0 was already queued."""
         cfg = self.cfg
-        T_CkCf = T_WCk.inv() * T_WCf
-        T = T_CkCf.data.reshape(8).detach().cpu().numpy().astype(np.float32)
+        ne = self.normal_eqs
         Xf = Xf.float().contiguous()
         Xk = Xk.float().contiguous()
         Q = Qk.float().contiguous()
         valid = valid.contiguous()
+        if _first is None:
+            T_CkCf = T_WCk.inv() * T_WCf
+            T = T_CkCf.data.reshape(8).detach().cpu().numpy().astype(np.float32)
+            first = None
+        else:
+            T, first = _first
         old_cost = float("inf")
         for step in range(cfg["max_iters"]):
-            H, g, new_cost = self.normal_eqs(T, Xf, Xk, Q, valid, cfg["sigma_ray"],
-                                             cfg["sigma_dist"], cfg["huber"])
+            if step == 0 and first is not None:
+                H, g, new_cost = first
+            else:
+                H, g, new_cost = ne(T, Xf, Xk, Q, valid, cfg["sigma_ray"], cfg["sigma_dist"],
+                                    cfg["huber"])
             if _DEBUG:
-                print(f"[gn] step {step} n={Xf.shape[0]} valid={int(valid.sum())} cost={new_cost:.4g} "
-                      f"Hdiag={np.diag(H)} g={g} T={T} "
-                      f"finite Xf={bool(torch.isfinite(Xf).all())} Xk={bool(torch.isfinite(Xk).all())} "
-                      f"Q={bool(torch.isfinite(Q).all())} |Xf|min={float(Xf.norm(dim=-1).min()):.3g} "
-                      f"|Xk|min={float(Xk.norm(dim=-1).min()):.3g}", flush=True)
+                print(f"[gn] step {step} cost={new_cost:.6g} Hdiag={np.diag(H)} T={T}", flush=True)
             tau = solve_normal_eqs(H, g)
             T = _retr_host(T, tau)
             self.last_iters = step + 1
@@ -189,5 +233,6 @@ class FrameTracker:
             old_cost = new_cost
             if step == cfg["max_iters"] - 1:
                 print("max iters reached 0")
-        T_CkCf = lietorch.Sim3(torch.from_numpy(T.copy()).to(Xf.device).view(1, 8))
+        ne.set_pose_host(T)
+        T_CkCf = lietorch.Sim3(ne.pose.clone().view(1, 8))
         return T_WCk * T_CkCf, T_CkCf

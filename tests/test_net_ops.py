@@ -39,7 +39,9 @@ def test_gemm_dense_bias_residual(M, N, K, groups):
 
 @pytest.mark.parametrize("M,N,K,groups,split,tile", [
     (768, 1024, 4096, 1, 3, 0), (768, 768, 768, 2, 2, 1), (200, 96, 200, 2, 5, 0),
-    (130, 300, 1000, 1, 7, 2), (300, 256, 2304, 4, 4, 3), (768, 1024, 1024, 1, 1, 3)])
+    (130, 300, 1000, 1, 7, 2), (300, 256, 2304, 4, 4, 3), (768, 1024, 1024, 1, 1, 3),
+    (700, 200, 960, 2, 1, 4), (520, 384, 640, 1, 2, 5), (768, 6400, 512, 2, 1, 4),
+    (300, 200, 1000, 1, 1, 6), (130, 96, 2000, 2, 1, 7), (600, 256, 200, 1, 1, 8)])
 def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
     """Split-K partials + ordered reduce + the full epilogue (bias, GELU,
     fp32 residual, fp16 out + fp16 copy) for every tile shape."""
@@ -58,7 +60,7 @@ def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
         assert torch.equal(C[g], C2[g])
 
 
-@pytest.mark.parametrize("split,tile", [(3, 1), (9, 0), (2, 3)])
+@pytest.mark.parametrize("split,tile", [(3, 1), (9, 0), (2, 3), (1, 4), (1, 5)])
 def test_gemm_implicit_conv_split_k(split, tile):
     from splatt3r_amd import ops, _lib
     B, H, W, Cin, Cout, k, stride, pad = 1, 12, 16, 768, 256, 3, 1, 1
