@@ -252,6 +252,194 @@ __global__ void __launch_bounds__(kThreads) k_attn(AttnP p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// No-RoPE variant (q/k already rotated by the projection GEMM's epilogue):
+// K and V tiles are streamed global -> LDS by buffer_load ... lds into a
+// kStages-deep ring (no register staging, no per-tile VALU), so up to
+// kStages-1 tiles are in flight while one is consumed.  Same math and
+// fragment layouts as k_attn.
+constexpr int kStages = 4;
+constexpr uint32_t kOOB = 0x80000000u;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int PERW, int MAXA>
+__device__ __forceinline__ void wait_tiles(int after) {
+  if constexpr (MAXA <= 0) {
+    wait_vm<0>();
+  } else {
+    if (after >= MAXA) wait_vm<PERW * MAXA>();
+    else wait_tiles<PERW, MAXA - 1>(after);
+  }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
+  const int64_t lim = bytes < 0x7fffffff ? bytes : 0x7fffffff;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)lim,
+                                           0x00020000);
+}
+
+#define S3_BLDS(rsrc, lptr, voff, soff)                                               \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(                                          \
+      (rsrc), (__attribute__((address_space(3))) void*)(lptr), 16, (int)(voff), (int)(soff), 0, 0)
+
+__global__ void __launch_bounds__(kThreads) k_attn_dma(AttnP p) {
+  // one array: stages of [K tile | V tile], then the per-wave P scratch
+  __shared__ __attribute__((aligned(1024))) f16 smem[kStages * 2 * KT * D + 4 * 16 * KT];
+  const int qtile = blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / p.H, h = bh % p.H;
+  const int g = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const f16* __restrict__ Qg = p.Q[g];
+  f16* Pw = smem + kStages * 2 * KT * D + wave * 16 * KT;
+
+  const int qrow = qtile * QT + wave * 16 + (lane & 15);
+  const bool qok = qrow < p.Nq;
+  f16x8 qf[2];
+  {
+    const f16* qp = Qg + ((int64_t)b * p.Nq + (qok ? qrow : 0)) * p.qs + h * D;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = 4 * ks + (lane >> 4);
+      f16x8 x = *reinterpret_cast<const f16x8*>(qp + c * 8);
+      qf[ks] = qok ? x : f16x8{};
+    }
+  }
+
+  // DMA assignment: per tile 8 K + 8 V wave-instructions (8 key rows of
+  // 128 B each), 2 + 2 per wave.  Lane l -> key row (l >> 3) of its group,
+  // LDS chunk (l & 7); K's global chunk is pre-swizzled (kswz involution).
+  const __amdgpu_buffer_rsrc_t rk =
+      make_rsrc(p.K[g], (((int64_t)b + 1) * p.Nk - 1) * p.ks * 2 + (h + 1) * D * 2);
+  const __amdgpu_buffer_rsrc_t rv =
+      make_rsrc(p.V[g], (((int64_t)b + 1) * p.Nk - 1) * p.vs * 2 + (h + 1) * D * 2);
+  const int lr = lane >> 3, lc = lane & 7;
+  uint32_t k_off[2], v_off[2];
+  int k_key[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wave * 2 + j) * 8 + lr;   // key row within the tile
+    k_key[j] = row;
+    k_off[j] = (uint32_t)((((int64_t)b * p.Nk + row) * p.ks + h * D + kswz(row, lc) * 8) * 2);
+    v_off[j] = (uint32_t)((((int64_t)b * p.Nk + row) * p.vs + h * D + lc * 8) * 2);
+  }
+  const int NT = (p.Nk + KT - 1) / KT;
+  auto issue = [&](int t, int st) {
+    f16* Ks = smem + st * 2 * KT * D;
+    f16* Vs = Ks + KT * D;
+    const int key0 = t * KT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = key0 + k_key[j] < p.Nk;
+      S3_BLDS(rk, Ks + (wave * 2 + j) * 512, ok ? k_off[j] : kOOB, (int64_t)key0 * p.ks * 2);
+      S3_BLDS(rv, Vs + (wave * 2 + j) * 512, ok ? v_off[j] : kOOB, (int64_t)key0 * p.vs * 2);
+    }
+  };
+
+  float m_run[4], l_run[4];
+  f32x4 o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { m_run[r] = -INFINITY; l_run[r] = 0.f; }
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) o[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int AHEAD = kStages - 1;
+#pragma unroll
+  for (int i = 0; i < AHEAD; ++i)
+    if (i < NT) issue(i, i);
+  for (int t = 0; t < NT; ++t) {
+    wait_tiles<4, AHEAD - 1>(NT - 1 - t);
+    __builtin_amdgcn_s_barrier();
+    if (t + AHEAD < NT) issue(t + AHEAD, (t + AHEAD) % kStages);
+    const f16* Ks = smem + (t % kStages) * 2 * KT * D;
+    const f16* Vs = Ks + KT * D;
+    f32x4 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int krow = kb * 16 + (lane & 15);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = 4 * ks + (lane >> 4);
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(&Ks[krow * D + kswz(krow, c) * 8]);
+        s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[ks], kf, s[kb], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const bool kok = t * KT + kb * 16 + (lane & 15) < p.Nk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[kb][r] = kok ? s[kb][r] * p.scale_log2 : -INFINITY;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = fmaxf(fmaxf(s[0][r], s[1][r]), fmaxf(s[2][r], s[3][r]));
+#pragma unroll
+      for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
+      const float m_new = fmaxf(m_run[r], mx);
+      const float alpha = exp2f(m_run[r] - m_new);
+      m_run[r] = m_new;
+      l_run[r] *= alpha;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) o[nb][r] *= alpha;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float e = exp2f(s[kb][r] - m_new);
+        s[kb][r] = e;
+        l_run[r] += e;
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qr = 4 * (lane >> 4) + r;
+        Pw[qr * KT + kb * 16 + (lane & 15)] = (f16)s[kb][r];
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only: this wave's P writes landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const f16x8 pa = *reinterpret_cast<const f16x8*>(&Pw[(lane & 15) * KT + ks * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int grp = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+        const int key0 = ks * 32 + 8 * grp + q4;
+        const int dcol = nb * 16 + 4 * p4;
+        typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(&Vs[key0 * D + dcol]));
+        const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(&Vs[(key0 + 4) * D + dcol]));
+        f16x8 vb;
+        const f16x4 lo16 = __builtin_bit_cast(f16x4, lo);
+        const f16x4 hi16 = __builtin_bit_cast(f16x4, hi);
+        vb[0] = lo16[0]; vb[1] = lo16[1]; vb[2] = lo16[2]; vb[3] = lo16[3];
+        vb[4] = hi16[0]; vb[5] = hi16[1]; vb[6] = hi16[2]; vb[7] = hi16[3];
+        o[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa, vb, o[nb], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float l = l_run[r];
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) l += __shfl_xor(l, o2, 64);
+    l_run[r] = 1.0f / l;
+  }
+  f16* Og = p.O[g];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = qtile * QT + wave * 16 + 4 * (lane >> 4) + r;
+    if (row >= p.Nq) continue;
+    f16* op = Og + ((int64_t)b * p.Nq + row) * p.os + h * D;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) op[nb * 16 + (lane & 15)] = (f16)(o[nb][r] * l_run[r]);
+  }
+}
+
 }  // namespace
 
 extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
@@ -278,7 +466,12 @@ extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
   p.cosT = a->rope_cos; p.sinT = a->rope_sin; p.maxpos = a->rope_maxpos;
   p.scale_log2 = a->scale * 1.4426950408889634f;
   dim3 grid((a->Nq + QT - 1) / QT, a->B * a->H, a->groups);
-  k_attn<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+  bool rope = false;
+  for (int g = 0; g < a->groups; ++g) rope = rope || p.qpos[g] || p.kpos[g];
+  if (rope)
+    k_attn<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+  else
+    k_attn_dma<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

@@ -235,6 +235,40 @@ def test_attention_rope_vs_torch(B, N, Nk, H, cross):
     assert rel_err(o, ref) < 5e-3, rel_err(o, ref)
 
 
+@pytest.mark.parametrize("B,N,Nk,H,groups,strided", [(1, 768, 768, 16, 1, True),
+                                                     (1, 768, 768, 12, 2, False),
+                                                     (2, 100, 70, 4, 1, False),
+                                                     (3, 5, 130, 2, 2, True)])
+def test_attention_no_rope_dma_path(B, N, Nk, H, groups, strided):
+    """The LDS-DMA ring kernel (q/k pre-rotated by the GEMM epilogue): plain
+    softmax(QK^T s)V, K/V read from strided views like the fused QKV buffer."""
+    from splatt3r_amd import ops, _lib
+    D = 64
+    Qs, Ks, Vs, Os, refs = [], [], [], [], []
+    for g in range(groups):
+        if strided:
+            qkv = _rand(B * max(N, Nk), 3 * H * D, seed=70 + g)
+            q, k, v = qkv[:B * N, :H * D], qkv[:B * Nk, H * D:2 * H * D], qkv[:B * Nk, 2 * H * D:]
+            qs = ks = vs = 3 * H * D
+        else:
+            q, k, v = (_rand(B * N, H * D, seed=80 + g), _rand(B * Nk, H * D, seed=90 + g),
+                       _rand(B * Nk, H * D, seed=100 + g))
+            qs = ks = vs = H * D
+        o = torch.empty(B * N, H * D, device="cuda", dtype=torch.float16)
+        Qs.append(q); Ks.append(k); Vs.append(v); Os.append(o)
+        Qf = q.float().reshape(B, N, H, D).transpose(1, 2)
+        Kf = k.float().reshape(B, Nk, H, D).transpose(1, 2)
+        Vf = v.float().reshape(B, Nk, H, D).transpose(1, 2)
+        r = ((Qf @ Kf.transpose(-2, -1)) * D ** -0.5).softmax(-1) @ Vf
+        refs.append(r.transpose(1, 2).reshape(B * N, H * D))
+    if strided:   # the sliced views must keep the fused buffer's row stride
+        Qs = [t.as_strided((B * N, H * D), (qs, 1)) for t in Qs]
+    ops.attention(Qs, Ks, Vs, Os, B=B, Nq=N, Nk=Nk, H=H, q_stride=qs, k_stride=ks, v_stride=vs,
+                  o_stride=H * D, scale=D ** -0.5)(_lib.stream())
+    for g in range(groups):
+        assert rel_err(Os[g], refs[g]) < 5e-3, (g, rel_err(Os[g], refs[g]))
+
+
 def test_layernorm_vs_torch():
     from splatt3r_amd import ops, _lib
     for C in (1024, 768, 128):
