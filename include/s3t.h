@@ -32,6 +32,20 @@ int s3t_ray_dist_normal_eqs(const float* T /* device [8] */, const float* Xf, co
                             float sigma_ray, float sigma_dist, float huber_k,
                             void* workspace, float* out36, void* stream);
 
+/* Queue `iters` complete GN iterations on the stream with no host round
+ * trip: normal equations at the device pose T, then a one-thread fp64
+ * Cholesky solve, T <- Exp(tau) * T (lietorch retr) and the reference's
+ * convergence test (rel cost decrease < rel_error or |tau| < delta_norm).
+ * state (device double[4]): [0] previous cost (init +inf), [1] iterations
+ * done (init 0), [2] flag (init 0; 1 converged, 2 Cholesky failed,
+ * 3 max_iters reached), [3] last cost.  Once the flag is set every queued
+ * kernel returns immediately, so the host queues iterations in chunks and
+ * reads `state` once per chunk. */
+int s3t_gn_iterations(const float* Xf, const float* Xk, const float* Q, const uint8_t* valid,
+                      int64_t n, float sigma_ray, float sigma_dist, float huber_k, int iters,
+                      int max_iters, float rel_error, float delta_norm, float* T /* device [8] */,
+                      double* state, void* workspace, float* out36, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

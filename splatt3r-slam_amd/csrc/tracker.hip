@@ -15,9 +15,11 @@ constexpr int kMaxBlocks = 1024;
 constexpr int NV = 36;  // 28 (H upper) + 7 (g) + 1 (cost)
 
 __global__ void __launch_bounds__(kThreads)
-k_normal_eqs(const float* __restrict__ Tdev, const float* __restrict__ Xf, const float* __restrict__ Xk,
+k_normal_eqs(const double* __restrict__ state, const float* __restrict__ Tdev,
+             const float* __restrict__ Xf, const float* __restrict__ Xk,
              const float* __restrict__ Q, const uint8_t* __restrict__ valid, int64_t n,
              float inv_sr, float inv_sd, float hk, float* __restrict__ partial) {
+  if (state && state[2] != 0.0) return;   // the device-side GN loop has finished
   float T[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) T[k] = Tdev[k];
@@ -95,7 +97,9 @@ k_normal_eqs(const float* __restrict__ Tdev, const float* __restrict__ Xf, const
 
 // One workgroup per output value; fixed-order fp64 tree (deterministic).
 __global__ void __launch_bounds__(kThreads)
-k_finalize(const float* __restrict__ partial, int nblocks, float* __restrict__ out) {
+k_finalize(const double* __restrict__ state, const float* __restrict__ partial, int nblocks,
+           float* __restrict__ out) {
+  if (state && state[2] != 0.0) return;
   const int k = blockIdx.x;
   double s = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += kThreads) s += (double)partial[b * NV + k];
@@ -105,6 +109,64 @@ k_finalize(const float* __restrict__ partial, int nblocks, float* __restrict__ o
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) out[k] = (float)((red[0] + red[1]) + (red[2] + red[3]));
+}
+
+// One Gauss-Newton update on the device (tracker.py:156-171 + retr +
+// nonlinear_optimizer.check_convergence): fp64 Cholesky of the 7x7 normal
+// equations, tau = H^-1 g, T <- Exp(tau) * T, convergence flags.
+// state: [0] previous cost (starts +inf), [1] iterations done, [2] flag
+// (0 running, 1 converged, 2 Cholesky failed, 3 max iterations), [3] cost.
+__global__ void k_gn_solve(const float* __restrict__ out36, float* __restrict__ T,
+                           double* __restrict__ state, int max_iters, float rel_error,
+                           float delta_norm) {
+  if (threadIdx.x != 0 || state[2] != 0.0) return;
+  double H[7][7], g[7];
+  int q = 0;
+  for (int a = 0; a < 7; ++a)
+    for (int b = a; b < 7; ++b) H[a][b] = H[b][a] = (double)out36[q++];
+  for (int a = 0; a < 7; ++a) g[a] = (double)out36[28 + a];
+  const double cost = (double)out36[35];
+  // Cholesky H = L L^T (in place, lower)
+  for (int j = 0; j < 7; ++j) {
+    double d = H[j][j];
+    for (int k = 0; k < j; ++k) d -= H[j][k] * H[j][k];
+    if (!(d > 0.0) || !isfinite(d)) { state[2] = 2.0; return; }
+    const double l = sqrt(d);
+    H[j][j] = l;
+    for (int i = j + 1; i < 7; ++i) {
+      double v = H[i][j];
+      for (int k = 0; k < j; ++k) v -= H[i][k] * H[j][k];
+      H[i][j] = v / l;
+    }
+  }
+  double y[7], x[7];
+  for (int i = 0; i < 7; ++i) {
+    double v = g[i];
+    for (int k = 0; k < i; ++k) v -= H[i][k] * y[k];
+    y[i] = v / H[i][i];
+  }
+  for (int i = 6; i >= 0; --i) {
+    double v = y[i];
+    for (int k = i + 1; k < 7; ++k) v -= H[k][i] * x[k];
+    x[i] = v / H[i][i];
+  }
+  float tau[7], Tn[8], Tc[8];
+  double nrm = 0.0;
+  for (int i = 0; i < 7; ++i) {
+    tau[i] = (float)x[i];
+    nrm += (double)tau[i] * tau[i];
+  }
+  for (int k = 0; k < 8; ++k) Tc[k] = T[k];
+  s3lie::retr_sim3(Tc, tau, Tn);
+  for (int k = 0; k < 8; ++k) T[k] = Tn[k];
+  const double old = state[0];
+  const double rel = fabs((old - cost) / old);   // nan at the first step, like math.fabs(inf/inf)
+  const int it = (int)state[1] + 1;
+  state[1] = it;
+  state[3] = cost;
+  state[0] = cost;
+  if (rel < rel_error || sqrt(nrm) < delta_norm) state[2] = 1.0;
+  else if (it >= max_iters) state[2] = 3.0;
 }
 
 int blocks_for(int64_t n) {
@@ -127,10 +189,32 @@ extern "C" int s3t_ray_dist_normal_eqs(const float* T, const float* Xf, const fl
   const int nb = blocks_for(n);
   float* partial = static_cast<float*>(workspace);
   // reference: sqrt_info = 1 / sigma * valid * sqrt(Q)  (tracker.py:175-176)
-  k_normal_eqs<<<nb, kThreads, 0, st>>>(T, Xf, Xk, Q, valid, n, 1.0f / sigma_ray,
+  k_normal_eqs<<<nb, kThreads, 0, st>>>(nullptr, T, Xf, Xk, Q, valid, n, 1.0f / sigma_ray,
                                        1.0f / sigma_dist, huber_k, partial);
   S3_LAUNCH_CHECK();
-  k_finalize<<<NV, kThreads, 0, st>>>(partial, nb, out36);
+  k_finalize<<<NV, kThreads, 0, st>>>(nullptr, partial, nb, out36);
   S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+extern "C" int s3t_gn_iterations(const float* Xf, const float* Xk, const float* Q,
+                                 const uint8_t* valid, int64_t n, float sigma_ray,
+                                 float sigma_dist, float huber_k, int iters, int max_iters,
+                                 float rel_error, float delta_norm, float* T, double* state,
+                                 void* workspace, float* out36, void* stream) {
+  S3_REQUIRE(T && state && n >= 0 && workspace && out36 && iters >= 0,
+             "s3t_gn_iterations: bad arguments");
+  hipStream_t st = s3::as_stream(stream);
+  const int nb = blocks_for(n);
+  float* partial = static_cast<float*>(workspace);
+  for (int i = 0; i < iters; ++i) {
+    k_normal_eqs<<<nb, kThreads, 0, st>>>(state, T, Xf, Xk, Q, valid, n, 1.0f / sigma_ray,
+                                         1.0f / sigma_dist, huber_k, partial);
+    S3_LAUNCH_CHECK();
+    k_finalize<<<NV, kThreads, 0, st>>>(state, partial, nb, out36);
+    S3_LAUNCH_CHECK();
+    k_gn_solve<<<1, 64, 0, st>>>(out36, T, state, max_iters, rel_error, delta_norm);
+    S3_LAUNCH_CHECK();
+  }
   return S3_OK;
 }

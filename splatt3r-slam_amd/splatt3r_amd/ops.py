@@ -78,6 +78,9 @@ ACT = {"none": 0, "gelu": 1, "relu": 2}
 # S3_SYNC_DEBUG=1: run plans op by op with a device sync after each (fault
 # localisation); S3_GRAPHS=0 disables HIP-graph capture.
 DEBUG_SYNC = os.environ.get("S3_SYNC_DEBUG", "0") == "1"
+# tuning overrides for experiments: S3_GEMM_TILE=<1..8> replaces the
+# library's automatic tile choice (only where a call leaves tile=0)
+TILE_OVERRIDE = int(os.environ.get("S3_GEMM_TILE", "0"))
 GRAPHS_ENABLED = os.environ.get("S3_GRAPHS", "1") != "0"
 
 
@@ -182,7 +185,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         a.rope_pos = _parr(rope_pos)
         split_k = 1
     a.split_k = int(auto_split_k(M, N, K, groups) if split_k is None else split_k)
-    a.tile = int(tile)
+    a.tile = int(tile) or TILE_OVERRIDE
     ws = None
     if a.split_k > 1:
         nbytes = _lib.lib().s3n_gemm_workspace_bytes(ctypes.byref(a))

@@ -26,7 +26,11 @@ _lib.register({
     "s3t_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
     "s3t_ray_dist_normal_eqs": (ctypes.c_int, [P_, P_, P_, P_, P_, ctypes.c_int64, ctypes.c_float,
                                                ctypes.c_float, ctypes.c_float, P_, P_, P_]),
+    "s3t_gn_iterations": (ctypes.c_int, [P_, P_, P_, P_, ctypes.c_int64, ctypes.c_float,
+                                         ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_float, ctypes.c_float, P_, P_, P_, P_, P_]),
 })
+GN_CHUNK = 8   # iterations queued per host check of the device-side GN state
 
 _TRIU = [(a, b) for a in range(7) for b in range(a, 7)]
 _DEBUG = os.environ.get("S3_TRACK_DEBUG", "0") == "1"
@@ -55,6 +59,29 @@ class NormalEquations:
         self.host = torch.empty(36, pin_memory=True)
         self.pose = torch.empty(8, device=self.device)
         self.pose_host = torch.empty(8, pin_memory=True)
+        self.state = torch.empty(4, dtype=torch.float64, device=self.device)
+        self.state_init = torch.tensor([float("inf"), 0.0, 0.0, 0.0], dtype=torch.float64).pin_memory()
+        self.state_host = torch.empty(4, dtype=torch.float64, pin_memory=True)
+
+    def gn_begin(self, cfg):
+        """Reset the device GN state (the pose slot must already hold T)."""
+        self.state.copy_(self.state_init, non_blocking=True)
+
+    def gn_queue(self, Xf, Xk, Q, valid, cfg, iters):
+        """Queue `iters` device-side GN iterations; the state is copied to
+        the pinned host mirror behind them (read after a sync)."""
+        n = Xf.shape[0]
+        _lib.require_cuda(Xf, Xk, Q, valid)
+        _lib.require_contig("s3t_gn_iterations", Xf, Xk, Q, valid)
+        need = _lib.lib().s3t_workspace_bytes(n)
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        _lib.call("s3t_gn_iterations", Xf.data_ptr(), Xk.data_ptr(), Q.data_ptr(),
+                  valid.data_ptr(), n, cfg["sigma_ray"], cfg["sigma_dist"], cfg["huber"],
+                  int(iters), int(cfg["max_iters"]), float(cfg["rel_error"]),
+                  float(cfg["delta_norm"]), self.pose.data_ptr(), self.state.data_ptr(),
+                  self.ws.data_ptr(), self.out.data_ptr(), _lib.stream(self.device))
+        self.state_host.copy_(self.state, non_blocking=True)
 
     def set_pose_host(self, T: np.ndarray):
         """Stream-ordered upload of a host pose into the device slot."""
@@ -154,7 +181,8 @@ class FrameTracker:
         stats = torch.stack([valid_opt.sum(), valid_kf.sum(), hit.sum()]).to(torch.float64)
         stats_host = torch.empty(3, dtype=torch.float64, pin_memory=True)
         stats_host.copy_(stats, non_blocking=True)
-        # queue GN iteration 0 at the device-side relative pose before syncing
+        # queue the first GN chunk at the device-side relative pose, then one
+        # sync covers the decision statistics and (usually) the whole GN
         T_CkCf = T_WCk.inv() * T_WCf
         Xf = Xf.float().contiguous()
         Xk = Xk.float().contiguous()
@@ -162,20 +190,16 @@ class FrameTracker:
         valid_c = valid_opt.contiguous()
         ne = self.normal_eqs
         ne.pose.copy_(T_CkCf.data.reshape(8))
-        pose_host = torch.empty(8, pin_memory=True)
-        pose_host.copy_(ne.pose, non_blocking=True)
-        ne.launch(Xf, Xk, Q, valid_c, self.cfg["sigma_ray"], self.cfg["sigma_dist"],
-                  self.cfg["huber"])
-        first = ne.fetch()            # the one sync for stats + pose + iteration 0
+        ne.gn_begin(self.cfg)
+        ne.gn_queue(Xf, Xk, Q, valid_c, self.cfg, GN_CHUNK)
+        torch.cuda.current_stream(ne.device).synchronize()
         n_opt, n_kf, n_unique = stats_host.tolist()
 
         if n_opt / n < self.cfg["min_match_frac"]:
             print(f"Skipped frame {frame.frame_id}")
             return False, [], True
         try:
-            T_WCf, T_CkCf = self.opt_pose_ray_dist_sim3(
-                Xf, Xk, T_WCf, T_WCk, Q, valid_c,
-                _first=(pose_host.numpy().copy(), first))
+            T_WCf, T_CkCf = self._gn_finish(Xf, Xk, Q, valid_c, T_WCk)
         except CholeskyError:
             print(f"Cholesky failed {frame.frame_id}")
             return False, [], True
@@ -200,30 +224,55 @@ class FrameTracker:
         return (frame.X_canon[idx_f2k], keyframe.X_canon, frame.T_WC, keyframe.T_WC,
                 Cf[idx_f2k], Ck)
 
-    def opt_pose_ray_dist_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid, _first=None):
-        """tracker.py:173-214 with the per-iteration work fused on the GPU.
-        `_first` = (T, (H, g, cost)) when iteration 0 was already queued."""
-        cfg = self.cfg
+    def _gn_finish(self, Xf, Xk, Q, valid, T_WCk):
+        """Drive the device-side GN loop (first chunk already queued and
+        synced) to its flag; returns (T_WCf, T_CkCf)."""
+        cfg, ne = self.cfg, self.normal_eqs
+        while True:
+            iters, flag = int(ne.state_host[1]), int(ne.state_host[2])
+            if flag != 0 or iters >= cfg["max_iters"]:
+                break
+            ne.gn_queue(Xf, Xk, Q, valid, cfg, min(GN_CHUNK, cfg["max_iters"] - iters))
+            torch.cuda.current_stream(ne.device).synchronize()
+        self.last_iters = iters
+        if _DEBUG:
+            print(f"[gn] iters={iters} flag={flag} cost={float(ne.state_host[3]):.6g}", flush=True)
+        if flag == 2:
+            raise CholeskyError("normal equations not positive definite")
+        if flag == 3:
+            print("max iters reached 0")
+        T_CkCf = lietorch.Sim3(ne.pose.clone().view(1, 8))
+        return T_WCk * T_CkCf, T_CkCf
+
+    def opt_pose_ray_dist_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid):
+        """tracker.py:173-214: the whole GN loop runs on the device
+        (s3t_gn_iterations), checked by the host once per chunk."""
         ne = self.normal_eqs
         Xf = Xf.float().contiguous()
         Xk = Xk.float().contiguous()
         Q = Qk.float().contiguous()
         valid = valid.contiguous()
-        if _first is None:
-            T_CkCf = T_WCk.inv() * T_WCf
-            T = T_CkCf.data.reshape(8).detach().cpu().numpy().astype(np.float32)
-            first = None
-        else:
-            T, first = _first
+        T_CkCf = T_WCk.inv() * T_WCf
+        ne.pose.copy_(T_CkCf.data.reshape(8))
+        ne.gn_begin(self.cfg)
+        ne.gn_queue(Xf, Xk, Q, valid, self.cfg, GN_CHUNK)
+        torch.cuda.current_stream(ne.device).synchronize()
+        return self._gn_finish(Xf, Xk, Q, valid, T_WCk)
+
+    def opt_pose_ray_dist_sim3_host(self, Xf, Xk, T_WCf, T_WCk, Qk, valid):
+        """Host-driven variant (one fused normal-equation launch + host
+        Cholesky per iteration), kept for A/B checks of the device loop."""
+        cfg = self.cfg
+        ne = self.normal_eqs
+        T = (T_WCk.inv() * T_WCf).data.reshape(8).detach().cpu().numpy().astype(np.float32)
+        Xf = Xf.float().contiguous()
+        Xk = Xk.float().contiguous()
+        Q = Qk.float().contiguous()
+        valid = valid.contiguous()
         old_cost = float("inf")
         for step in range(cfg["max_iters"]):
-            if step == 0 and first is not None:
-                H, g, new_cost = first
-            else:
-                H, g, new_cost = ne(T, Xf, Xk, Q, valid, cfg["sigma_ray"], cfg["sigma_dist"],
-                                    cfg["huber"])
-            if _DEBUG:
-                print(f"[gn] step {step} cost={new_cost:.6g} Hdiag={np.diag(H)} T={T}", flush=True)
+            H, g, new_cost = ne(T, Xf, Xk, Q, valid, cfg["sigma_ray"], cfg["sigma_dist"],
+                                cfg["huber"])
             tau = solve_normal_eqs(H, g)
             T = _retr_host(T, tau)
             self.last_iters = step + 1

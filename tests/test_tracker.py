@@ -113,3 +113,33 @@ def test_opt_pose_ray_dist_sim3_recovers_pose():
     got = T_CkCf.act(d(Xf)).cpu().numpy()
     np.testing.assert_allclose(got, Xk, atol=2e-4)
     assert 1 <= tr.last_iters < 50
+
+
+@pytest.mark.gpu
+def test_device_gn_loop_matches_host_loop():
+    """s3t_gn_iterations (Cholesky/retr/convergence on the device) follows
+    the host-driven loop: same iteration count, same pose to fp32 noise."""
+    import lietorch
+    from splatt3r_amd.tracker import FrameTracker
+    Xf, Xk, Q, valid, _ = _scene(196608, 5, noise=0.01)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    I = lietorch.Sim3.Identity(1, device="cuda")
+    tr = FrameTracker(None, None, "cuda")
+    _, T_dev = tr.opt_pose_ray_dist_sim3(d(Xf), d(Xk), I, I, d(Q), d(valid))
+    it_dev = tr.last_iters
+    _, T_host = tr.opt_pose_ray_dist_sim3_host(d(Xf), d(Xk), I, I, d(Q), d(valid))
+    assert abs(tr.last_iters - it_dev) <= 1
+    np.testing.assert_allclose(T_dev.data.cpu().numpy(), T_host.data.cpu().numpy(), atol=2e-5)
+
+
+@pytest.mark.gpu
+def test_device_gn_reports_cholesky_failure():
+    import lietorch
+    from splatt3r_amd.tracker import CholeskyError, FrameTracker
+    Xf, Xk, Q, valid, _ = _scene(4096, 6)
+    valid[:] = False                       # H = 0: not positive definite
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    I = lietorch.Sim3.Identity(1, device="cuda")
+    tr = FrameTracker(None, None, "cuda")
+    with pytest.raises(CholeskyError):
+        tr.opt_pose_ray_dist_sim3(d(Xf), d(Xk), I, I, d(Q), d(valid))
