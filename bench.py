@@ -94,7 +94,7 @@ def _kernel_profile(net, reps=3):
             recs += plan.run_timed()
     torch.cuda.synchronize()
     agg = {}
-    for kind, flops, e0, e1 in recs:
+    for kind, flops, e0, e1, *_ in recs:
         a = agg.setdefault(kind, [0, 0, 0.0])
         a[0] += 1
         a[1] += flops
