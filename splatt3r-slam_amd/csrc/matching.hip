@@ -10,6 +10,8 @@
 #include "common.hpp"
 #include "s3m.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -178,6 +180,93 @@ k_refine(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
   p1_new[pi * 2 + 1] = v_new;
 }
 
+// Cooperative refine: 16 lanes per query point (4 queries per wave).  At
+// each dilation level the (2r+1)^2 window candidates are dealt round-robin
+// over the 16 lanes, every lane issues the descriptor loads of all its
+// candidates before any arithmetic (up to 4 x 3 16-B loads in flight per
+// lane, instead of one dependent candidate at a time), and a 16-lane
+// butterfly picks the level's winner.  Same result as the sequential scan
+// of matching_kernels.cu:50-72: the sequential loop keeps the FIRST
+// candidate (in (i, j) order) that strictly beats the running maximum, which
+// is the smallest-index candidate holding the level's maximum score if that
+// score beats the maximum carried in from the previous levels.  The fp16
+// dot product keeps the reference's rounding of every product and partial
+// sum (v_mul_f16 / v_add_f16, no contraction in this file).
+constexpr int kRefLanes = 16;
+constexpr int kRefMaxPer = 4;   // candidates per lane -> (2r+1)^2 <= 64, r <= 3
+
+template <int F>
+__global__ void __launch_bounds__(kBlock)
+k_refine_coop(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
+              const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
+              int n, int radius, int dilation_max) {
+  static_assert(F % 8 == 0, "16-B descriptor chunks");
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  constexpr int NC = F / 8;
+  const int lane = threadIdx.x & (kRefLanes - 1);
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kRefLanes;
+  const int64_t b = blockIdx.y;
+  const bool live = i < n;                 // dead groups still join the shuffles
+  const int64_t pi = b * (int64_t)n + (live ? i : 0);
+  const h8* q8 = reinterpret_cast<const h8*>(D21 + pi * F);
+  h8 q[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) q[c] = q8[c];
+  const _Float16* d11 = D11 + b * (int64_t)h * w * F;
+
+  const int side = 2 * radius + 1, ncand = side * side;
+  int64_t u0 = p1[pi * 2 + 0], v0 = p1[pi * 2 + 1];
+  float max_score = 0.0f;                  // Half() == 0, see k_refine
+  int64_t u_new = u0, v_new = v0;
+  for (int d = dilation_max; d > 0; --d) {
+    const int rd = radius * d;
+    h8 row[kRefMaxPer][NC];
+    bool ok[kRefMaxPer];
+#pragma unroll
+    for (int t = 0; t < kRefMaxPer; ++t) {
+      const int c = lane + t * kRefLanes;
+      const int ii = c / side, jj = c - ii * side;
+      const int64_t u = u0 - rd + (int64_t)ii * d, v = v0 - rd + (int64_t)jj * d;
+      ok[t] = live && c < ncand && v >= 0 && v < h && u >= 0 && u < w;
+      const h8* r8 = reinterpret_cast<const h8*>(d11 + (ok[t] ? (v * w + u) * F : 0));
+#pragma unroll
+      for (int cc = 0; cc < NC; ++cc) row[t][cc] = r8[cc];
+    }
+    float best = -INFINITY;
+    int best_c = 1 << 30;
+#pragma unroll
+    for (int t = 0; t < kRefMaxPer; ++t) {
+      _Float16 score = (_Float16)0.0f;
+#pragma unroll
+      for (int cc = 0; cc < NC; ++cc) {
+        const h8 prod = q[cc] * row[t][cc];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) score = score + prod[e];
+      }
+      // candidates of one lane come in increasing index: strict > keeps the first
+      if (ok[t] && (float)score > best) { best = (float)score; best_c = lane + t * kRefLanes; }
+    }
+#pragma unroll
+    for (int m = kRefLanes / 2; m > 0; m >>= 1) {
+      const float ob = __shfl_xor(best, m, kRefLanes);
+      const int oc = __shfl_xor(best_c, m, kRefLanes);
+      if (ob > best || (ob == best && oc < best_c)) { best = ob; best_c = oc; }
+    }
+    if (best > max_score) {
+      max_score = best;
+      const int ii = best_c / side, jj = best_c - ii * side;
+      u_new = u0 - rd + (int64_t)ii * d;
+      v_new = v0 - rd + (int64_t)jj * d;
+    }
+    u0 = u_new;
+    v0 = v_new;
+  }
+  if (live && lane == 0) {
+    p1_new[pi * 2 + 0] = u_new;
+    p1_new[pi * 2 + 1] = v_new;
+  }
+}
+
 // |x| / max(||x||, 1e-12) (F.normalize), strict order ((x0^2+x1^2)+x2^2).
 __device__ __forceinline__ void normalize3(const float* x, float* o) {
   float nrm = sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
@@ -289,7 +378,18 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* 
   dim3 grid((unsigned)s3::cdiv(n, kBlock), (unsigned)b);
   auto d11 = reinterpret_cast<const _Float16*>(D11);
   auto d21 = reinterpret_cast<const _Float16*>(D21);
-  if (fdim == 24)
+  const int side = 2 * radius + 1;
+  if (side * side <= kRefLanes * kRefMaxPer && (fdim == 24 || fdim == 16 || fdim == 32)) {
+    dim3 cg((unsigned)s3::cdiv((int64_t)n * kRefLanes, kBlock), (unsigned)b);
+    auto go = [&](auto tag) {
+      constexpr int F = decltype(tag)::value;
+      k_refine_coop<F><<<cg, kBlock, 0, s3::as_stream(stream)>>>(d11, d21, p1, p1_new, h, w, n,
+                                                               radius, dilation_max);
+    };
+    if (fdim == 24) go(std::integral_constant<int, 24>{});
+    else if (fdim == 16) go(std::integral_constant<int, 16>{});
+    else go(std::integral_constant<int, 32>{});
+  } else if (fdim == 24)
     k_refine<24><<<grid, kBlock, 0, s3::as_stream(stream)>>>(
         d11, d21, p1, p1_new, h, w, n, fdim, radius, dilation_max);
   else

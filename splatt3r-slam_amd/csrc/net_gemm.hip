@@ -101,26 +101,11 @@ __device__ __forceinline__ void wait_tiles(int after) {
   }
 }
 
-// bias -> act -> + R1 -> + R2 -> store (plain / ConvT / pixel-shuffle
-// scatter) -> optional fp16 copy, for one output element.
-template <bool kBias = true>
-__device__ __forceinline__ void epilogue(const GemmP& p, int g, int row, int col, float v) {
-  const float* __restrict__ bias = p.bias[g];
-  const void* R1 = p.R1[g];
-  const void* R2 = p.R2[g];
+// Store of one finished element (plain / ConvT / pixel-shuffle scatter) and
+// its optional fp16 copy.
+__device__ __forceinline__ void store_out(const GemmP& p, int g, int row, int col, float v) {
   void* C = p.C[g];
   f16* C2 = p.C2[g];
-  if (kBias && bias) v += bias[col];
-  if (p.act == S3N_ACT_GELU) v = gelu(v);
-  else if (p.act == S3N_ACT_RELU) v = fmaxf(v, 0.0f);
-  if (R1) {
-    const int64_t o = (int64_t)row * p.ldr1 + col;
-    v += p.r1_f16 ? (float)reinterpret_cast<const f16*>(R1)[o] : reinterpret_cast<const float*>(R1)[o];
-  }
-  if (R2) {
-    const int64_t o = (int64_t)row * p.ldr2 + col;
-    v += p.r2_f16 ? (float)reinterpret_cast<const f16*>(R2)[o] : reinterpret_cast<const float*>(R2)[o];
-  }
   int64_t off;
   if (p.store_mode == S3N_STORE_PLAIN) {
     off = (int64_t)row * p.ldc + col;
@@ -147,10 +132,101 @@ __device__ __forceinline__ void epilogue(const GemmP& p, int g, int row, int col
   if (C2) C2[(int64_t)row * p.ldc2 + col] = (f16)v;
 }
 
+__device__ __forceinline__ float act_fn(const GemmP& p, float v) {
+  if (p.act == S3N_ACT_GELU) return gelu(v);
+  if (p.act == S3N_ACT_RELU) return fmaxf(v, 0.0f);
+  return v;
+}
+
+__device__ __forceinline__ float load_res(const void* R, int r_f16, int64_t o) {
+  return r_f16 ? (float)reinterpret_cast<const f16*>(R)[o] : reinterpret_cast<const float*>(R)[o];
+}
+
+// bias -> act -> + R1 -> + R2 -> store, for one element (split-K combine).
+template <bool kBias = true>
+__device__ __forceinline__ void epilogue(const GemmP& p, int g, int row, int col, float v) {
+  const float* __restrict__ bias = p.bias[g];
+  if (kBias && bias) v += bias[col];
+  v = act_fn(p, v);
+  if (p.R1[g]) v += load_res(p.R1[g], p.r1_f16, (int64_t)row * p.ldr1 + col);
+  if (p.R2[g]) v += load_res(p.R2[g], p.r2_f16, (int64_t)row * p.ldr2 + col);
+  store_out(p, g, row, col, v);
+}
+
+// Row of accumulator register r of a 32x32 MFMA block, relative to the
+// block row of this lane half (lane >> 5 adds 4).
+__device__ __forceinline__ int acc_row(int r) { return (r & 3) + 8 * (r >> 2); }
+
+// The same epilogue for the 16 elements one lane holds of a 32x32 block
+// (rows row0 + acc_row(r), one column).  Every operand load is issued before
+// the first store: R1 may be the output itself (in-place residual add), so
+// a load placed after a store could not be hoisted and each of the 16 would
+// pay a full memory latency on its own.
+template <bool kBias = true>
+__device__ __forceinline__ void epilogue_block(const GemmP& p, int g, int row0, int col,
+                                               const float (&v)[16]) {
+  if (col >= p.N) return;
+  const float* __restrict__ bias = p.bias[g];
+  const void* R1 = p.R1[g];
+  const void* R2 = p.R2[g];
+  const float bv = (kBias && bias) ? bias[col] : 0.0f;
+  // rows past M only occur in the last row tile: clamp the loads there
+  // (their values are dropped), so the load batch stays branch-free
+  const int rmax = p.M - 1 - row0;
+  float r1[16], r2[16];
+  if (R1) {
+    const int64_t o = (int64_t)row0 * p.ldr1 + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      r1[r] = load_res(R1, p.r1_f16, o + (int64_t)min(acc_row(r), rmax) * p.ldr1);
+  }
+  if (R2) {
+    const int64_t o = (int64_t)row0 * p.ldr2 + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      r2[r] = load_res(R2, p.r2_f16, o + (int64_t)min(acc_row(r), rmax) * p.ldr2);
+  }
+  float x[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float t = v[r];
+    if (kBias && bias) t += bv;
+    t = act_fn(p, t);
+    if (R1) t += r1[r];
+    if (R2) t += r2[r];
+    x[r] = t;
+  }
+  if (p.store_mode == S3N_STORE_PLAIN) {
+    const int64_t o = (int64_t)row0 * p.ldc + col;
+    f16* C2 = p.C2[g];
+    const int64_t o2 = (int64_t)row0 * p.ldc2 + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (acc_row(r) > rmax) continue;
+      const int64_t e = o + (int64_t)acc_row(r) * p.ldc;
+      if (p.c_f16) reinterpret_cast<f16*>(p.C[g])[e] = (f16)x[r];
+      else reinterpret_cast<float*>(p.C[g])[e] = x[r];
+      if (C2) C2[o2 + (int64_t)acc_row(r) * p.ldc2] = (f16)x[r];
+    }
+  } else {
+    for (int r = 0; r < 16; ++r)
+      if (acc_row(r) <= rmax) store_out(p, g, row0 + acc_row(r), col, x[r]);
+  }
+}
+
 // NWM x NWN waves, each owning a (BM/NWM) x (BN/NWN) block of 32x32
 // accumulators.
+// Waves per SIMD the LDS footprint allows (the register budget the
+// compiler may use without costing occupancy).
+constexpr int lds_waves_per_simd(int BM, int BN, int NW, int S) {
+  const int wg = (160 * 1024) / (S * (BM + BN) * 64 * 2);
+  const int w = (wg > 8 ? 8 : wg) * NW / 4;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
 template <int BM, int BN, int NWM, int NWN, int AMODE, int kStages>
-__global__ void __launch_bounds__(64 * NWM * NWN) k_gemm(GemmP p) {
+__global__ void __launch_bounds__(64 * NWM * NWN, lds_waves_per_simd(BM, BN, NWM * NWN, kStages))
+k_gemm(GemmP p) {
   constexpr int NW = NWM * NWN;
   constexpr int WM = BM / NWM, WN = BN / NWN;
   constexpr int FM = WM / 32, FN = WN / 32;
@@ -335,6 +411,7 @@ __global__ void __launch_bounds__(64 * NWM * NWN) k_gemm(GemmP p) {
   if (p.rope_pos[g]) {
     // bias, then RoPE: the partner column (col ^ 16, same rows) sits in lane
     // ^ 16 of the same 32x32 accumulator, so one xor-shuffle fetches it.
+    // Positions, then the cos/sin rows, are loaded for all 16 rows at once.
     const int64_t* __restrict__ pos = p.rope_pos[g];
     const float* __restrict__ bias = p.bias[g];
 #pragma unroll
@@ -342,22 +419,31 @@ __global__ void __launch_bounds__(64 * NWM * NWN) k_gemm(GemmP p) {
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const int col = n0 + wn * WN + fn * 32 + (lane & 31);
+        const int row0 = m0 + wm * WM + fm * 32 + 4 * (lane >> 5);
         const float bv = (bias && col < N) ? bias[col] : 0.0f;
         const int d = col & 63, j = col & 15;
         const bool lo = (col & 31) < 16, rot = col < p.rope_ncols;
+        float x[16], xp[16];
+        int64_t ps[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm * WM + fm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          float x = acc[fm][fn][r] + bv;
-          const float xp = __shfl_xor(x, 16, 64);
-          if (row >= M || col >= N) continue;
-          if (rot) {
-            const int64_t ps = pos[(int64_t)row * 2 + (d >> 5)];
-            const float cs = p.rope_cos[ps * 16 + j], sn = p.rope_sin[ps * 16 + j];
-            x = lo ? x * cs - xp * sn : x * cs + xp * sn;
-          }
-          epilogue<false>(p, g, row, col, x);
+          x[r] = acc[fm][fn][r] + bv;
+          xp[r] = __shfl_xor(x[r], 16, 64);
+          const int row = row0 + acc_row(r);
+          ps[r] = (rot && row < M) ? pos[(int64_t)row * 2 + (d >> 5)] : 0;
         }
+        if (rot) {
+          float cs[16], sn[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            cs[r] = p.rope_cos[ps[r] * 16 + j];
+            sn[r] = p.rope_sin[ps[r] * 16 + j];
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            x[r] = lo ? x[r] * cs[r] - xp[r] * sn[r] : x[r] * cs[r] + xp[r] * sn[r];
+        }
+        epilogue_block<false>(p, g, row0, col, x);
       }
     return;
   }
@@ -366,15 +452,19 @@ __global__ void __launch_bounds__(64 * NWM * NWN) k_gemm(GemmP p) {
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       const int col = n0 + wn * WN + fn * 32 + (lane & 31);
+      const int row0 = m0 + wm * WM + fm * 32 + 4 * (lane >> 5);
       if (col >= N) continue;
+      if (p.split_k > 1) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WM + fm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= M) continue;
-        if (p.split_k > 1)
-          p.ws[(((int64_t)g * p.split_k + s_idx) * M + row) * N + col] = acc[fm][fn][r];
-        else
-          epilogue(p, g, row, col, acc[fm][fn][r]);
+        for (int r = 0; r < 16; ++r) {
+          const int row = row0 + acc_row(r);
+          if (row < M) p.ws[(((int64_t)g * p.split_k + s_idx) * M + row) * N + col] = acc[fm][fn][r];
+        }
+      } else {
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[fm][fn][r];
+        epilogue_block(p, g, row0, col, v);
       }
     }
 }

@@ -135,6 +135,24 @@ def test_hip_refine_bitexact_vs_oracle(f):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("f,radius,dil", [(24, 3, 5), (24, 2, 3), (32, 1, 2), (24, 4, 2), (8, 3, 5)])
+def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil):
+    """Quantised descriptors make many equal fp16 scores: the cooperative
+    kernel must keep the first candidate in the reference's scan order.
+    radius 4 (81 candidates) and fdim 8 take the per-lane kernel."""
+    import mast3r_slam_backends as be
+    rng = np.random.default_rng(100 + f + radius)
+    b, h, w = 2, 33, 47
+    D11 = (rng.integers(-2, 3, size=(b, h, w, f)) * 0.125).astype(np.float16)
+    D21 = (rng.integers(-2, 3, size=(b, h * w, f)) * 0.125).astype(np.float16)
+    p1 = np.stack([rng.integers(-3, w + 3, size=(b, h * w)),
+                   rng.integers(-3, h + 3, size=(b, h * w))], -1).astype(np.int64)
+    ref = oracle.refine_matches(D11, D21, p1, radius, dil)
+    (out,) = be.refine_matches(_to(D11), _to(D21), _to(p1), radius, dil)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
 def test_hip_match_end_to_end_vs_oracle():
     from splatt3r_amd.matching import match
     rng = np.random.default_rng(7)
