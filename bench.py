@@ -58,6 +58,8 @@ def _args():
     ap.add_argument("--no-c3", action="store_true", help="skip the 4.19M-splat raster microbench")
     ap.add_argument("--no-pairs", action="store_true", help="skip the keyframe-pair batch leg")
     ap.add_argument("--pairs-per-rank", type=int, default=4)
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="encode each frame inside its own step (no side-stream overlap)")
     return ap.parse_args()
 
 
@@ -169,11 +171,14 @@ def main():
     seed = 1234
     model = load_splatt3r(None, device=dev, cfg=FULL, seed=seed, symmetric=True)
     nfr = a.warmup + a.steps + 1
-    frames = tum_like_sequence(nfr, H, W, seed=rank, step_px=2.0, device=dev)
+    # one frame past the last timed one: its encoder is queued (pipelined)
+    # by the last timed step, so the timed region holds exactly K encodes
+    frames = tum_like_sequence(nfr + 1, H, W, seed=rank, step_px=2.0, device=dev)
     fe = Frontend(model, device=dev, spatial_stride=4, render=True)
+    nxt = (lambda i: None) if a.no_pipeline else (lambda i: frames[i + 1])
 
     for i in range(a.warmup + 1):          # frame 0 = INIT, then W tracked frames
-        fe.step(i, frames[i])
+        fe.step(i, frames[i], next_img=nxt(i))
     torch.cuda.synchronize()
     s0 = dict(fe.stats)
     model.encoder.events = []
@@ -181,7 +186,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.warmup + 1, nfr):
-        fe.step(i, frames[i])
+        fe.step(i, frames[i], next_img=nxt(i))
     torch.cuda.synchronize()
     _barrier(ws)
     t = time.perf_counter() - t0

@@ -11,6 +11,15 @@ rendering on (the default):
   gaussians_to_world            when should_append_gaussians says so
   splatt3r_render               2*h*w splats into the frame's view, read
                                 back to host (the reference writes a PNG)
+
+Software pipelining: when the caller passes the next frame's image
+(`step(i, img, next_img=...)`, as the reference's loop could with
+dataset[i + 1]), the encoder of frame i + 1 is queued on a side HIP stream
+before frame i's decoder, matching, GN and render are queued on the main
+stream, so the two chains share the chip (the 768-token GEMMs fill only a
+part of the 256 CUs) and the encoder also fills the host-sync gaps of the
+tracker.  Every frame is still encoded exactly once, from its own image;
+the outputs are identical.
 """
 from __future__ import annotations
 
@@ -61,6 +70,35 @@ class Frontend:
                           gaussians_world=0, rendered=0)
         self.last_render = None
         self.fps_timer = None
+        self.enc_stream = torch.cuda.Stream(device=device) if torch.cuda.is_available() else None
+        self._next = None          # (frame index, Frame whose encoder is queued, done event)
+
+    def _prefetch(self, i, img):
+        """Create frame i and queue its encoder on the side stream."""
+        main = torch.cuda.current_stream(self.device)
+        frame = create_frame(i, img, None, device=self.device)
+        ready = torch.cuda.Event()
+        ready.record(main)                       # the image upload / producer
+        with torch.cuda.stream(self.enc_stream):
+            self.enc_stream.wait_event(ready)
+            frame.feat, frame.pos, _ = self.model.encoder._encode_image(frame.img,
+                                                                         frame.img_true_shape)
+            done = torch.cuda.Event()
+            done.record(self.enc_stream)
+        # allocated on the side stream, read on the main one
+        frame.feat.record_stream(main)
+        frame.pos.record_stream(main)
+        frame.img.record_stream(self.enc_stream)
+        self._next = (i, frame, done)
+
+    def _take_prefetched(self, i, T_WC):
+        if self._next is None or self._next[0] != i:
+            return None
+        _, frame, done = self._next
+        self._next = None
+        torch.cuda.current_stream(self.device).wait_event(done)
+        frame.T_WC = T_WC
+        return frame
 
     def _render(self, frame, ref, target):
         if not self.render:
@@ -78,12 +116,21 @@ class Frontend:
             self.stats["gaussians_world"] += int(gs[0].shape[0])
         return gs
 
-    def step(self, i: int, img) -> Frame:
+    def step(self, i: int, img, next_img=None) -> Frame:
         if self.fps_timer is None:
             self.fps_timer = time.time()
         T_WC = (lietorch.Sim3.Identity(1, device=self.device) if self.last_T_WC is None
                 else self.last_T_WC)
-        frame = create_frame(i, img, T_WC, device=self.device)
+        frame = self._take_prefetched(i, T_WC)
+        if frame is None and self.enc_stream is not None:
+            # every encode goes through the side stream (one encoder plan,
+            # one stream: no two replays of its buffers can overlap)
+            self._prefetch(i, img)
+            frame = self._take_prefetched(i, T_WC)
+        if frame is None:
+            frame = create_frame(i, img, T_WC, device=self.device)
+        if next_img is not None and self.enc_stream is not None:
+            self._prefetch(i + 1, next_img)
         self.stats["frames"] += 1
         add_new_kf = False
         if self.mode == Mode.INIT:
