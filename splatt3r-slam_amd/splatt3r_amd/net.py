@@ -110,8 +110,17 @@ class PackedWeights:
         hp = ("downstream_head1", "downstream_head2")
         self.mlp_fc1_w = torch.stack([lin(f"{h}.head_local_features.fc1.weight") for h in hp])
         self.mlp_fc1_b = torch.stack([f32(sd[f"{h}.head_local_features.fc1.bias"]) for h in hp])
-        self.mlp_fc2_w = torch.stack([lin(f"{h}.head_local_features.fc2.weight") for h in hp])
-        self.mlp_fc2_b = torch.stack([f32(sd[f"{h}.head_local_features.fc2.bias"]) for h in hp])
+        # fc2 rows are stored pixel-shuffle-permuted: GEMM column (i*p + j)*Cout + co
+        # holds reference output channel co*p*p + i*p + j (F.pixel_shuffle), so
+        # the epilogue's ConvT-style scatter writes each (i, j) row run as one
+        # contiguous stretch of p*Cout floats instead of Cout-strided scalars
+        pp = cfg.patch * cfg.patch
+        fc2 = torch.stack([lin(f"{h}.head_local_features.fc2.weight") for h in hp])
+        fb2 = torch.stack([f32(sd[f"{h}.head_local_features.fc2.bias"]) for h in hp])
+        cout = fc2.shape[1] // pp
+        perm = torch.arange(fc2.shape[1], device=fc2.device).view(cout, pp).t().reshape(-1)
+        self.mlp_fc2_w = fc2[:, perm].contiguous()
+        self.mlp_fc2_b = fb2[:, perm].contiguous()
         # DPTs: groups (h1 pts, h1 gauss, h2 pts, h2 gauss)
         dp = (f"{hp[0]}.dpt", f"{hp[0]}.gaussian_dpt.dpt", f"{hp[1]}.dpt", f"{hp[1]}.gaussian_dpt.dpt")
         S = lambda fn: torch.stack([fn(d) for d in dp])
@@ -331,7 +340,7 @@ class PairPlan:
                        bias=_g(w.mlp_fc1_b, 2), act="gelu"))
         P.add(ops.gemm(_g(um, 2), _g(w.mlp_fc2_w, 2), _g(self.feat25, 2), M, nloc, hidm, lda=hidm,
                        bias=_g(w.mlp_fc2_b, 2),
-                       store=("pixshuf", ht, wt, p, nloc // (p * p))))
+                       store=("convt", ht, wt, p, nloc // (p * p))))   # rows pre-permuted
         # ---- DPTs: 4 groups (h1 pts, h1 gauss, h2 pts, h2 gauss)
         g4 = lambda t: _g(t, 4)
         head_of = (0, 0, 1, 1)
