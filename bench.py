@@ -58,6 +58,8 @@ def _args():
     ap.add_argument("--no-c3", action="store_true", help="skip the 4.19M-splat raster microbench")
     ap.add_argument("--no-pairs", action="store_true", help="skip the keyframe-pair batch leg")
     ap.add_argument("--pairs-per-rank", type=int, default=4)
+    ap.add_argument("--no-kprof", action="store_true",
+                    help="skip the per-launch network profile (roofline object)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="encode each frame inside its own step (no side-stream overlap)")
     return ap.parse_args()
@@ -217,7 +219,7 @@ def main():
                             "keyframes": st["keyframes"], "reloc": st["reloc"],
                             "rendered": st["rendered"], "tracked": st["tracked"]},
     }
-    if rank == 0:
+    if rank == 0 and not a.no_kprof:
         prof = _kernel_profile(model.encoder)
         flops_frame = sum(v[1] for v in prof.values())
         net_tflops = sum(v[1] for v in prof.values()) / (sum(v[2] for v in prof.values()) * 1e-3) / 1e12

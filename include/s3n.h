@@ -96,6 +96,11 @@ typedef struct {
 size_t s3n_gemm_workspace_bytes(const s3n_gemm_args* args);
 int s3n_gemm(const s3n_gemm_args* args, void* stream);
 
+/* Tuning hook (not on the product path): flags applied to later s3n_gemm
+ * launches; 1 = skip the MFMAs, 2 = skip the operand DMA (results are then
+ * garbage).  0 restores normal operation. */
+void s3n_gemm_set_debug(int flags);
+
 /* Fused multi-head attention softmax(Q K^T * scale) V with 2-D RoPE
  * (pos_embed.py:142-159, base 100, F0 1) applied to Q and K on load.
  * Q rows at Q + (b*Nq + n)*q_stride + h*64, K/V likewise; O rows at

@@ -182,7 +182,7 @@ k_refine(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
 
 // Cooperative refine: 16 lanes per query point (4 queries per wave).  At
 // each dilation level the (2r+1)^2 window candidates are dealt round-robin
-// over the 16 lanes, every lane issues the descriptor loads of all its
+// over the 16 lanes in image-row order, every lane issues the descriptor loads of all its
 // candidates before any arithmetic (up to 4 x 3 16-B loads in flight per
 // lane, instead of one dependent candidate at a time), and a 16-lane
 // butterfly picks the level's winner.  Same result as the sequential scan
@@ -222,12 +222,17 @@ k_refine_coop(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21
     const int rd = radius * d;
     h8 row[kRefMaxPer][NC];
     bool ok[kRefMaxPer];
+    int cidx[kRefMaxPer];
 #pragma unroll
     for (int t = 0; t < kRefMaxPer; ++t) {
-      const int c = lane + t * kRefLanes;
-      const int ii = c / side, jj = c - ii * side;
+      // slot s walks the window row by row (u fastest), so the lanes of a
+      // query read neighbouring pixels of one image row; c is the
+      // candidate's index in the reference's (i = u outer, j = v inner) scan
+      const int s = lane + t * kRefLanes;
+      const int jj = s / side, ii = s - jj * side;
+      cidx[t] = ii * side + jj;
       const int64_t u = u0 - rd + (int64_t)ii * d, v = v0 - rd + (int64_t)jj * d;
-      ok[t] = live && c < ncand && v >= 0 && v < h && u >= 0 && u < w;
+      ok[t] = live && s < ncand && v >= 0 && v < h && u >= 0 && u < w;
       const h8* r8 = reinterpret_cast<const h8*>(d11 + (ok[t] ? (v * w + u) * F : 0));
 #pragma unroll
       for (int cc = 0; cc < NC; ++cc) row[t][cc] = r8[cc];
@@ -243,8 +248,8 @@ k_refine_coop(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21
 #pragma unroll
         for (int e = 0; e < 8; ++e) score = score + prod[e];
       }
-      // candidates of one lane come in increasing index: strict > keeps the first
-      if (ok[t] && (float)score > best) { best = (float)score; best_c = lane + t * kRefLanes; }
+      const float sc = (float)score;
+      if (ok[t] && (sc > best || (sc == best && cidx[t] < best_c))) { best = sc; best_c = cidx[t]; }
     }
 #pragma unroll
     for (int m = kRefLanes / 2; m > 0; m >>= 1) {

@@ -45,6 +45,7 @@ struct GemmP {
   int tiles_m, tiles_n;
   int split_k, kt_per_split;
   float* ws;
+  int debug;       // s3n_gemm_set_debug flags (tuning only)
   int col_major;   // tile order: 1 = M fastest (each XCD owns a band of N)
   const float* rope_cos;
   const float* rope_sin;
@@ -324,7 +325,7 @@ k_gemm(GemmP p) {
       if constexpr (AMODE == kDense) {
         off = a_off[j];
         if (tail && k0 + a_kc[j] * 8 >= K) off = kOOB;
-        S3_BLDS(ra, As + (wave * AW + j) * 512, off, k0 * 2);
+        if (!(p.debug & 2)) S3_BLDS(ra, As + (wave * AW + j) * 512, off, k0 * 2);
       } else {
         off = kOOB;
         const int iy = a_iy0[j] + c_ky[j], ix = a_ix0[j] + c_kx[j];
@@ -336,14 +337,14 @@ k_gemm(GemmP p) {
           c_ci[j] -= p.cC;
           if (++c_kx[j] == p.ks) { c_kx[j] = 0; ++c_ky[j]; }
         }
-        S3_BLDS(ra, As + (wave * AW + j) * 512, off, 0);
+        if (!(p.debug & 2)) S3_BLDS(ra, As + (wave * AW + j) * 512, off, 0);
       }
     }
 #pragma unroll
     for (int j = 0; j < BW; ++j) {
       uint32_t off = b_off[j];
       if (tail && k0 + b_kc[j] * 8 >= K) off = kOOB;
-      S3_BLDS(rb, Bs + (wave * BW + j) * 512, off, k0 * 2);
+      if (!(p.debug & 2)) S3_BLDS(rb, Bs + (wave * BW + j) * 512, off, k0 * 2);
     }
   };
 
@@ -389,6 +390,7 @@ k_gemm(GemmP p) {
       }
     }
     if (kt + AHEAD < KT) issue(kt_begin + kt + AHEAD, (kt + AHEAD) % kStages);
+    if (p.debug & 1) continue;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       if constexpr (AMODE == kConvRelu) {
@@ -512,6 +514,9 @@ int launch(const GemmP& p, hipStream_t st) {
 
 }  // namespace
 
+static int g_gemm_debug = 0;
+extern "C" void s3n_gemm_set_debug(int flags) { g_gemm_debug = flags; }
+
 extern "C" size_t s3n_gemm_workspace_bytes(const s3n_gemm_args* a) {
   if (!a || a->split_k <= 1) return 0;
   return sizeof(float) * (size_t)a->groups * a->split_k * (size_t)a->M * a->N;
@@ -566,6 +571,7 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
       S3_REQUIRE(a->rope_pos[g], "s3n_gemm: RoPE positions missing for group %d", g);
   }
   p.ws = static_cast<float*>(a->workspace);
+  p.debug = g_gemm_debug;
   if (p.split_k > 1)
     S3_REQUIRE(p.ws, "s3n_gemm: split_k > 1 needs a workspace (s3n_gemm_workspace_bytes)");
   hipStream_t st = s3::as_stream(stream);

@@ -1,0 +1,37 @@
+"""Where does a GEMM launch's time go?  Each tile config timed in full, with
+the MFMAs skipped (operand DMA + barriers + LDS reads) and with the DMA
+skipped (LDS reads + MFMAs on stale LDS), HIP-graph replays (tuning only).
+
+  python -m splatt3r_amd.bench_gemm_parts
+"""
+from __future__ import annotations
+
+import torch
+
+from splatt3r_amd import _lib, ops
+from splatt3r_amd.bench_gemm import timeit
+
+SHAPES = [(768, 1024, 1024), (768, 4096, 1024), (768, 1024, 4096), (4096, 4096, 4096),
+          (1536, 6400, 7168)]
+
+
+def main():
+    L = _lib.lib()
+    for M, N, K in SHAPES:
+        A = torch.randn(M, K, device="cuda").half()
+        B = torch.randn(N, K, device="cuda").half() * K ** -0.5
+        C = torch.empty(M, N, device="cuda", dtype=torch.float16)
+        fl = 2 * M * N * K
+        for tile in (1, 6, 2, 3, 4, 5):
+            c = ops.gemm([A], [B], [C], M, N, K, lda=K, split_k=1, tile=tile)
+            r = []
+            for dbg in (0, 1, 2, 3):
+                L.s3n_gemm_set_debug(dbg)
+                r.append(timeit(lambda: c(_lib.stream()), reps=10))
+            L.s3n_gemm_set_debug(0)
+            print(f"{M}x{N}x{K} t{tile}: full {r[0]:7.1f} us ({fl / r[0] / 1e6:5.0f} TF)  "
+                  f"no-mfma {r[1]:7.1f}  no-dma {r[2]:7.1f}  neither {r[3]:7.1f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -60,6 +60,7 @@ _PP = ctypes.POINTER(P)
 _lib.register({
     "s3n_gemm": (ctypes.c_int, [_GP, P]),
     "s3n_gemm_workspace_bytes": (ctypes.c_size_t, [_GP]),
+    "s3n_gemm_set_debug": (None, [ctypes.c_int]),
     "s3n_attention": (ctypes.c_int, [_AP, P]),
     "s3n_layernorm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _PP, I64, _PP, _PP,
                                      ctypes.c_float, _PP, I64, _PP, I64, P]),
@@ -134,6 +135,112 @@ def auto_split_k(M, N, K, groups) -> int:
     return max(1, min(kt // 4, -(-256 // tiles64)))
 
 
+# Per-shape launch configuration measured on the device (S3_GEMM_TUNE=0
+# falls back to the static policy).  Candidates are timed on scratch
+# operands of the call's exact shape, layout and epilogue (the weights and
+# tables are the real ones; they are only read), so tuning never touches
+# plan buffers.  The choice is cached per process and shape.
+TUNE = os.environ.get("S3_GEMM_TUNE", "1") != "0"
+_TUNE_CACHE: dict = {}
+TUNE_LOG = os.environ.get("S3_GEMM_TUNE_LOG", "0") == "1"
+_TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128, 128),
+                6: (64, 64), 8: (64, 128)}
+
+
+def _tune_key(a):
+    f = ("M", "N", "K", "groups", "lda", "ldb", "ldc", "act", "r1_f16", "r2_f16", "c_f16",
+         "ldr1", "ldr2", "ldc2", "store_mode", "sS", "sCout", "a_mode", "cH", "cW", "cC", "ksize",
+         "stride", "pad", "oH", "oW", "relu_in", "rope_ncols")
+    return tuple(getattr(a, k) for k in f) + (bool(a.R1[0]), bool(a.R2[0]), bool(a.C2[0]),
+                                               bool(a.bias[0]))
+
+
+def _tune_candidates(a, split_ok):
+    kt = -(-a.K // 64)
+    out = []
+    for tile, (bm, bn) in _TILE_SHAPES.items():
+        tiles = a.groups * -(-a.M // bm) * -(-a.N // bn)
+        for sk in (1, 2, 3, 4, 6, 8):
+            if sk > 1 and (not split_ok or kt // sk < 4 or tiles * sk > 4096):
+                continue
+            out.append((tile, sk))
+    return out
+
+
+def _tuned(a, A, B, bias, rope, rope_pos, split_ok):
+    key = _tune_key(a)
+    if key in _TUNE_CACHE:
+        return _TUNE_CACHE[key]
+    dev = next(t.device for t in (*A, *B) if isinstance(t, torch.Tensor))
+    g = a.groups
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0)
+
+    def scratch(n, dt):
+        t = torch.empty(int(n), device=dev, dtype=dt)
+        if dt == torch.float16 or dt == torch.float32:
+            t.normal_(0.0, 0.1, generator=gen)
+        return t
+
+    if a.a_mode == 0:
+        a_elems = (a.M - 1) * a.lda + a.K
+    else:
+        a_elems = a.M // (a.oH * a.oW) * a.cH * a.cW * a.cC
+    if a.store_mode == 0:
+        c_elems = (a.M - 1) * a.ldc + a.N
+    else:
+        c_elems = a.M * a.sS * a.sS * a.sCout
+    t = GemmArgs.from_buffer_copy(a)
+    keep = []
+    for i in range(g):
+        sa = scratch(a_elems, torch.float16)
+        sc = scratch(c_elems, torch.float16 if a.c_f16 else torch.float32)
+        keep += [sa, sc]
+        t.A[i], t.C[i] = sa.data_ptr(), sc.data_ptr()
+        if a.R1[i]:
+            r = scratch((a.M - 1) * a.ldr1 + a.N, torch.float16 if a.r1_f16 else torch.float32)
+            keep.append(r)
+            t.R1[i] = r.data_ptr()
+        if a.R2[i]:
+            r = scratch((a.M - 1) * a.ldr2 + a.N, torch.float16 if a.r2_f16 else torch.float32)
+            keep.append(r)
+            t.R2[i] = r.data_ptr()
+        if a.C2[i]:
+            r = scratch((a.M - 1) * a.ldc2 + a.N, torch.float16)
+            keep.append(r)
+            t.C2[i] = r.data_ptr()
+    L = _lib.lib()
+    st = _lib.stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    best, best_ms = (a.tile, a.split_k), None
+    for tile, sk in _tune_candidates(a, split_ok):
+        t.tile, t.split_k = tile, sk
+        ws = None
+        if sk > 1:
+            ws = torch.empty(L.s3n_gemm_workspace_bytes(ctypes.byref(t)) // 4 + 1,
+                             dtype=torch.float32, device=dev)
+            t.workspace = ws.data_ptr()
+        ref = ctypes.byref(t)
+        if L.s3n_gemm(ref, st) != 0:
+            continue
+        torch.cuda._sleep(2_000_000)         # queue the timed launches behind a GPU sleep
+        ev[0].record()
+        for _ in range(6):
+            L.s3n_gemm(ref, st)
+        ev[1].record()
+        ev[1].synchronize()
+        ms = ev[0].elapsed_time(ev[1])
+        if best_ms is None or ms < best_ms:
+            best, best_ms = (tile, sk), ms
+        del ws
+    _TUNE_CACHE[key] = best
+    if TUNE_LOG:
+        print(f"[gemm-tune] {a.M}x{a.N}x{a.K} g{a.groups} mode{a.a_mode} st{a.store_mode} "
+              f"-> tile {best[0]} split {best[1]} ({best_ms / 6 * 1e3:.1f} us; static "
+              f"tile {a.tile} split {a.split_k})", flush=True)
+    return best
+
+
 def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1=None,
          ldr1=0, R2=None, ldr2=0, C2=None, ldc2=0, conv=None, store=None, split_k=None,
          tile=0, rope=None, rope_pos=None, rope_ncols=0) -> Call:
@@ -186,6 +293,9 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         split_k = 1
     a.split_k = int(auto_split_k(M, N, K, groups) if split_k is None else split_k)
     a.tile = int(tile) or TILE_OVERRIDE
+    if TUNE and not tile and not TILE_OVERRIDE and torch.cuda.is_available():
+        a.tile, a.split_k = _tuned(a, A, B, bias, rope, rope_pos,
+                                   split_ok=split_k is None and rope_pos is None)
     ws = None
     if a.split_k > 1:
         nbytes = _lib.lib().s3n_gemm_workspace_bytes(ctypes.byref(a))
