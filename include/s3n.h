@@ -97,8 +97,10 @@ size_t s3n_gemm_workspace_bytes(const s3n_gemm_args* args);
 int s3n_gemm(const s3n_gemm_args* args, void* stream);
 
 /* Tuning hook (not on the product path): flags applied to later s3n_gemm
- * launches; 1 = skip the MFMAs, 2 = skip the operand DMA (results are then
- * garbage).  0 restores normal operation. */
+ * launches; 1 = skip the MFMAs, 2 = skip the operand DMA, 4 = skip the
+ * epilogue, 8 = skip the K loop (results are then garbage), 16 = force the
+ * per-register epilogue instead of the LDS-staged vector one (results
+ * valid).  0 restores normal operation. */
 void s3n_gemm_set_debug(int flags);
 
 /* Fused multi-head attention softmax(Q K^T * scale) V with 2-D RoPE

@@ -18,7 +18,6 @@ typedef _Float16 f16;
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 64;
 constexpr int kThreads = 256;
 
 struct GemmP {
@@ -46,6 +45,7 @@ struct GemmP {
   int split_k, kt_per_split;
   float* ws;
   int debug;       // s3n_gemm_set_debug flags (tuning only)
+  int vec_epi;     // LDS-staged epilogue with 8-column vector accesses (host-checked)
   int col_major;   // tile order: 1 = M fastest (each XCD owns a band of N)
   const float* rope_cos;
   const float* rope_sin;
@@ -53,7 +53,14 @@ struct GemmP {
   const int64_t* rope_pos[S3N_MAX_GROUPS];
 };
 
-__device__ __forceinline__ int swz(int row, int kc) { return (kc ^ ((row >> 1) & 7)); }
+// XOR swizzle of the 16-B chunks of one LDS tile row (BK fp16 = 128 or
+// 256 B): every 16-lane group of a ds_read_b128 fragment read (rows of one
+// 32-row block at one logical chunk) then hits 16 distinct 16-B bank slots.
+template <int BK>
+__device__ __forceinline__ int swz(int row, int kc) {
+  if constexpr (BK == 64) return kc ^ ((row >> 1) & 7);   // 2 rows per 256-B bank row
+  else return kc ^ (row & 15);                            // 1 row per 256-B bank row
+}
 
 __device__ __forceinline__ float gelu(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
@@ -104,9 +111,7 @@ __device__ __forceinline__ void wait_tiles(int after) {
 
 // Store of one finished element (plain / ConvT / pixel-shuffle scatter) and
 // its optional fp16 copy.
-__device__ __forceinline__ void store_out(const GemmP& p, int g, int row, int col, float v) {
-  void* C = p.C[g];
-  f16* C2 = p.C2[g];
+__device__ __forceinline__ int64_t out_offset(const GemmP& p, int row, int col) {
   int64_t off;
   if (p.store_mode == S3N_STORE_PLAIN) {
     off = (int64_t)row * p.ldc + col;
@@ -128,6 +133,13 @@ __device__ __forceinline__ void store_out(const GemmP& p, int g, int row, int co
     const int64_t oy = (int64_t)ty * p.sS + i, ox = (int64_t)tx * p.sS + j;
     off = (((int64_t)b * p.sH * p.sS + oy) * ((int64_t)p.sW * p.sS) + ox) * p.sCout + co;
   }
+  return off;
+}
+
+__device__ __forceinline__ void store_out(const GemmP& p, int g, int row, int col, float v) {
+  void* C = p.C[g];
+  f16* C2 = p.C2[g];
+  const int64_t off = out_offset(p, row, col);
   if (p.c_f16) reinterpret_cast<f16*>(C)[off] = (f16)v;
   else reinterpret_cast<float*>(C)[off] = v;
   if (C2) C2[(int64_t)row * p.ldc2 + col] = (f16)v;
@@ -217,24 +229,174 @@ __device__ __forceinline__ void epilogue_block(const GemmP& p, int g, int row0, 
 
 // NWM x NWN waves, each owning a (BM/NWM) x (BN/NWN) block of 32x32
 // accumulators.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void load8(const float* q, float (&v)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(q);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(q + 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = b[e]; }
+}
+
+__device__ __forceinline__ void load8_res(const void* R, int f16in, int64_t o, float (&v)[8]) {
+  if (f16in) {
+    const f16x8 h = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(R) + o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)h[e];
+  } else {
+    load8(reinterpret_cast<const float*>(R) + o, v);
+  }
+}
+
+__device__ __forceinline__ void store8_f32(float* q, const float (&v)[8]) {
+  *reinterpret_cast<f32x4*>(q) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(q + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
+__device__ __forceinline__ void store8_f16(f16* q, const float (&v)[8]) {
+  f16x8 h;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) h[e] = (f16)v[e];
+  *reinterpret_cast<f16x8*>(q) = h;
+}
+
+// The accumulator tile goes through LDS (row-major fp32, the staging ring
+// is free once the K loop is done) and comes back as 8-column row chunks,
+// so that bias / residual / RoPE-table loads and the stores are 16/32-B
+// vector accesses along rows (fully coalesced) instead of one 2-4 B access
+// per accumulator register.  The host enables it when every row stride and
+// base is 16-B aligned and 8-column chunks stay contiguous in the output.
+template <int BM, int BN, int NWM, int NWN, int FM, int FN, int LDT>
+__device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int n0,
+                                             f32x16 (&acc)[FM][FN], float* stage) {
+  constexpr int WM = BM / NWM, WN = BN / NWN, NT = 64 * NWM * NWN;
+  constexpr int CPR = BN / 8;                 // 8-column chunks per tile row
+  constexpr int NCH = BM * CPR / NT;          // chunks per thread
+  static_assert(NCH * NT == BM * CPR, "chunks must split over the threads");
+  // small tiles: the chunk operands (bias, fp32 residual, RoPE position) are
+  // loaded before the LDS staging so their latency overlaps it
+  constexpr bool kPre = NCH <= 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / NWN, wn = wave % NWN;
+  const float* __restrict__ bias = p.bias[g];
+  const void* R1 = p.R1[g];
+  const void* R2 = p.R2[g];
+  const int64_t* __restrict__ pos = p.rope_pos[g];
+  f16* C2 = p.C2[g];
+  const bool split = p.split_k > 1;
+  float pb[kPre ? NCH : 1][8], pr[kPre ? NCH : 1][8];
+  int64_t pps[kPre ? NCH : 1];
+  if constexpr (kPre) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = tid + k * NT, rl = c / CPR, cl = (c % CPR) * 8;
+      const int row = min(m0 + rl, p.M - 1), col = min(n0 + cl, p.N - 8);
+      if (bias && !split) load8(bias + col, pb[k]);
+      if (R1 && !split) load8_res(R1, p.r1_f16, (int64_t)row * p.ldr1 + col, pr[k]);
+      pps[k] = (pos && col < p.rope_ncols) ? pos[(int64_t)row * 2 + ((col & 63) >> 5)] : 0;
+    }
+  }
+  __syncthreads();   // every wave is done with the K loop's LDS reads
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        stage[(wm * WM + fm * 32 + acc_row(r) + 4 * (lane >> 5)) * LDT + wn * WN + fn * 32 +
+              (lane & 31)] = acc[fm][fn][r];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = tid + k * NT;
+    const int rl = c / CPR, cl = (c % CPR) * 8;
+    const int row = m0 + rl, col = n0 + cl;
+    if (row >= p.M || col >= p.N) continue;
+    float v[8];
+    load8(stage + rl * LDT + cl, v);
+    if (split) {
+      store8_f32(p.ws + (((int64_t)g * p.split_k + blockIdx.y) * p.M + row) * p.N + col, v);
+      continue;
+    }
+    if (bias) {
+      float bl[8];
+      if constexpr (kPre) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bl[e] = pb[k][e];
+      } else {
+        load8(bias + col, bl);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bl[e];
+    }
+    if (pos && col < p.rope_ncols) {
+      // partner columns col ^ 16 of the same 64-wide head: same row of the tile
+      float xp[8], bp[8], cs[8], sn[8];
+      load8(stage + rl * LDT + (cl ^ 16), xp);
+      if (bias) {
+        load8(bias + (col ^ 16), bp);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xp[e] += bp[e];
+      }
+      int64_t ps;
+      if constexpr (kPre) ps = pps[k];
+      else ps = pos[(int64_t)row * 2 + ((col & 63) >> 5)];
+      load8(p.rope_cos + ps * 16 + (col & 15), cs);
+      load8(p.rope_sin + ps * 16 + (col & 15), sn);
+      const bool lo = (col & 31) < 16;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = lo ? v[e] * cs[e] - xp[e] * sn[e] : v[e] * cs[e] + xp[e] * sn[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = act_fn(p, v[e]);
+    if (R1) {
+      float t[8];
+      if constexpr (kPre) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = pr[k][e];
+      } else {
+        load8_res(R1, p.r1_f16, (int64_t)row * p.ldr1 + col, t);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    if (R2) {
+      float t[8];
+      load8_res(R2, p.r2_f16, (int64_t)row * p.ldr2 + col, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    const int64_t off = out_offset(p, row, col);
+    if (p.c_f16) store8_f16(reinterpret_cast<f16*>(p.C[g]) + off, v);
+    else store8_f32(reinterpret_cast<float*>(p.C[g]) + off, v);
+    if (C2) store8_f16(C2 + (int64_t)row * p.ldc2 + col, v);
+  }
+}
+
 // Waves per SIMD the LDS footprint allows (the register budget the
 // compiler may use without costing occupancy).
-constexpr int lds_waves_per_simd(int BM, int BN, int NW, int S) {
-  const int wg = (160 * 1024) / (S * (BM + BN) * 64 * 2);
+constexpr int lds_waves_per_simd(int BM, int BN, int NW, int S, int BK) {
+  const int wg = (160 * 1024) / (S * (BM + BN) * BK * 2);
   const int w = (wg > 8 ? 8 : wg) * NW / 4;
   return w < 1 ? 1 : (w > 8 ? 8 : w);
 }
 
-template <int BM, int BN, int NWM, int NWN, int AMODE, int kStages>
-__global__ void __launch_bounds__(64 * NWM * NWN, lds_waves_per_simd(BM, BN, NWM * NWN, kStages))
+template <int BM, int BN, int NWM, int NWN, int AMODE, int kStages, int BK>
+__global__ void __launch_bounds__(64 * NWM * NWN,
+                                  lds_waves_per_simd(BM, BN, NWM * NWN, kStages, BK))
 k_gemm(GemmP p) {
   constexpr int NW = NWM * NWN;
   constexpr int WM = BM / NWM, WN = BN / NWN;
   constexpr int FM = WM / 32, FN = WN / 32;
-  // One LDS-DMA wave instruction moves 64 lanes x 16 B = 8 rows of the
-  // 128-B (BK = 64 fp16) tile rows.  Each wave issues AW + BW per K tile.
-  constexpr int AW = BM / 8 / NW, BW = BN / 8 / NW;
-  static_assert(AW * 8 * NW == BM && BW * 8 * NW == BN, "LDS-DMA rows must split over waves");
+  // One LDS-DMA wave instruction moves 64 lanes x 16 B = RPI tile rows of
+  // BK fp16.  Each wave issues AW + BW per K tile.
+  static_assert(BK == 64 || BK == 128, "K tile");
+  constexpr int CPR = BK / 8;          // 16-B chunks per tile row
+  constexpr int RPI = 64 / CPR;        // rows per DMA instruction
+  constexpr int AW = BM / RPI / NW, BW = BN / RPI / NW;
+  static_assert(AW * RPI * NW == BM && BW * RPI * NW == BN, "LDS-DMA rows must split over waves");
   static_assert(WM % 32 == 0 && WN % 32 == 0, "32x32 accumulator blocks");
   constexpr int PERW = AW + BW;
   constexpr int STAGE = (BM + BN) * BK;
@@ -261,7 +423,7 @@ k_gemm(GemmP p) {
   // Lane -> (row within its 8-row group, LDS chunk); the global k chunk is
   // pre-swizzled so the LDS image is the XOR-swizzled layout the fragment
   // reads expect (swz is an involution).
-  const int lrow = lane >> 3, lchunk = lane & 7;
+  const int lrow = lane / CPR, lchunk = lane % CPR;
   uint32_t a_off[AW];   // dense: byte offset of the lane's row chunk at k = 0
   int64_t a_img[AW];    // conv: element offset of the lane's image
   int a_iy0[AW], a_ix0[AW];
@@ -272,8 +434,8 @@ k_gemm(GemmP p) {
   int c_ci[AW], c_ky[AW], c_kx[AW];
 #pragma unroll
   for (int j = 0; j < AW; ++j) {
-    const int r = (wave * AW + j) * 8 + lrow;
-    a_kc[j] = swz(r, lchunk);
+    const int r = (wave * AW + j) * RPI + lrow;
+    a_kc[j] = swz<BK>(r, lchunk);
     const int m = m0 + r;
     a_ok[j] = m < M;
     const int mm = a_ok[j] ? m : 0;
@@ -298,8 +460,8 @@ k_gemm(GemmP p) {
   int b_kc[BW];
 #pragma unroll
   for (int j = 0; j < BW; ++j) {
-    const int r = (wave * BW + j) * 8 + lrow;
-    b_kc[j] = swz(r, lchunk);
+    const int r = (wave * BW + j) * RPI + lrow;
+    b_kc[j] = swz<BK>(r, lchunk);
     b_ok[j] = (n0 + r) < N;
     b_off[j] = b_ok[j] ? (uint32_t)(((int64_t)(n0 + r) * p.ldb + b_kc[j] * 8) * 2) : kOOB;
   }
@@ -359,7 +521,7 @@ k_gemm(GemmP p) {
   // kStages-deep ring: tiles kt+1 .. kt+kStages-2 stay in flight while
   // tile kt is consumed; one raw barrier per K tile.
   constexpr int AHEAD = kStages - 1;
-  const int KT = kt_end - kt_begin;   // this workgroup's K tiles
+  const int KT = (p.debug & 8) ? 0 : kt_end - kt_begin;   // this workgroup's K tiles
 #pragma unroll
   for (int i = 0; i < AHEAD; ++i)
     if (i < KT) issue(kt_begin + i, i);
@@ -381,12 +543,12 @@ k_gemm(GemmP p) {
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm) {
         const int row = wm * WM + fm * 32 + (lane & 31);
-        af[ks][fm] = *reinterpret_cast<const f16x8*>(As + row * BK + swz(row, kc) * 8);
+        af[ks][fm] = *reinterpret_cast<const f16x8*>(As + row * BK + swz<BK>(row, kc) * 8);
       }
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const int row = wn * WN + fn * 32 + (lane & 31);
-        bf[ks][fn] = *reinterpret_cast<const f16x8*>(Bs + row * BK + swz(row, kc) * 8);
+        bf[ks][fn] = *reinterpret_cast<const f16x8*>(Bs + row * BK + swz<BK>(row, kc) * 8);
       }
     }
     if (kt + AHEAD < KT) issue(kt_begin + kt + AHEAD, (kt + AHEAD) % kStages);
@@ -409,6 +571,14 @@ k_gemm(GemmP p) {
   }
 
   // ---- epilogue ----
+  if (p.debug & 4) return;
+  if (p.vec_epi) {
+    // row pitch BN + 4 floats where it fits (rows 16 B apart in the banks)
+    constexpr int LDT = BM * (BN + 4) * 4 <= kStages * STAGE * 2 ? BN + 4 : BN;
+    static_assert(BM * LDT * 4 <= kStages * STAGE * 2, "epilogue staging must fit the ring");
+    epilogue_vec<BM, BN, NWM, NWN, FM, FN, LDT>(p, g, m0, n0, acc, reinterpret_cast<float*>(smem));
+    return;
+  }
   const int s_idx = blockIdx.y;
   if (p.rope_pos[g]) {
     // bias, then RoPE: the partner column (col ^ 16, same rows) sits in lane
@@ -483,7 +653,7 @@ __global__ void __launch_bounds__(kThreads) k_splitk_reduce(GemmP p) {
   epilogue(p, g, (int)(i / p.N), (int)(i % p.N), v);
 }
 
-template <int BM, int BN, int S, int NWM = 2, int NWN = 2>
+template <int BM, int BN, int S, int NWM = 2, int NWN = 2, int BK = 64>
 int launch(const GemmP& p, hipStream_t st) {
   constexpr int NT = 64 * NWM * NWN;
   GemmP q = p;
@@ -498,11 +668,11 @@ int launch(const GemmP& p, hipStream_t st) {
   q.col_major = (int64_t)p.N * p.K > a_bytes;
   dim3 grid(q.tiles_m * q.tiles_n, q.split_k, p.groups);
   if (p.a_mode == S3N_A_DENSE)
-    k_gemm<BM, BN, NWM, NWN, kDense, S><<<grid, NT, 0, st>>>(q);
+    k_gemm<BM, BN, NWM, NWN, kDense, S, BK><<<grid, NT, 0, st>>>(q);
   else if (p.relu_in)
-    k_gemm<BM, BN, NWM, NWN, kConvRelu, S><<<grid, NT, 0, st>>>(q);
+    k_gemm<BM, BN, NWM, NWN, kConvRelu, S, BK><<<grid, NT, 0, st>>>(q);
   else
-    k_gemm<BM, BN, NWM, NWN, kConv, S><<<grid, NT, 0, st>>>(q);
+    k_gemm<BM, BN, NWM, NWN, kConv, S, BK><<<grid, NT, 0, st>>>(q);
   S3_LAUNCH_CHECK();
   if (q.split_k > 1) {
     dim3 rg((unsigned)s3::cdiv((int64_t)p.M * p.N, kThreads), p.groups);
@@ -572,6 +742,23 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   }
   p.ws = static_cast<float*>(a->workspace);
   p.debug = g_gemm_debug;
+  // 8-column vector epilogue: every row stride a multiple of 8 elements,
+  // every base 16-B aligned, chunks contiguous in the output layout
+  {
+    auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    bool v = a->N % 8 == 0 && !(g_gemm_debug & 16);
+    if (a->store_mode == S3N_STORE_PLAIN) v = v && a->ldc % 8 == 0;
+    else if (a->store_mode == S3N_STORE_CONVT) v = v && a->sCout % 8 == 0;
+    else v = false;
+    for (int g = 0; g < a->groups && v; ++g) {
+      v = al(a->C[g]) && (!a->bias[g] || al(a->bias[g])) &&
+          (!a->R1[g] || (al(a->R1[g]) && a->ldr1 % 8 == 0)) &&
+          (!a->R2[g] || (al(a->R2[g]) && a->ldr2 % 8 == 0)) &&
+          (!a->C2[g] || (al(a->C2[g]) && a->ldc2 % 8 == 0));
+    }
+    if (any_rope) v = v && al(a->rope_cos) && al(a->rope_sin);
+    p.vec_epi = v ? 1 : 0;
+  }
   if (p.split_k > 1)
     S3_REQUIRE(p.ws, "s3n_gemm: split_k > 1 needs a workspace (s3n_gemm_workspace_bytes)");
   hipStream_t st = s3::as_stream(stream);
@@ -583,6 +770,11 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   if (a->tile == 6) return launch<64, 64, 4>(p, st);
   if (a->tile == 7) return launch<64, 64, 5>(p, st);
   if (a->tile == 8) return launch<64, 128, 4>(p, st);
+  // K tile 128: half the K iterations (and barriers) per output tile
+  if (a->tile == 9) return launch<64, 64, 3, 2, 2, 128>(p, st);
+  if (a->tile == 10) return launch<64, 64, 2, 2, 2, 128>(p, st);
+  if (a->tile == 11) return launch<64, 128, 2, 2, 2, 128>(p, st);
+  if (a->tile == 12) return launch<128, 128, 2, 2, 2, 128>(p, st);
   // Tile choice: fill the 256 CUs before growing the tile.
   auto tiles = [&](int bm, int bn) {
     return (int64_t)a->groups * ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);

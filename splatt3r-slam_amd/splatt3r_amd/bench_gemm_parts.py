@@ -11,8 +11,7 @@ import torch
 from splatt3r_amd import _lib, ops
 from splatt3r_amd.bench_gemm import timeit
 
-SHAPES = [(768, 1024, 1024), (768, 4096, 1024), (768, 1024, 4096), (4096, 4096, 4096),
-          (1536, 6400, 7168)]
+SHAPES = [(768, 1024, 1024), (768, 4096, 1024), (768, 1024, 4096)]
 
 
 def main():
@@ -22,15 +21,16 @@ def main():
         B = torch.randn(N, K, device="cuda").half() * K ** -0.5
         C = torch.empty(M, N, device="cuda", dtype=torch.float16)
         fl = 2 * M * N * K
-        for tile in (1, 6, 2, 3, 4, 5):
+        for tile in (1, 10, 2, 3):
             c = ops.gemm([A], [B], [C], M, N, K, lda=K, split_k=1, tile=tile)
             r = []
-            for dbg in (0, 1, 2, 3):
+            for dbg in (0, 1, 2, 3, 8, 12):
                 L.s3n_gemm_set_debug(dbg)
                 r.append(timeit(lambda: c(_lib.stream()), reps=10))
             L.s3n_gemm_set_debug(0)
             print(f"{M}x{N}x{K} t{tile}: full {r[0]:7.1f} us ({fl / r[0] / 1e6:5.0f} TF)  "
-                  f"no-mfma {r[1]:7.1f}  no-dma {r[2]:7.1f}  neither {r[3]:7.1f}", flush=True)
+                  f"no-mfma {r[1]:7.1f}  no-dma {r[2]:7.1f}  neither {r[3]:7.1f}  "
+                  f"no-loop {r[4]:6.1f}  no-loop-no-epi {r[5]:6.1f}", flush=True)
 
 
 if __name__ == "__main__":

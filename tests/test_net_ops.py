@@ -41,7 +41,9 @@ def test_gemm_dense_bias_residual(M, N, K, groups):
     (768, 1024, 4096, 1, 3, 0), (768, 768, 768, 2, 2, 1), (200, 96, 200, 2, 5, 0),
     (130, 300, 1000, 1, 7, 2), (300, 256, 2304, 4, 4, 3), (768, 1024, 1024, 1, 1, 3),
     (700, 200, 960, 2, 1, 4), (520, 384, 640, 1, 2, 5), (768, 6400, 512, 2, 1, 4),
-    (300, 200, 1000, 1, 1, 6), (130, 96, 2000, 2, 1, 7), (600, 256, 200, 1, 1, 8)])
+    (300, 200, 1000, 1, 1, 6), (130, 96, 2000, 2, 1, 7), (600, 256, 200, 1, 1, 8),
+    (768, 1024, 1000, 1, 1, 9), (300, 200, 1000, 2, 3, 10), (130, 300, 968, 1, 2, 11),
+    (700, 256, 2304, 2, 1, 12), (64, 64, 136, 1, 1, 9)])
 def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
     """Split-K partials + ordered reduce + the full epilogue (bias, GELU,
     fp32 residual, fp16 out + fp16 copy) for every tile shape."""
@@ -60,10 +62,12 @@ def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
         assert torch.equal(C[g], C2[g])
 
 
-@pytest.mark.parametrize("split,tile", [(3, 1), (9, 0), (2, 3), (1, 4), (1, 5)])
-def test_gemm_implicit_conv_split_k(split, tile):
+@pytest.mark.parametrize("split,tile,Cin", [(3, 1, 768), (9, 0, 768), (2, 3, 768), (1, 4, 768),
+                                            (1, 5, 768), (1, 9, 768), (2, 10, 768), (1, 11, 96),
+                                            (1, 12, 768), (1, 9, 96), (2, 9, 136)])
+def test_gemm_implicit_conv_split_k(split, tile, Cin):
     from splatt3r_amd import ops, _lib
-    B, H, W, Cin, Cout, k, stride, pad = 1, 12, 16, 768, 256, 3, 1, 1
+    B, H, W, Cout, k, stride, pad = 1, 12, 16, 256, 3, 1, 1
     x = _rand(B, H, W, Cin, seed=13)
     w = _rand(Cout, Cin, k, k, scale=(Cin * k * k) ** -0.5, seed=14)
     out = torch.empty(B, H, W, Cout, device="cuda")
@@ -327,3 +331,59 @@ def test_gaussian_postprocess_vs_torch():
                opacities=gs[:, 13].sigmoid(), means=p3 + offs)
     for k, v in ref.items():
         assert rel_err(out[k], v) < 1e-5, k
+
+
+@pytest.mark.parametrize("case", ["plain", "res16", "split", "rope", "convt", "tile3", "tile4"])
+def test_gemm_vector_epilogue_matches_register_epilogue(case):
+    """The LDS-staged 8-column epilogue and the per-register epilogue
+    (s3n_gemm_set_debug(16)) apply the same operations in the same order:
+    bit-identical outputs."""
+    from splatt3r_amd import ops, _lib
+    from splatt3r_amd.net import positions, rope_tables
+    M, N, K, g = 300, 384, 320, 2
+    A = [_rand(M, K, seed=40 + i) for i in range(g)]
+    W = [_rand(N, K, scale=K ** -0.5, seed=50 + i) for i in range(g)]
+    b = [_rand(N, dtype=torch.float32, seed=60 + i) for i in range(g)]
+    kw = dict(lda=K, bias=b, act="gelu")
+    out_dt = torch.float32
+    if case == "res16":
+        kw.update(R1=[_rand(M, N, dtype=torch.float32, seed=70 + i) for i in range(g)], ldr1=N,
+                  R2=[_rand(M, N, seed=80 + i) for i in range(g)], ldr2=N, act="none")
+        out_dt = torch.float16
+    if case == "split":
+        kw.update(split_k=3, R1=[_rand(M, N, dtype=torch.float32, seed=70 + i) for i in range(g)],
+                  ldr1=N)
+    if case == "rope":
+        cos, sin = rope_tables(64, "cuda")
+        pos = [positions(3, 10, 10, "cuda").reshape(-1, 2) for _ in range(g)]
+        kw.update(rope=(cos, sin), rope_pos=pos, rope_ncols=256, act="none")
+        out_dt = torch.float16
+    if case == "tile3":
+        kw.update(tile=3, split_k=1)
+    if case == "tile4":
+        kw.update(tile=4, split_k=1)
+    if case == "convt":
+        s, cout = 2, 96                                  # N = s*s*cout = 384
+        kw.update(store=("convt", 15, 20, s, cout), act="none")
+        C = [torch.empty(1, 30, 40, cout, device="cuda", dtype=out_dt) for _ in range(g)]
+    else:
+        C = [torch.empty(M, N, device="cuda", dtype=out_dt) for _ in range(g)]
+    C2 = [torch.empty(M, N, device="cuda", dtype=torch.float16) for _ in range(g)]
+    if case != "convt":
+        kw.update(C2=C2, ldc2=N)
+    L = _lib.lib()
+    outs = []
+    for dbg in (16, 0):
+        for c in C:
+            c.fill_(0)
+        L.s3n_gemm_set_debug(dbg)
+        try:
+            ops.gemm(A, W, C, M, N, K, **kw)(_lib.stream())
+        finally:
+            L.s3n_gemm_set_debug(0)
+        outs.append([c.clone() for c in C] + ([c.clone() for c in C2] if case != "convt" else []))
+    for x, y in zip(*outs):
+        if case == "rope":   # the two paths may contract x*cos -/+ x'*sin differently
+            assert rel_err(y, x.float()) < 2e-3
+        else:
+            assert torch.equal(x, y)
