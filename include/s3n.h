@@ -127,6 +127,11 @@ typedef struct {
 
 int s3n_attention(const s3n_attn_args* args, void* stream);
 
+/* Tuning hook (not on the product path), kernels for pre-rotated q/k:
+ * 0 = transposed-score kernel with 2 key groups (default), 1 = the
+ * P-through-LDS kernel, 2 = transposed-score with 1 key group, 3 = with 4. */
+void s3n_attention_set_variant(int variant);
+
 /* LayerNorm over the last dim C (eps), per group gamma/beta:
  * y = (x - mean) * rsqrt(var + eps) * gamma + beta.  x fp32 [rows, ldx];
  * out16 (fp16, ld16) and/or out32 (fp32, ld32) may be NULL. */

@@ -440,7 +440,215 @@ __global__ void __launch_bounds__(kThreads) k_attn_dma(AttnP p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Transposed-score variant of k_attn_dma: S^T = K Q^T (the same two MFMA
+// operands in swapped order), so every lane owns ONE query (lane & 15) and
+// 4 keys per 16-key block.  Consequences:
+//  * the softmax max / sum over keys is in-lane (16 values per tile) plus a
+//    2-step exchange over the four 16-lane rows, instead of 4 rows x 4
+//    cross-lane steps;
+//  * P^T is already in the B-operand layout of O^T = V^T P^T: the 8 keys a
+//    lane feeds to one 16x16x32 MFMA are its own 4 + 4 scores of two
+//    adjacent key blocks (MFMA k-order is free as long as V^T uses the same
+//    permutation), so P never goes through LDS;
+//  * V^T comes from the same ds_read_b64_tr_b16 transpose reads with the key
+//    bases of that permutation, and the rescale by alpha is one factor per
+//    lane.
+__device__ __forceinline__ float xchg16(float x) { return __shfl_xor(x, 16, 64); }
+__device__ __forceinline__ float xchg32(float x) { return __shfl_xor(x, 32, 64); }
+
+// SPLIT key-range groups of 4 waves per workgroup (SPLIT x 256 threads):
+// group s streams every SPLIT-th key tile through its own LDS-DMA ring, and
+// the groups' (max, sum, O) partials are merged through LDS at the end.
+// More waves per SIMD for the same 64-query tile, half the serial tile
+// chain per wave.
+template <int SPLIT, int STAGES>
+__global__ void __launch_bounds__(kThreads * SPLIT) k_attn_st(AttnP p) {
+  constexpr int RING = STAGES * 2 * KT * D;        // fp16 elements per group
+  __shared__ __attribute__((aligned(1024))) f16 smem[SPLIT * RING];
+  const int qtile = blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / p.H, h = bh % p.H;
+  const int g = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sp = wid >> 2, wave = wid & 3;         // key group, query wave
+  const int grp = lane >> 4, li = lane & 15;
+  const f16* __restrict__ Qg = p.Q[g];
+  f16* ring = smem + sp * RING;
+
+  const int qrow = qtile * QT + wave * 16 + li;
+  const bool qok = qrow < p.Nq;
+  f16x8 qf[2];
+  {
+    const f16* qp = Qg + ((int64_t)b * p.Nq + (qok ? qrow : 0)) * p.qs + h * D;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 x = *reinterpret_cast<const f16x8*>(qp + (4 * ks + grp) * 8);
+      qf[ks] = qok ? x : f16x8{};
+    }
+  }
+
+  const __amdgpu_buffer_rsrc_t rk =
+      make_rsrc(p.K[g], (((int64_t)b + 1) * p.Nk - 1) * p.ks * 2 + (h + 1) * D * 2);
+  const __amdgpu_buffer_rsrc_t rv =
+      make_rsrc(p.V[g], (((int64_t)b + 1) * p.Nk - 1) * p.vs * 2 + (h + 1) * D * 2);
+  const int lr = lane >> 3, lc = lane & 7;
+  uint32_t k_off[2], v_off[2];
+  int k_key[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wave * 2 + j) * 8 + lr;
+    k_key[j] = row;
+    k_off[j] = (uint32_t)((((int64_t)b * p.Nk + row) * p.ks + h * D + kswz(row, lc) * 8) * 2);
+    v_off[j] = (uint32_t)((((int64_t)b * p.Nk + row) * p.vs + h * D + lc * 8) * 2);
+  }
+  const int NT = (p.Nk + KT - 1) / KT;
+  const int NTs = (NT - sp + SPLIT - 1) / SPLIT;     // this group's tiles: sp, sp+SPLIT, ...
+  const int NTmax = (NT + SPLIT - 1) / SPLIT;        // every group runs as many barriers
+  auto issue = [&](int i, int st) {
+    f16* Ks = ring + st * 2 * KT * D;
+    f16* Vs = Ks + KT * D;
+    const int key0 = (i * SPLIT + sp) * KT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = key0 + k_key[j] < p.Nk;
+      S3_BLDS(rk, Ks + (wave * 2 + j) * 512, ok ? k_off[j] : kOOB, (int64_t)key0 * p.ks * 2);
+      S3_BLDS(rv, Vs + (wave * 2 + j) * 512, ok ? v_off[j] : kOOB, (int64_t)key0 * p.vs * 2);
+    }
+  };
+
+  float m_run = -INFINITY, l_run = 0.f;   // per lane: its query, its keys
+  f32x4 o[4];                              // O^T blocks: d = 16 nb + 4 grp + r, query li
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) o[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int AHEAD = STAGES - 1;
+#pragma unroll
+  for (int i = 0; i < AHEAD; ++i)
+    if (i < NTs) issue(i, i);
+  for (int i = 0; i < NTmax; ++i) {
+    if (i < NTs) wait_tiles<4, AHEAD - 1>(NTs - 1 - i);
+    __builtin_amdgcn_s_barrier();
+    if (i >= NTs) continue;
+    if (i + AHEAD < NTs) issue(i + AHEAD, (i + AHEAD) % STAGES);
+    const int t = i * SPLIT + sp;
+    const f16* Ks = ring + (i % STAGES) * 2 * KT * D;
+    const f16* Vs = Ks + KT * D;
+    f32x4 s[4];   // S^T blocks: key 16 kb + 4 grp + r, query li
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int krow = kb * 16 + li;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = 4 * ks + grp;
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(&Ks[krow * D + kswz(krow, c) * 8]);
+        s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[ks], s[kb], 0, 0, 0);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool kok = t * KT + kb * 16 + 4 * grp + r < p.Nk;
+        s[kb][r] = kok ? s[kb][r] * p.scale_log2 : -INFINITY;
+        mx = fmaxf(mx, s[kb][r]);
+      }
+    mx = fmaxf(mx, xchg16(mx));
+    mx = fmaxf(mx, xchg32(mx));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = exp2f(s[kb][r] - m_new);
+        s[kb][r] = e;
+        ls += e;
+      }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) o[nb] *= alpha;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 pb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pb[r] = (f16)s[2 * ks][r];
+        pb[4 + r] = (f16)s[2 * ks + 1][r];
+      }
+      const int q4 = li >> 2, p4 = li & 3;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int dcol = nb * 16 + 4 * p4;
+        const int klo = ks * 32 + 4 * grp + q4, khi = klo + 16;
+        typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(&Vs[klo * D + dcol]));
+        const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(&Vs[khi * D + dcol]));
+        const f16x4 lo16 = __builtin_bit_cast(f16x4, lo);
+        const f16x4 hi16 = __builtin_bit_cast(f16x4, hi);
+        f16x8 va;
+        va[0] = lo16[0]; va[1] = lo16[1]; va[2] = lo16[2]; va[3] = lo16[3];
+        va[4] = hi16[0]; va[5] = hi16[1]; va[6] = hi16[2]; va[7] = hi16[3];
+        o[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb, o[nb], 0, 0, 0);
+      }
+    }
+  }
+  if constexpr (SPLIT > 1) {
+    // merge the key groups: groups 1.. publish (m, l, O) per lane, group 0
+    // rescales to the common max and sums
+    constexpr int REC = 18;                        // m, l, 16 O values
+    static_assert(SPLIT * 256 * REC * 4 <= SPLIT * RING * 2, "merge scratch");
+    float* xs = reinterpret_cast<float*>(smem);
+    __syncthreads();                               // all rings drained
+    if (sp > 0) {
+      float* rec = xs + (((sp - 1) * 4 + wave) * 64 + lane) * REC;
+      rec[0] = m_run;
+      rec[1] = l_run;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rec[2 + nb * 4 + r] = o[nb][r];
+    }
+    __syncthreads();
+    if (sp > 0) return;
+#pragma unroll
+    for (int s2 = 1; s2 < SPLIT; ++s2) {
+      const float* rec = xs + (((s2 - 1) * 4 + wave) * 64 + lane) * REC;
+      const float m2 = rec[0];
+      const float m = fmaxf(m_run, m2);
+      const float a1 = exp2f(m_run - m), a2 = exp2f(m2 - m);
+      l_run = l_run * a1 + rec[1] * a2;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[nb][r] = o[nb][r] * a1 + rec[2 + nb * 4 + r] * a2;
+      m_run = m;
+    }
+  }
+  float l = l_run;
+  l += xchg16(l);
+  l += xchg32(l);
+  const float inv = 1.0f / l;
+  if (!qok) return;
+  f16* op = p.O[g] + ((int64_t)b * p.Nq + qrow) * p.os + h * D;
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    f16x4 w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w[r] = (f16)(o[nb][r] * inv);
+    *reinterpret_cast<f16x4*>(op + nb * 16 + 4 * grp) = w;
+  }
+}
+
 }  // namespace
+
+static int g_attn_variant = 0;
+extern "C" void s3n_attention_set_variant(int v) { g_attn_variant = v; }
 
 extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
   S3_REQUIRE(a && a->B > 0 && a->Nq >= 0 && a->Nk > 0 && a->H > 0, "s3n_attention: bad sizes");
@@ -470,8 +678,14 @@ extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
   for (int g = 0; g < a->groups; ++g) rope = rope || p.qpos[g] || p.kpos[g];
   if (rope)
     k_attn<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
-  else
+  else if (g_attn_variant == 1)
     k_attn_dma<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+  else if (g_attn_variant == 2)
+    k_attn_st<1, kStages><<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+  else if (g_attn_variant == 3)
+    k_attn_st<4, 2><<<grid, kThreads * 4, 0, s3::as_stream(stream)>>>(p);
+  else
+    k_attn_st<2, 2><<<grid, kThreads * 2, 0, s3::as_stream(stream)>>>(p);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

@@ -61,6 +61,7 @@ _lib.register({
     "s3n_gemm": (ctypes.c_int, [_GP, P]),
     "s3n_gemm_workspace_bytes": (ctypes.c_size_t, [_GP]),
     "s3n_gemm_set_debug": (None, [ctypes.c_int]),
+    "s3n_attention_set_variant": (None, [ctypes.c_int]),
     "s3n_attention": (ctypes.c_int, [_AP, P]),
     "s3n_layernorm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _PP, I64, _PP, _PP,
                                      ctypes.c_float, _PP, I64, _PP, I64, P]),

@@ -242,8 +242,10 @@ def test_attention_rope_vs_torch(B, N, Nk, H, cross):
 @pytest.mark.parametrize("B,N,Nk,H,groups,strided", [(1, 768, 768, 16, 1, True),
                                                      (1, 768, 768, 12, 2, False),
                                                      (2, 100, 70, 4, 1, False),
-                                                     (3, 5, 130, 2, 2, True)])
-def test_attention_no_rope_dma_path(B, N, Nk, H, groups, strided):
+                                                     (3, 5, 130, 2, 2, True),
+                                                     (1, 200, 330, 3, 1, False)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_attention_no_rope_dma_path(B, N, Nk, H, groups, strided, variant):
     """The LDS-DMA ring kernel (q/k pre-rotated by the GEMM epilogue): plain
     softmax(QK^T s)V, K/V read from strided views like the fused QKV buffer."""
     from splatt3r_amd import ops, _lib
@@ -267,8 +269,12 @@ def test_attention_no_rope_dma_path(B, N, Nk, H, groups, strided):
         refs.append(r.transpose(1, 2).reshape(B * N, H * D))
     if strided:   # the sliced views must keep the fused buffer's row stride
         Qs = [t.as_strided((B * N, H * D), (qs, 1)) for t in Qs]
-    ops.attention(Qs, Ks, Vs, Os, B=B, Nq=N, Nk=Nk, H=H, q_stride=qs, k_stride=ks, v_stride=vs,
-                  o_stride=H * D, scale=D ** -0.5)(_lib.stream())
+    _lib.lib().s3n_attention_set_variant(variant)
+    try:
+        ops.attention(Qs, Ks, Vs, Os, B=B, Nq=N, Nk=Nk, H=H, q_stride=qs, k_stride=ks,
+                      v_stride=vs, o_stride=H * D, scale=D ** -0.5)(_lib.stream())
+    finally:
+        _lib.lib().s3n_attention_set_variant(0)
     for g in range(groups):
         assert rel_err(Os[g], refs[g]) < 5e-3, (g, rel_err(Os[g], refs[g]))
 
