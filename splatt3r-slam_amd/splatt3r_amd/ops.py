@@ -312,7 +312,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
                      + (f" k{conv['k']}s{conv['stride']}" if conv is not None else "")
                      + (f" {act}" if act != "none" else "") + (" R1" if R1 else "")
                      + (f" st={store[0]}" if store else "")
-                     + (f" sk{a.split_k}" if a.split_k > 1 else "")
+                     + (f" t{a.tile}" if a.tile else "") + (f" sk{a.split_k}" if a.split_k > 1 else "")
                      + (" rope" if rope_pos is not None else ""))
 
 
