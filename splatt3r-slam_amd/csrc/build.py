@@ -41,6 +41,7 @@ SOURCES = {
     "net_gemm.hip": FAST,
     "net_attn.hip": FAST,
     "net_ops.hip": STRICT,
+    "gn_backend.hip": STRICT,
 }
 
 

@@ -1,0 +1,420 @@
+// Backend pose-graph Gauss-Newton on rays (include/s3g.h), restating
+// splatt3r_slam/backend/src/gn_kernels.cu:812-1227 (ray_align_kernel +
+// gauss_newton_rays_cuda) MI355X-first:
+//  * an edge's h*w correspondences are split over many workgroups (the
+//    reference runs ONE 256-thread block per edge, i.e. a handful of CUs);
+//  * the 14-dof Jacobian of an edge is [-Jj, Jj] (ray_align_kernel sets
+//    Ji = -Jj after apply_Sim3_adj_inv), so H_e = [[A, -A], [-A, A]] and
+//    g_e = [-u, u] with A = sum w Jj^T Jj (28 upper values) and u = sum w r
+//    Jj: 35 accumulators per thread instead of 119, same products (a sign
+//    flip is exact);
+//  * slices are reduced in a fixed order in fp64, the dense 7(N - fix)
+//    system is assembled and Cholesky-solved on the device in fp64
+//    (replacing the host Eigen SimplicialLLT and the per-iteration
+//    device->host copies), then the poses are retracted; a device flag ends
+//    the queued iterations once |dx| < delta_thresh.
+#include "common.hpp"
+#include "s3g.h"
+#include "sim3_math.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int NA = 35;   // 28 (A upper, row-major) + 7 (u)
+
+__device__ __forceinline__ float huber_w(float r) {
+  const float a = fabsf(r);
+  return a < 1.345f ? 1.0f : 1.345f / a;
+}
+
+// gn_kernels.cu:251-271 relSim3: T_ij = T_i^-1 T_j
+__device__ __forceinline__ void rel_sim3(const float* Ti, const float* Tj, float* Tij) {
+  const float si_inv = 1.0f / Ti[7];
+  Tij[7] = si_inv * Tj[7];
+  float qi_inv[4];
+  s3lie::quat_inv(Ti + 3, qi_inv);
+  s3lie::quat_comp(qi_inv, Tj + 3, Tij + 3);
+  float d[3] = {Tj[0] - Ti[0], Tj[1] - Ti[1], Tj[2] - Ti[2]};
+  s3lie::act_so3(qi_inv, d, Tij);
+  Tij[0] *= si_inv; Tij[1] *= si_inv; Tij[2] *= si_inv;
+}
+
+// gn_kernels.cu:276-296 apply_Sim3_adj_inv (row vector X times Adj^-1)
+__device__ __forceinline__ void adj_inv(const float* T, const float* X, float* Y) {
+  const float s_inv = 1.0f / T[7];
+  float Ra[3];
+  s3lie::act_so3(T + 3, X, Ra);
+  Y[0] = s_inv * Ra[0];
+  Y[1] = s_inv * Ra[1];
+  Y[2] = s_inv * Ra[2];
+  s3lie::act_so3(T + 3, X + 3, Y + 3);
+  const float* t = T;
+  Y[3] += s_inv * (t[1] * Ra[2] - t[2] * Ra[1]);
+  Y[4] += s_inv * (t[2] * Ra[0] - t[0] * Ra[2]);
+  Y[5] += s_inv * (t[0] * Ra[1] - t[1] * Ra[0]);
+  Y[6] = X[6] + s_inv * (t[0] * Ra[0] + t[1] * Ra[1] + t[2] * Ra[2]);
+}
+
+struct EdgeP {
+  const float* Twc;
+  const float* Xs;
+  const float* Cs;
+  int64_t n;
+  const int32_t* ii;
+  const int32_t* jj;
+  const int64_t* idx;
+  const uint8_t* valid;
+  const float* Q;
+  float inv_sr, inv_sd, C_thresh, Q_thresh;
+  float* partial;   // [E, S, NA]
+  const double* state;
+};
+
+// grid (S, E): slice s of edge e.
+__global__ void __launch_bounds__(kThreads) k_ray_align(EdgeP p) {
+  if (p.state && p.state[0] != 0.0) return;
+  const int s = blockIdx.x, S = gridDim.x, e = blockIdx.y;
+  const int ix = p.ii[e], jx = p.jj[e];
+  float Ti[8], Tj[8], Tij[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { Ti[k] = p.Twc[ix * 8 + k]; Tj[k] = p.Twc[jx * 8 + k]; }
+  rel_sim3(Ti, Tj, Tij);
+  float acc[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) acc[k] = 0.f;
+  const int64_t n = p.n;
+  const int64_t chunk = (n + S - 1) / S;
+  const int64_t k0 = (int64_t)s * chunk, k1 = min(n, k0 + chunk);
+  const float* Xi_all = p.Xs + (int64_t)ix * n * 3;
+  const float* Xj_all = p.Xs + (int64_t)jx * n * 3;
+  const float* Ci_all = p.Cs + (int64_t)ix * n;
+  const float* Cj_all = p.Cs + (int64_t)jx * n;
+  const int64_t* idx = p.idx + (int64_t)e * n;
+  const uint8_t* vm = p.valid + (int64_t)e * n;
+  const float* Qe = p.Q + (int64_t)e * n;
+  for (int64_t k = k0 + threadIdx.x; k < k1; k += kThreads) {
+    const bool vmk = vm[k] != 0;
+    const int64_t ind = vmk ? idx[k] : 0;
+    const float Xi[3] = {Xi_all[ind * 3], Xi_all[ind * 3 + 1], Xi_all[ind * 3 + 2]};
+    const float Xj[3] = {Xj_all[k * 3], Xj_all[k * 3 + 1], Xj_all[k * 3 + 2]};
+    const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
+    const float n1i = sqrtf(n2i);
+    const float n1i_inv = 1.0f / n1i;
+    const float ri[3] = {n1i_inv * Xi[0], n1i_inv * Xi[1], n1i_inv * Xi[2]};
+    float P[3];
+    s3lie::act_sim3(Tij, Xj, P);
+    const float n2j = P[0] * P[0] + P[1] * P[1] + P[2] * P[2];
+    const float n1j = sqrtf(n2j);
+    const float n1j_inv = 1.0f / n1j;
+    const float rj[3] = {n1j_inv * P[0], n1j_inv * P[1], n1j_inv * P[2]};
+    const float err[4] = {rj[0] - ri[0], rj[1] - ri[1], rj[2] - ri[2], n1j - n1i};
+    const float q = Qe[k];
+    const float ci = Ci_all[ind], cj = Cj_all[k];
+    const bool valid = vmk & (q > p.Q_thresh) & (ci > p.C_thresh) & (cj > p.C_thresh);
+    const float sq = sqrtf(q);
+    const float swr = valid ? p.inv_sr * sq : 0.f;
+    const float swd = valid ? p.inv_sd * sq : 0.f;
+    float w[4];
+    w[0] = huber_w(swr * err[0]) * (swr * swr);
+    w[1] = huber_w(swr * err[1]) * (swr * swr);
+    w[2] = huber_w(swr * err[2]) * (swr * swr);
+    w[3] = huber_w(swd * err[3]) * (swd * swd);
+    const float n3 = n1j_inv / n2j;
+    const float dxx = n1j_inv - P[0] * P[0] * n3, dyy = n1j_inv - P[1] * P[1] * n3;
+    const float dzz = n1j_inv - P[2] * P[2] * n3;
+    const float dxy = -P[0] * P[1] * n3, dxz = -P[0] * P[2] * n3, dyz = -P[1] * P[2] * n3;
+    const float Jl[4][7] = {{dxx, dxy, dxz, 0.f, rj[2], -rj[1], 0.f},
+                            {dxy, dyy, dyz, -rj[2], 0.f, rj[0], 0.f},
+                            {dxz, dyz, dzz, rj[1], -rj[0], 0.f, 0.f},
+                            {rj[0], rj[1], rj[2], 0.f, 0.f, 0.f, n1j}};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float Jj[7];
+      adj_inv(Ti, Jl[r], Jj);
+      int c = 0;
+#pragma unroll
+      for (int a = 0; a < 7; ++a)
+#pragma unroll
+        for (int b = a; b < 7; ++b) acc[c++] += w[r] * Jj[a] * Jj[b];
+#pragma unroll
+      for (int a = 0; a < 7; ++a) acc[28 + a] += w[r] * err[r] * Jj[a];
+    }
+  }
+  __shared__ float red[kThreads / 64][NA];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    float v = acc[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wave][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < NA)
+    p.partial[((int64_t)e * S + s) * NA + threadIdx.x] =
+        (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+// Per edge, fixed-order fp64 sum of the slices: esum [E, NA].
+__global__ void k_edge_sum(const float* __restrict__ partial, int S, int E,
+                           double* __restrict__ esum, const double* state) {
+  if (state && state[0] != 0.0) return;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= E * NA) return;
+  const int e = t / NA, k = t % NA;
+  double s = 0.0;
+  for (int i = 0; i < S; ++i) s += (double)partial[((int64_t)e * S + i) * NA + k];
+  esum[t] = s;
+}
+
+__device__ __forceinline__ double a_elem(const double* A, int a, int b) {
+  // upper-triangle row-major index of (min, max)
+  const int r = a < b ? a : b, c = a < b ? b : a;
+  return A[r * 7 - r * (r - 1) / 2 + (c - r)];
+}
+
+// Dense H [n x n], b [n] over the unfixed poses: edge blocks (io,io)+A,
+// (io,jo)-A, (jo,io)-A, (jo,jo)+A and b(io) -u, b(jo) +u (SparseBlock
+// update_lhs/update_rhs with Hs = {A, -A, -A, A}, gs = {-u, u}).
+__global__ void k_assemble(const double* __restrict__ esum, const int32_t* __restrict__ ii,
+                           const int32_t* __restrict__ jj, int E, int num_fix, int n,
+                           double* __restrict__ H, double* __restrict__ b, const double* state) {
+  if (state && state[0] != 0.0) return;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)n * n + n) return;
+  if (t < (int64_t)n * n) {
+    const int r = (int)(t / n), c = (int)(t % n);
+    const int pr = r / 7, a = r % 7, pc = c / 7, bb = c % 7;
+    double h = 0.0;
+    for (int e = 0; e < E; ++e) {
+      const int io = ii[e] - num_fix, jo = jj[e] - num_fix;
+      const double* A = esum + (int64_t)e * NA;
+      double sgn = 0.0;
+      if (pr == io && pc == io) sgn += 1.0;
+      if (pr == io && pc == jo) sgn -= 1.0;
+      if (pr == jo && pc == io) sgn -= 1.0;
+      if (pr == jo && pc == jo) sgn += 1.0;
+      if (sgn != 0.0) h += sgn * a_elem(A, a, bb);
+    }
+    H[t] = h;
+  } else {
+    const int r = (int)(t - (int64_t)n * n);
+    const int pr = r / 7, a = r % 7;
+    double v = 0.0;
+    for (int e = 0; e < E; ++e) {
+      const int io = ii[e] - num_fix, jo = jj[e] - num_fix;
+      const double u = esum[(int64_t)e * NA + 28 + a];
+      if (pr == io) v -= u;
+      if (pr == jo) v += u;
+    }
+    b[r] = v;
+  }
+}
+
+// One workgroup: in-place fp64 Cholesky H = L L^T (lower), then L L^T x = b,
+// dx = -x (fp32).  Not positive definite -> dx = 0 (the reference returns
+// zeros when SimplicialLLT fails), which then ends the iterations.
+__global__ void __launch_bounds__(kThreads)
+k_chol_solve(double* __restrict__ H, double* __restrict__ b, int n, float* __restrict__ dx,
+             double* state) {
+  if (state && state[0] != 0.0) return;
+  __shared__ int fail;
+  __shared__ double piv;
+  const int tid = threadIdx.x;
+  if (tid == 0) fail = 0;
+  __syncthreads();
+  for (int k = 0; k < n; ++k) {
+    if (tid == 0) {
+      const double d = H[(int64_t)k * n + k];
+      if (!(d > 0.0)) fail = 1;
+      piv = fail ? 1.0 : sqrt(d);
+      H[(int64_t)k * n + k] = piv;
+    }
+    __syncthreads();
+    if (fail) break;
+    const double pv = piv;
+    for (int i = k + 1 + tid; i < n; i += kThreads) H[(int64_t)i * n + k] /= pv;
+    __syncthreads();
+    const int m = n - k - 1;
+    for (int64_t t = tid; t < (int64_t)m * m; t += kThreads) {
+      const int i = k + 1 + (int)(t / m), j = k + 1 + (int)(t % m);
+      if (j <= i) H[(int64_t)i * n + j] -= H[(int64_t)i * n + k] * H[(int64_t)j * n + k];
+    }
+    __syncthreads();
+  }
+  if (fail) {
+    for (int i = tid; i < n; i += kThreads) dx[i] = 0.f;
+    return;
+  }
+  // forward: L y = b (y overwrites b)
+  for (int k = 0; k < n; ++k) {
+    if (tid == 0) b[k] /= H[(int64_t)k * n + k];
+    __syncthreads();
+    const double yk = b[k];
+    for (int i = k + 1 + tid; i < n; i += kThreads) b[i] -= H[(int64_t)i * n + k] * yk;
+    __syncthreads();
+  }
+  // backward: L^T x = y
+  for (int k = n - 1; k >= 0; --k) {
+    if (tid == 0) b[k] /= H[(int64_t)k * n + k];
+    __syncthreads();
+    const double xk = b[k];
+    for (int i = tid; i < k; i += kThreads) b[i] -= H[(int64_t)k * n + i] * xk;
+    __syncthreads();
+  }
+  for (int i = tid; i < n; i += kThreads) dx[i] = (float)(-b[i]);
+}
+
+// pose_retr_kernel (gn_kernels.cu:414-454): T_k <- Exp(dx_k) T_k for the
+// unfixed poses, |dx|, iteration count and the termination flag.
+// state: [0] flag (1 = |dx| < delta_thresh), [1] iterations, [2] |dx|.
+__global__ void __launch_bounds__(kThreads)
+k_retr(float* __restrict__ Twc, int n_poses, int num_fix, const float* __restrict__ dx,
+       float delta_thresh, double* state) {
+  if (state[0] != 0.0) return;
+  const int tid = threadIdx.x;
+  for (int k = num_fix + tid; k < n_poses; k += kThreads) {
+    float T[8], out[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) T[c] = Twc[k * 8 + c];
+    s3lie::retr_sim3(T, dx + (k - num_fix) * 7, out);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) Twc[k * 8 + c] = out[c];
+  }
+  const int m = (n_poses - num_fix) * 7;
+  double s = 0.0;
+  for (int i = tid; i < m; i += kThreads) s += (double)dx[i] * (double)dx[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  __shared__ double red[kThreads / 64];
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) {
+    const float nrm = (float)sqrt((red[0] + red[1]) + (red[2] + red[3]));
+    state[1] += 1.0;
+    state[2] = nrm;
+    if (nrm < delta_thresh) state[0] = 1.0;
+  }
+}
+
+struct Ws {
+  float* partial;
+  double* esum;
+  double* H;
+  double* b;
+  double* state;
+  int S;
+};
+
+int slices(int n_edges, int64_t n_points) {
+  int S = (int)s3::cdiv(1024, n_edges > 0 ? n_edges : 1);
+  const int64_t maxs = s3::cdiv(n_points, 1024);
+  if (S > maxs) S = (int)maxs;
+  return S < 1 ? 1 : S;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+Ws carve(void* ws, int n_poses, int n_edges, int64_t n_points, int num_fix) {
+  Ws w;
+  w.S = slices(n_edges, n_points);
+  const int n = 7 * (n_poses - num_fix);
+  char* p = static_cast<char*>(ws);
+  w.partial = reinterpret_cast<float*>(p);
+  p += align256(sizeof(float) * (size_t)n_edges * w.S * NA);
+  w.esum = reinterpret_cast<double*>(p);
+  p += align256(sizeof(double) * (size_t)n_edges * NA);
+  w.H = reinterpret_cast<double*>(p);
+  p += align256(sizeof(double) * (size_t)n * n);
+  w.b = reinterpret_cast<double*>(p);
+  p += align256(sizeof(double) * (size_t)n);
+  w.state = reinterpret_cast<double*>(p);
+  return w;
+}
+
+int check_args(int n_poses, int n_edges, int64_t n_points, int num_fix) {
+  S3_REQUIRE(n_poses > num_fix && num_fix >= 0 && n_edges >= 0 && n_points > 0,
+             "s3g: bad sizes (poses %d, fixed %d, edges %d)", n_poses, num_fix, n_edges);
+  S3_REQUIRE(7LL * (n_poses - num_fix) <= 7 * 4096, "s3g: at most 4096 free poses");
+  return S3_OK;
+}
+
+int queue_system(const float* Twc, const float* Xs, const float* Cs, int64_t n_points,
+                 const int32_t* ii, const int32_t* jj, int n_edges, const int64_t* idx,
+                 const uint8_t* valid, const float* Q, float sigma_ray, float sigma_dist,
+                 float C_thresh, float Q_thresh, int num_fix, int n, const Ws& w,
+                 const double* state, hipStream_t st) {
+  if (n_edges > 0) {
+    EdgeP p{Twc, Xs, Cs, n_points, ii, jj, idx, valid, Q, 1.0f / sigma_ray, 1.0f / sigma_dist,
+            C_thresh, Q_thresh, w.partial, state};
+    k_ray_align<<<dim3(w.S, n_edges), kThreads, 0, st>>>(p);
+    S3_LAUNCH_CHECK();
+    k_edge_sum<<<(unsigned)s3::cdiv((int64_t)n_edges * NA, kThreads), kThreads, 0, st>>>(
+        w.partial, w.S, n_edges, w.esum, state);
+    S3_LAUNCH_CHECK();
+  }
+  k_assemble<<<(unsigned)s3::cdiv((int64_t)n * n + n, kThreads), kThreads, 0, st>>>(
+      w.esum, ii, jj, n_edges, num_fix, n, w.H, w.b, state);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+}  // namespace
+
+extern "C" size_t s3g_workspace_bytes(int n_poses, int n_edges, int64_t n_points, int num_fix) {
+  const int S = slices(n_edges, n_points);
+  const size_t n = 7 * (size_t)(n_poses > num_fix ? n_poses - num_fix : 0);
+  return align256(sizeof(float) * (size_t)n_edges * S * NA) +
+         align256(sizeof(double) * (size_t)n_edges * NA) + align256(sizeof(double) * n * n) +
+         align256(sizeof(double) * n) + align256(sizeof(double) * 4);
+}
+
+extern "C" int s3g_ray_system(const float* Twc, int n_poses, const float* Xs, const float* Cs,
+                              int64_t n_points, const int32_t* ii, const int32_t* jj, int n_edges,
+                              const int64_t* idx_ii2jj, const uint8_t* valid_match,
+                              const float* Q, float sigma_ray, float sigma_dist, float C_thresh,
+                              float Q_thresh, int num_fix, void* workspace, double* H, double* b,
+                              void* stream) {
+  if (int r = check_args(n_poses, n_edges, n_points, num_fix)) return r;
+  S3_REQUIRE(workspace && H && b, "s3g_ray_system: null workspace/output");
+  hipStream_t st = s3::as_stream(stream);
+  Ws w = carve(workspace, n_poses, n_edges, n_points, num_fix);
+  w.H = H;
+  w.b = b;
+  const int n = 7 * (n_poses - num_fix);
+  return queue_system(Twc, Xs, Cs, n_points, ii, jj, n_edges, idx_ii2jj, valid_match, Q,
+                      sigma_ray, sigma_dist, C_thresh, Q_thresh, num_fix, n, w, nullptr, st);
+}
+
+extern "C" int s3g_gauss_newton_rays(float* Twc, int n_poses, const float* Xs, const float* Cs,
+                                     int64_t n_points, const int32_t* ii, const int32_t* jj,
+                                     int n_edges, const int64_t* idx_ii2jj,
+                                     const uint8_t* valid_match, const float* Q, float sigma_ray,
+                                     float sigma_dist, float C_thresh, float Q_thresh,
+                                     int max_iter, float delta_thresh, int num_fix,
+                                     void* workspace, float* dx, float* stats, void* stream) {
+  if (int r = check_args(n_poses, n_edges, n_points, num_fix)) return r;
+  S3_REQUIRE(workspace && dx && stats && max_iter >= 0, "s3g_gauss_newton_rays: bad arguments");
+  hipStream_t st = s3::as_stream(stream);
+  Ws w = carve(workspace, n_poses, n_edges, n_points, num_fix);
+  const int n = 7 * (n_poses - num_fix);
+  S3_HIP(hipMemsetAsync(w.state, 0, sizeof(double) * 4, st));
+  S3_HIP(hipMemsetAsync(dx, 0, sizeof(float) * n, st));
+  for (int it = 0; it < max_iter; ++it) {
+    if (int r = queue_system(Twc, Xs, Cs, n_points, ii, jj, n_edges, idx_ii2jj, valid_match, Q,
+                             sigma_ray, sigma_dist, C_thresh, Q_thresh, num_fix, n, w, w.state,
+                             st))
+      return r;
+    k_chol_solve<<<1, kThreads, 0, st>>>(w.H, w.b, n, dx, w.state);
+    S3_LAUNCH_CHECK();
+    k_retr<<<1, kThreads, 0, st>>>(Twc, n_poses, num_fix, dx, delta_thresh, w.state);
+    S3_LAUNCH_CHECK();
+  }
+  // stats = {iterations, |dx|} (fp32) from the device state
+  double host_state[4];
+  S3_HIP(hipMemcpyAsync(host_state, w.state, sizeof(host_state), hipMemcpyDeviceToHost, st));
+  S3_HIP(hipStreamSynchronize(st));
+  stats[0] = (float)host_state[1];
+  stats[1] = (float)host_state[2];
+  return S3_OK;
+}

@@ -7,11 +7,18 @@ Same names, argument order, return lists and errors as the reference:
   refine_matches(D11 f16 [b,h,w,F], D21 f16 [b,n,F], p1 i64 [b,n,2], radius,
                  dilation_max) -> [p1_new i64 [b,n,2]]
 Non-contiguous inputs raise RuntimeError (reference CHECK_CONTIGUOUS).
-gauss_newton_rays / gauss_newton_calib are the backend GN solver
-(scheduled after the hot path): they raise
-NotImplementedError until that row lands.
+  gauss_newton_rays(Twc f32 [N,8] (updated in place), Xs f32 [N,hw,3],
+                    Cs f32 [N,hw,1], ii i64 [E], jj i64 [E], idx_ii2jj i64 [E,hw],
+                    valid_match bool [E,hw,1], Q f32 [E,hw,1], sigma_ray, sigma_dist,
+                    C_thresh, Q_thresh, max_iter, delta_thresh) -> [dx f32 [N-1,7]]
+    (gn.cpp:28-52 -> gn_kernels.cu:1139-1227; include/s3g.h; the whole
+    iteration loop runs on the device, pose 0 fixed as in the reference).
+gauss_newton_calib (calibrated backend, config use_calib) is not built: it
+raises NotImplementedError.
 """
 from __future__ import annotations
+
+import ctypes
 
 import torch
 
@@ -56,11 +63,94 @@ def refine_matches(D11, D21, p1, radius, dilation_max):
     return [p1_new]
 
 
-def gauss_newton_rays(*args, **kwargs):
-    raise NotImplementedError(
-        "gauss_newton_rays: backend GN solver is SURVEY.md §8(f) row f1 (not yet built)")
+_lib.register({
+    "s3g_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                              ctypes.c_int]),
+    "s3g_ray_system": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                      ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "s3g_gauss_newton_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                             ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                             ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                             ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]),
+})
+
+NUM_FIX = 1   # gn_kernels.cu:1156
+
+
+def _gn_inputs(name, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q):
+    _lib.require_cuda(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q)
+    _lib.require_contig(name, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q)
+    N, hw = Xs.shape[0], Xs.shape[1]
+    E = ii.shape[0]
+    if Twc.shape != (N, 8) or Cs.shape[:2] != (N, hw) or jj.shape != (E,):
+        raise RuntimeError(f"{name}: pose/point shape mismatch")
+    if idx_ii2jj.shape[:2] != (E, hw) or valid_match.shape[:2] != (E, hw) or \
+            Q.shape[:2] != (E, hw):
+        raise RuntimeError(f"{name}: edge shape mismatch")
+    for t in (Twc, Xs, Cs, Q):
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"{name}: expected float32 poses/points/confidences")
+    if idx_ii2jj.dtype != torch.int64 or valid_match.dtype != torch.bool:
+        raise RuntimeError(f"{name}: idx_ii2jj must be int64 and valid_match bool")
+    # create_inds (gn_kernels.cu:160-170): global keyframe ids -> rows of Twc
+    unique = torch.unique(torch.cat([ii, jj]), sorted=True)
+    if unique.numel() != N:
+        raise RuntimeError(f"{name}: Twc/Xs rows ({N}) must be the {unique.numel()} unique "
+                           "keyframes of ii/jj, in sorted order")
+    ii_l = torch.searchsorted(unique, ii).to(torch.int32).contiguous()
+    jj_l = torch.searchsorted(unique, jj).to(torch.int32).contiguous()
+    return N, hw, E, ii_l, jj_l
+
+
+def gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, sigma_ray, sigma_dist,
+                      C_thresh, Q_thresh, max_iter, delta_thresh):
+    N, hw, E, ii_l, jj_l = _gn_inputs("gauss_newton_rays", Twc, Xs, Cs, ii, jj, idx_ii2jj,
+                                      valid_match, Q)
+    dev = Twc.device
+    L = _lib.lib()
+    ws = torch.empty(int(L.s3g_workspace_bytes(N, E, hw, NUM_FIX)), dtype=torch.uint8,
+                     device=dev)
+    dx = torch.zeros(N - NUM_FIX, 7, device=dev, dtype=torch.float32)
+    stats = (ctypes.c_float * 2)()
+    _lib.call("s3g_gauss_newton_rays", Twc.data_ptr(), N, Xs.data_ptr(), Cs.data_ptr(), hw,
+              ii_l.data_ptr(), jj_l.data_ptr(), E, idx_ii2jj.data_ptr(), valid_match.data_ptr(),
+              Q.data_ptr(), float(sigma_ray), float(sigma_dist), float(C_thresh),
+              float(Q_thresh), int(max_iter), float(delta_thresh), NUM_FIX, ws.data_ptr(),
+              dx.data_ptr(), stats, _lib.stream(dev))
+    gauss_newton_rays.last_stats = (int(stats[0]), float(stats[1]))
+    return [dx]
+
+
+def ray_system(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, sigma_ray, sigma_dist, C_thresh,
+               Q_thresh):
+    """One iteration's dense normal equations (H, b) in fp64 (diagnostics
+    and tests; the reference keeps them inside gauss_newton_rays_cuda)."""
+    N, hw, E, ii_l, jj_l = _gn_inputs("ray_system", Twc, Xs, Cs, ii, jj, idx_ii2jj,
+                                      valid_match, Q)
+    dev = Twc.device
+    n = 7 * (N - NUM_FIX)
+    L = _lib.lib()
+    ws = torch.empty(int(L.s3g_workspace_bytes(N, E, hw, NUM_FIX)), dtype=torch.uint8,
+                     device=dev)
+    H = torch.empty(n, n, device=dev, dtype=torch.float64)
+    b = torch.empty(n, device=dev, dtype=torch.float64)
+    _lib.call("s3g_ray_system", Twc.data_ptr(), N, Xs.data_ptr(), Cs.data_ptr(), hw,
+              ii_l.data_ptr(), jj_l.data_ptr(), E, idx_ii2jj.data_ptr(), valid_match.data_ptr(),
+              Q.data_ptr(), float(sigma_ray), float(sigma_dist), float(C_thresh),
+              float(Q_thresh), NUM_FIX, ws.data_ptr(), H.data_ptr(), b.data_ptr(),
+              _lib.stream(dev))
+    return H, b
 
 
 def gauss_newton_calib(*args, **kwargs):
     raise NotImplementedError(
-        "gauss_newton_calib: backend GN solver is SURVEY.md §8(f) row f1 (not yet built)")
+        "gauss_newton_calib: the calibrated backend solver (config use_calib) is not built")

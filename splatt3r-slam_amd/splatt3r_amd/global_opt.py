@@ -1,0 +1,110 @@
+"""FactorGraph of the SLAM backend (splatt3r_slam/global_opt.py:12-158),
+ray mode: keyframe pairs -> batched symmetric decode + matching (one fused
+pair plan per batch, splatt3r_utils.splatt3r_match_symmetric) -> two-way
+edges -> the device-resident Gauss-Newton of include/s3g.h
+(mast3r_slam_backends.gauss_newton_rays).
+
+Same attribute names, edge bookkeeping and acceptance rule as the
+reference; the calibrated solve (config use_calib) is not built.
+"""
+from __future__ import annotations
+
+import torch
+
+import lietorch
+import mast3r_slam_backends
+from splatt3r_amd.config import config
+from splatt3r_amd.splatt3r_utils import splatt3r_match_symmetric
+
+
+class FactorGraph:
+    def __init__(self, model, frames, K=None, device="cuda"):
+        self.model = model
+        self.frames = frames
+        self.device = device
+        self.cfg = config["local_opt"]
+        L = lambda dt: torch.as_tensor([], dtype=dt, device=device)
+        self.ii, self.jj = L(torch.long), L(torch.long)
+        self.idx_ii2jj, self.idx_jj2ii = L(torch.long), L(torch.long)
+        self.valid_match_j, self.valid_match_i = L(torch.bool), L(torch.bool)
+        self.Q_ii2jj, self.Q_jj2ii = L(torch.float32), L(torch.float32)
+        self.window_size = self.cfg["window_size"]
+        self.K = K
+
+    def add_factors(self, ii, jj, min_match_frac, is_reloc=False):
+        """global_opt.py:30-99."""
+        kf_ii = [self.frames[i] for i in ii]
+        kf_jj = [self.frames[j] for j in jj]
+        feat_i = torch.cat([k.feat for k in kf_ii])
+        feat_j = torch.cat([k.feat for k in kf_jj])
+        pos_i = torch.cat([k.pos for k in kf_ii])
+        pos_j = torch.cat([k.pos for k in kf_jj])
+        shape_i = [k.img_true_shape for k in kf_ii]
+        shape_j = [k.img_true_shape for k in kf_jj]
+        (idx_i2j, idx_j2i, valid_match_j, valid_match_i, Qii, Qjj, Qji, Qij) = \
+            splatt3r_match_symmetric(self.model, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j)
+        b = torch.arange(idx_i2j.shape[0], device=idx_i2j.device)[:, None].repeat(
+            1, idx_i2j.shape[1])
+        Qj = torch.sqrt(Qii[b, idx_i2j] * Qji)
+        Qi = torch.sqrt(Qjj[b, idx_j2i] * Qij)
+        valid_j = valid_match_j & (Qj > self.cfg["Q_conf"])
+        valid_i = valid_match_i & (Qi > self.cfg["Q_conf"])
+        match_frac_j = valid_j.sum(dim=(1, 2)) / (valid_j.shape[1] * valid_j.shape[2])
+        match_frac_i = valid_i.sum(dim=(1, 2)) / (valid_i.shape[1] * valid_i.shape[2])
+        ii_t = torch.as_tensor(ii, device=self.device)
+        jj_t = torch.as_tensor(jj, device=self.device)
+        # both directions must clear the threshold; consecutive edges always stay
+        invalid = (torch.minimum(match_frac_j, match_frac_i) < min_match_frac) & \
+            ~(ii_t == jj_t - 1)
+        if is_reloc and bool(invalid.any()):
+            return False
+        keep = ~invalid
+        self.ii = torch.cat([self.ii, ii_t[keep]])
+        self.jj = torch.cat([self.jj, jj_t[keep]])
+        self.idx_ii2jj = torch.cat([self.idx_ii2jj, idx_i2j[keep]])
+        self.idx_jj2ii = torch.cat([self.idx_jj2ii, idx_j2i[keep]])
+        self.valid_match_j = torch.cat([self.valid_match_j, valid_match_j[keep]])
+        self.valid_match_i = torch.cat([self.valid_match_i, valid_match_i[keep]])
+        self.Q_ii2jj = torch.cat([self.Q_ii2jj, Qj[keep]])
+        self.Q_jj2ii = torch.cat([self.Q_jj2ii, Qi[keep]])
+        return bool(keep.sum() > 0)
+
+    def get_unique_kf_idx(self):
+        return torch.unique(torch.cat([self.ii, self.jj]), sorted=True)
+
+    def prep_two_way_edges(self):
+        """global_opt.py:105-111."""
+        ii = torch.cat((self.ii, self.jj), dim=0)
+        jj = torch.cat((self.jj, self.ii), dim=0)
+        idx = torch.cat((self.idx_ii2jj, self.idx_jj2ii), dim=0)
+        valid = torch.cat((self.valid_match_j, self.valid_match_i), dim=0)
+        Q = torch.cat((self.Q_ii2jj, self.Q_jj2ii), dim=0)
+        return ii, jj, idx, valid, Q
+
+    def get_poses_points(self, unique_kf_idx):
+        kfs = [self.frames[int(i)] for i in unique_kf_idx]
+        Xs = torch.stack([k.X_canon for k in kfs])
+        T_WCs = lietorch.Sim3(torch.stack([k.T_WC.data.reshape(1, 8) for k in kfs]))
+        Cs = torch.stack([k.get_average_conf() for k in kfs])
+        return Xs, T_WCs, Cs
+
+    def solve_GN_rays(self):
+        """global_opt.py:121-158."""
+        pin = self.cfg["pin"]
+        unique = self.get_unique_kf_idx()
+        if unique.numel() <= pin:
+            return None
+        Xs, T_WCs, Cs = self.get_poses_points(unique)
+        ii, jj, idx, valid, Q = self.prep_two_way_edges()
+        pose_data = T_WCs.data[:, 0, :].contiguous()
+        (dx,) = mast3r_slam_backends.gauss_newton_rays(
+            pose_data, Xs.contiguous().float(), Cs.contiguous().float(), ii.contiguous(),
+            jj.contiguous(), idx.contiguous(), valid.contiguous(), Q.contiguous().float(),
+            self.cfg["sigma_ray"], self.cfg["sigma_dist"], self.cfg["C_conf"],
+            self.cfg["Q_conf"], self.cfg["max_iters"], self.cfg["delta_norm"])
+        for k in range(pin, unique.numel()):
+            self.frames[int(unique[k])].T_WC = lietorch.Sim3(pose_data[k:k + 1].clone())
+        return dx
+
+    def solve_GN_calib(self):
+        raise NotImplementedError("calibrated backend GN (gauss_newton_calib) is not built")
