@@ -32,6 +32,17 @@ int s3r_pack_splats(const float* means, const float* scales, const float* rotati
                     float* means_out, float* cov6_out, float* shs_out,
                     float* opac_out, void* stream);
 
+/* The pose-dependent camera of one render (decoder_splatting_cuda.py:36-55
+ * + cuda_splatting.py:67-113 for a single target view), in fp64 on the
+ * device in one thread instead of two 4x4 inverses and two matmuls:
+ *   Mc = matrix(T_context), Mt = matrix(T_target)    (lietorch Sim3 [8])
+ *   extr = Mc^-1 Mt, extr[:3,3] *= scale
+ *   view = (extr^-1)^T, full = view @ proj_t, campos = extr[:3,3]
+ * proj_t is the transposed projection matrix [16] (row-major, device).
+ * Outputs (device, fp32, row-major): view [16], full [16], campos [3]. */
+int s3r_camera(const float* T_context, const float* T_target, const float* proj_t, float scale,
+               float* view, float* full, float* campos, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,6 +3,7 @@
 // colour: 56 B) and writes the rasterizer inputs once (52 B).
 #include "common.hpp"
 #include "s3r.h"
+#include "sim3_math.hpp"
 
 namespace {
 
@@ -49,7 +50,85 @@ k_pack(const float* __restrict__ means, const float* __restrict__ scales,
   oo[p] = opac[p];
 }
 
+__device__ void sim3_mat(const float* T, double* M) {
+  float R[9];
+  const float q[4] = {T[3], T[4], T[5], T[6]};
+  s3lie::quat_to_rot(q, R);
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) M[4 * r + c] = (double)(R[3 * r + c] * T[7]);
+    M[4 * r + 3] = (double)T[r];
+  }
+  M[12] = M[13] = M[14] = 0.0;
+  M[15] = 1.0;
+}
+
+// Gauss-Jordan inverse with partial pivoting (4x4, fp64).
+__device__ void inv4(const double* A, double* out) {
+  double m[4][8];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      m[r][c] = A[4 * r + c];
+      m[r][4 + c] = r == c ? 1.0 : 0.0;
+    }
+  for (int c = 0; c < 4; ++c) {
+    int p = c;
+    for (int r = c + 1; r < 4; ++r)
+      if (fabs(m[r][c]) > fabs(m[p][c])) p = r;
+    if (p != c)
+      for (int k = 0; k < 8; ++k) { const double t = m[c][k]; m[c][k] = m[p][k]; m[p][k] = t; }
+    const double d = 1.0 / m[c][c];
+    for (int k = 0; k < 8; ++k) m[c][k] *= d;
+    for (int r = 0; r < 4; ++r)
+      if (r != c) {
+        const double f = m[r][c];
+        for (int k = 0; k < 8; ++k) m[r][k] -= f * m[c][k];
+      }
+  }
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) out[4 * r + c] = m[r][4 + c];
+}
+
+__device__ void mul4(const double* A, const double* B, double* C) {
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      double s = 0.0;
+      for (int k = 0; k < 4; ++k) s += A[4 * r + k] * B[4 * k + c];
+      C[4 * r + c] = s;
+    }
+}
+
+__global__ void k_camera(const float* __restrict__ Tc, const float* __restrict__ Tt,
+                         const float* __restrict__ proj_t, float scale, float* __restrict__ view,
+                         float* __restrict__ full, float* __restrict__ campos) {
+  if (threadIdx.x != 0) return;
+  double Mc[16], Mt[16], Ic[16], E[16], Ie[16], V[16], P[16], F[16];
+  sim3_mat(Tc, Mc);
+  sim3_mat(Tt, Mt);
+  inv4(Mc, Ic);
+  mul4(Ic, Mt, E);
+  for (int r = 0; r < 3; ++r) E[4 * r + 3] *= (double)scale;
+  inv4(E, Ie);
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) V[4 * r + c] = Ie[4 * c + r];
+  for (int k = 0; k < 16; ++k) P[k] = (double)proj_t[k];
+  mul4(V, P, F);
+  for (int k = 0; k < 16; ++k) {
+    view[k] = (float)V[k];
+    full[k] = (float)F[k];
+  }
+  for (int r = 0; r < 3; ++r) campos[r] = (float)E[4 * r + 3];
+}
+
 }  // namespace
+
+extern "C" int s3r_camera(const float* T_context, const float* T_target, const float* proj_t,
+                          float scale, float* view, float* full, float* campos, void* stream) {
+  S3_REQUIRE(T_context && T_target && proj_t && view && full && campos, "s3r_camera: null");
+  k_camera<<<1, 64, 0, s3::as_stream(stream)>>>(T_context, T_target, proj_t, scale, view, full,
+                                                campos);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
 
 extern "C" int s3r_pack_splats(const float* means, const float* scales, const float* rotations,
                                const float* sh, const float* opacities, const float* img,

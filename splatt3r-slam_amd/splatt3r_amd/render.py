@@ -22,6 +22,7 @@ from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianR
 from splatt3r_amd import _lib
 
 _lib.register({
+    "s3r_camera": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_float] + [ctypes.c_void_p] * 4),
     "s3r_pack_splats": (ctypes.c_int, [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.c_int,
                         ctypes.c_float, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_void_p]),
 })
@@ -103,6 +104,46 @@ def camera_settings(extrinsics, intrinsics, near, far, image_shape, background_c
             projmatrix=full_projection[i], sh_degree=sh_degree,
             campos=extrinsics[i, :3, 3], prefiltered=False, debug=False))
     return out, scale
+
+
+_INTR_CACHE: dict = {}
+
+
+def camera_settings_sim3(T_context, T_target, K, image_shape, background_color, near=0.1,
+                         far=1000.0, sh_degree=0):
+    """camera_settings for the per-frame render (one target view) straight
+    from the two Sim3 poses: the intrinsics-only part (fov, projection,
+    scale) is computed once per (K, image size, near, far) with the same
+    torch ops as camera_settings and cached on the device; the pose part
+    (two 4x4 inverses, the scale-invariant rescale, the products) is one
+    fp64 HIP thread (s3r_camera).  Returns ([settings], scale)."""
+    dev = T_context.device
+    h, w = image_shape
+    Kc = K.detach().to("cpu", torch.float32).reshape(3, 3)
+    key = (tuple(Kc.flatten().tolist()), h, w, float(near), float(far), str(dev))
+    hit = _INTR_CACHE.get(key)
+    if hit is None:
+        nr = torch.full((1,), float(near))
+        fr = torch.full((1,), float(far))
+        scale = 1 / nr
+        intr = normalize_intrinsics(Kc[None], (h, w))[..., :3, :3]
+        fov_x, fov_y = get_fov(intr).unbind(dim=-1)
+        tx = float((0.5 * fov_x).tan()[0])
+        ty = float((0.5 * fov_y).tan()[0])
+        projT = get_projection_matrix(nr * scale, fr * scale, fov_x, fov_y).transpose(1, 2)
+        hit = (tx, ty, projT[0].contiguous().to(dev), float(scale[0]))
+        _INTR_CACHE[key] = hit
+    tx, ty, projT, scale = hit
+    buf = torch.empty(35, device=dev, dtype=torch.float32)
+    Tc = T_context.reshape(-1, 8)[0].float().contiguous()
+    Tt = T_target.reshape(-1, 8)[0].float().contiguous()
+    _lib.call("s3r_camera", Tc.data_ptr(), Tt.data_ptr(), projT.data_ptr(), float(scale),
+              buf.data_ptr(), buf[16:].data_ptr(), buf[32:].data_ptr(), _lib.stream(dev))
+    st = GaussianRasterizationSettings(
+        image_height=h, image_width=w, tanfovx=tx, tanfovy=ty, bg=background_color,
+        scale_modifier=1.0, viewmatrix=buf[:16].view(4, 4), projmatrix=buf[16:32].view(4, 4),
+        sh_degree=sh_degree, campos=buf[32:35], prefiltered=False, debug=False)
+    return [st], torch.tensor([scale])
 
 
 def render_cuda(extrinsics, intrinsics, near, far, image_shape, background_color,

@@ -24,7 +24,8 @@ import torch
 import lietorch
 from splatt3r_amd import _lib, matching
 from splatt3r_amd.config import config
-from splatt3r_amd.render import (DecoderSplattingCUDA, camera_settings, normalize_intrinsics,
+from splatt3r_amd.render import (DecoderSplattingCUDA, camera_settings, camera_settings_sim3,
+                                  normalize_intrinsics,
                                  pack_splats)
 
 C0 = 0.28209479177387814
@@ -222,20 +223,15 @@ def splatt3r_render(model, frame, ref_frame, K=None, target_T_WC=None):
     g1, g2 = frame.gaussian_pred, frame.gaussian_pred_cross
     dev = g1["means"].device
     _, h, w, _ = g1["means"].shape
-    context = _sim3_to_4x4(frame.T_WC).to(dev)
-    target = context.clone() if target_T_WC is None else _sim3_to_4x4(target_T_WC).to(dev)
-    # intrinsics-only math on the host (no device sync for the fov floats)
+    # intrinsics-only math on the host (cached), the pose part in one fp64
+    # HIP thread: decoder_splatting_cuda.py:36-55 + cuda_splatting.py:67-113
     K_use = (_estimate_default_intrinsics(h, w, "cpu") if K is None
              else K.detach().to(device="cpu", dtype=torch.float32).clone())
-    if K_use.dim() == 2:
-        K_use = K_use.unsqueeze(0)
-    # decoder_splatting_cuda.py:36-55
-    extr = torch.linalg.inv_ex(context)[0] @ target   # inv_ex: no host-side error check
-    intr = normalize_intrinsics(K_use, (h, w))[..., :3, :3]
-    near = torch.full((1,), 0.1)
-    far = torch.full((1,), 1000.0)
-    bg = model.decoder.background_color.to(dev)[None]
-    settings, scale = camera_settings(extr, intr, near, far, (h, w), bg, 0)
+    T_tgt = frame.T_WC if target_T_WC is None else target_T_WC
+    bg = model.decoder.background_color.to(dev)
+    settings, scale = camera_settings_sim3(frame.T_WC.data.to(dev), T_tgt.data.to(dev),
+                                           K_use.reshape(-1, 3, 3)[0], (h, w), bg, near=0.1,
+                                           far=1000.0, sh_degree=0)
     views = []
     for g, img in ((g1, frame.img), (g2, ref_frame.img)):
         views.append(dict(means=g["means"].reshape(-1, 3), scales=g["scales"].reshape(-1, 3),

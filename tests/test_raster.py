@@ -269,3 +269,33 @@ def test_hip_render_glue_boundary_vs_reference_capture():
     np.testing.assert_allclose(shs.cpu().numpy(), g["in_shs"], rtol=1e-5, atol=1e-5)
     np.testing.assert_array_equal(opac.cpu().numpy(), g["in_opacities"])
     del pack_splats
+
+
+def _mat_to_sim3(M):
+    """[sR | t] 4x4 -> lietorch Sim3 data (t, q xyzw, s)."""
+    M = np.asarray(M, np.float64).reshape(4, 4)
+    s = np.cbrt(np.linalg.det(M[:3, :3]))
+    R = M[:3, :3] / s
+    w = np.sqrt(max(1e-12, 1 + R[0, 0] + R[1, 1] + R[2, 2])) / 2
+    q = np.array([(R[2, 1] - R[1, 2]) / (4 * w), (R[0, 2] - R[2, 0]) / (4 * w),
+                  (R[1, 0] - R[0, 1]) / (4 * w), w])
+    return np.concatenate([M[:3, 3], q / np.linalg.norm(q), [s]]).astype(np.float32)
+
+
+@pytest.mark.gpu
+def test_hip_camera_settings_from_sim3_vs_reference_capture():
+    """camera_settings_sim3 (cached intrinsics + one fp64 s3r_camera thread)
+    reproduces the settings the reference decoder glue built for the
+    captured poses/intrinsics (render_boundary.npz)."""
+    from splatt3r_amd.render import camera_settings_sim3
+    g = np.load(os.path.join(GOLDEN, "render_boundary.npz"))
+    Tc = torch.from_numpy(_mat_to_sim3(g["head_ctx_pose"])).cuda()
+    Tt = torch.from_numpy(_mat_to_sim3(g["head_tgt_pose"])).cuda()
+    K = torch.from_numpy(g["head_K"].reshape(3, 3))
+    h, w = int(g["settings_image_height"]), int(g["settings_image_width"])
+    (st,), scale = camera_settings_sim3(Tc, Tt, K, (h, w), torch.zeros(3, device="cuda"))
+    assert abs(st.tanfovx - float(g["settings_tanfovx"])) < 1e-6
+    assert abs(st.tanfovy - float(g["settings_tanfovy"])) < 1e-6
+    np.testing.assert_allclose(st.viewmatrix.cpu().numpy(), g["settings_viewmatrix"], atol=2e-6)
+    np.testing.assert_allclose(st.projmatrix.cpu().numpy(), g["settings_projmatrix"], atol=1e-5)
+    np.testing.assert_allclose(st.campos.cpu().numpy(), g["settings_campos"], atol=2e-6)
