@@ -91,6 +91,17 @@ typedef struct {
   int rope_maxpos;
   int rope_ncols;
   const int64_t* rope_pos[S3N_MAX_GROUPS];
+  /* Fused 1x1 tail (the DPT head's last conv, dpt_block.py:323): when
+   * tail_w[g] is set, every finished, activated output row (all N columns:
+   * N must equal the tile width, split_k <= 1) is multiplied by tail_w
+   * [tail_n, N] fp16 and offset by tail_b [tail_n] into tail_out fp32
+   * [M, ld_tail] (tail_n % 8 == 0, <= 16).  C[g] may then be NULL: the
+   * N-wide activation never goes to memory. */
+  const void* tail_w[S3N_MAX_GROUPS];
+  const float* tail_b[S3N_MAX_GROUPS];
+  float* tail_out[S3N_MAX_GROUPS];
+  int tail_n;
+  int64_t ld_tail;
 } s3n_gemm_args;
 
 size_t s3n_gemm_workspace_bytes(const s3n_gemm_args* args);

@@ -46,6 +46,11 @@ struct GemmP {
   float* ws;
   int debug;       // s3n_gemm_set_debug flags (tuning only)
   int vec_epi;     // LDS-staged epilogue with 8-column vector accesses (host-checked)
+  const f16* tail_w[S3N_MAX_GROUPS];   // fused 1x1 tail (s3n.h), tail_n % 8 == 0
+  const float* tail_b[S3N_MAX_GROUPS];
+  float* tail_out[S3N_MAX_GROUPS];
+  int tail_n;
+  int64_t ld_tail;
   int col_major;   // tile order: 1 = M fastest (each XCD owns a band of N)
   const float* rope_cos;
   const float* rope_sin;
@@ -267,7 +272,7 @@ __device__ __forceinline__ void store8_f16(f16* q, const float (&v)[8]) {
 // vector accesses along rows (fully coalesced) instead of one 2-4 B access
 // per accumulator register.  The host enables it when every row stride and
 // base is 16-B aligned and 8-column chunks stay contiguous in the output.
-template <int BM, int BN, int NWM, int NWN, int FM, int FN, int LDT>
+template <int BM, int BN, int NWM, int NWN, int FM, int FN, int LDT, int RING_BYTES>
 __device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int n0,
                                              f32x16 (&acc)[FM][FN], float* stage) {
   constexpr int WM = BM / NWM, WN = BN / NWN, NT = 64 * NWM * NWN;
@@ -285,6 +290,7 @@ __device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int 
   const int64_t* __restrict__ pos = p.rope_pos[g];
   f16* C2 = p.C2[g];
   const bool split = p.split_k > 1;
+  const f16* __restrict__ tw = p.tail_w[g];
   float pb[kPre ? NCH : 1][8], pr[kPre ? NCH : 1][8];
   int64_t pps[kPre ? NCH : 1];
   if constexpr (kPre) {
@@ -368,10 +374,53 @@ __device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int 
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += t[e];
     }
-    const int64_t off = out_offset(p, row, col);
-    if (p.c_f16) store8_f16(reinterpret_cast<f16*>(p.C[g]) + off, v);
-    else store8_f32(reinterpret_cast<float*>(p.C[g]) + off, v);
+    if (p.C[g]) {
+      const int64_t off = out_offset(p, row, col);
+      if (p.c_f16) store8_f16(reinterpret_cast<f16*>(p.C[g]) + off, v);
+      else store8_f32(reinterpret_cast<float*>(p.C[g]) + off, v);
+    }
     if (C2) store8_f16(C2 + (int64_t)row * p.ldc2 + col, v);
+    if (tw) store8_f32(stage + rl * LDT + cl, v);   // the tail reads the finished row
+  }
+  if (tw) {
+    // fused 1x1 tail: out[row, o] = sum_k v[row, k] w[o, k] + b[o] (fp32
+    // activations, fp16 weights, fp32 accumulation), 8 outputs per thread.
+    // The tail weights sit behind the staged tile in LDS when they fit.
+    constexpr int kWOff = BM * LDT * 4;
+    constexpr bool kWLds = kWOff + 16 * BN * 2 <= RING_BYTES;
+    const f16* wsrc = tw;
+    if constexpr (kWLds) {
+      f16* wl = reinterpret_cast<f16*>(reinterpret_cast<char*>(stage) + kWOff);
+      for (int i = tid * 8; i < p.tail_n * BN; i += NT * 8)
+        *reinterpret_cast<f16x8*>(wl + i) = *reinterpret_cast<const f16x8*>(tw + i);
+      wsrc = wl;
+    }
+    __syncthreads();
+    const int TC = p.tail_n / 8;
+    const float* __restrict__ tb = p.tail_b[g];
+    for (int c = tid; c < BM * TC; c += NT) {
+      const int rl = c / TC, oc = (c % TC) * 8;
+      const int row = m0 + rl;
+      if (row >= p.M) continue;
+      float a[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = 0.f;
+      for (int k = 0; k < BN; k += 8) {
+        float x[8];
+        load8(stage + rl * LDT + k, x);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const f16x8 w8 = *reinterpret_cast<const f16x8*>(wsrc + (oc + e) * BN + k);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a[e] += x[j] * (float)w8[j];
+        }
+      }
+      if (tb) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += tb[oc + e];
+      }
+      store8_f32(p.tail_out[g] + (int64_t)row * p.ld_tail + oc, a);
+    }
   }
 }
 
@@ -576,7 +625,8 @@ k_gemm(GemmP p) {
     // row pitch BN + 4 floats where it fits (rows 16 B apart in the banks)
     constexpr int LDT = BM * (BN + 4) * 4 <= kStages * STAGE * 2 ? BN + 4 : BN;
     static_assert(BM * LDT * 4 <= kStages * STAGE * 2, "epilogue staging must fit the ring");
-    epilogue_vec<BM, BN, NWM, NWN, FM, FN, LDT>(p, g, m0, n0, acc, reinterpret_cast<float*>(smem));
+    epilogue_vec<BM, BN, NWM, NWN, FM, FN, LDT, kStages * STAGE * 2>(
+        p, g, m0, n0, acc, reinterpret_cast<float*>(smem));
     return;
   }
   const int s_idx = blockIdx.y;
@@ -655,6 +705,8 @@ __global__ void __launch_bounds__(kThreads) k_splitk_reduce(GemmP p) {
 
 template <int BM, int BN, int S, int NWM = 2, int NWN = 2, int BK = 64>
 int launch(const GemmP& p, hipStream_t st) {
+  S3_REQUIRE(!p.tail_w[0] || p.N == BN,
+             "s3n_gemm: the fused tail needs N == the tile width (%d, N = %d)", BN, p.N);
   constexpr int NT = 64 * NWM * NWN;
   GemmP q = p;
   q.tiles_m = (p.M + BM - 1) / BM;
@@ -703,8 +755,14 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
     S3_REQUIRE(a->K == a->ksize * a->ksize * a->cC, "s3n_gemm: conv K != ks*ks*Cin");
     S3_REQUIRE(a->oH > 0 && a->oW > 0 && a->M % (a->oH * a->oW) == 0, "s3n_gemm: conv M");
   }
+  const bool tail = a->tail_w[0] != nullptr;
   for (int g = 0; g < a->groups; ++g)
-    S3_REQUIRE(a->A[g] && a->B[g] && a->C[g], "s3n_gemm: null operand in group %d", g);
+    S3_REQUIRE(a->A[g] && a->B[g] && (a->C[g] || tail) && (!tail || (a->tail_w[g] && a->tail_out[g])),
+               "s3n_gemm: null operand in group %d", g);
+  if (tail)
+    S3_REQUIRE(a->tail_n > 0 && a->tail_n % 8 == 0 && a->tail_n <= 16 && a->ld_tail % 8 == 0 &&
+                   a->split_k <= 1 && a->store_mode == S3N_STORE_PLAIN,
+               "s3n_gemm: tail needs tail_n in {8, 16}, ld_tail %% 8 == 0, split_k 1, plain store");
   if (a->M == 0) return S3_OK;
   GemmP p;
   p.M = a->M; p.N = a->N; p.K = a->K; p.groups = a->groups;
@@ -746,19 +804,31 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   // every base 16-B aligned, chunks contiguous in the output layout
   {
     auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
-    bool v = a->N % 8 == 0 && !(g_gemm_debug & 16);
+    bool v = a->N % 8 == 0 && (!(g_gemm_debug & 16) || tail);
     if (a->store_mode == S3N_STORE_PLAIN) v = v && a->ldc % 8 == 0;
     else if (a->store_mode == S3N_STORE_CONVT) v = v && a->sCout % 8 == 0;
     else v = false;
     for (int g = 0; g < a->groups && v; ++g) {
-      v = al(a->C[g]) && (!a->bias[g] || al(a->bias[g])) &&
+      v = (!a->C[g] || al(a->C[g])) && (!a->bias[g] || al(a->bias[g])) &&
+          (!a->tail_w[g] || (al(a->tail_w[g]) && al(a->tail_out[g]) &&
+                             (!a->tail_b[g] || al(a->tail_b[g])))) &&
           (!a->R1[g] || (al(a->R1[g]) && a->ldr1 % 8 == 0)) &&
           (!a->R2[g] || (al(a->R2[g]) && a->ldr2 % 8 == 0)) &&
           (!a->C2[g] || (al(a->C2[g]) && a->ldc2 % 8 == 0));
     }
     if (any_rope) v = v && al(a->rope_cos) && al(a->rope_sin);
     p.vec_epi = v ? 1 : 0;
+    S3_REQUIRE(!tail || v, "s3n_gemm: the fused tail needs the vector epilogue (aligned operands, "
+                           "N %% 8 == 0)");
   }
+  for (int g = 0; g < S3N_MAX_GROUPS; ++g) {
+    const bool on = g < a->groups && tail;
+    p.tail_w[g] = on ? (const f16*)a->tail_w[g] : nullptr;
+    p.tail_b[g] = on ? a->tail_b[g] : nullptr;
+    p.tail_out[g] = on ? a->tail_out[g] : nullptr;
+  }
+  p.tail_n = a->tail_n;
+  p.ld_tail = a->ld_tail;
   if (p.split_k > 1)
     S3_REQUIRE(p.ws, "s3n_gemm: split_k > 1 needs a workspace (s3n_gemm_workspace_bytes)");
   hipStream_t st = s3::as_stream(stream);
@@ -775,6 +845,12 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   if (a->tile == 10) return launch<64, 64, 2, 2, 2, 128>(p, st);
   if (a->tile == 11) return launch<64, 128, 2, 2, 2, 128>(p, st);
   if (a->tile == 12) return launch<128, 128, 2, 2, 2, 128>(p, st);
+  // the fused tail needs one column tile per row block
+  if (tail) {
+    S3_REQUIRE(a->N == 64 || a->N == 128, "s3n_gemm: the fused tail needs N of 64 or 128");
+    if (a->N == 128) return launch<64, 128, 3>(p, st);
+    return launch<64, 64, 3>(p, st);
+  }
   // Tile choice: fill the 256 CUs before growing the tile.
   auto tiles = [&](int bm, int bn) {
     return (int64_t)a->groups * ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);

@@ -416,12 +416,13 @@ class PairPlan:
         P.add(self._conv(g4(prev), w.h0_w, g4(c1), Bp, hh, ww, Fd, Fd // 2, 3, 1, 1, bias=g4(w.h0_b)))
         c1u = e(4, Bp, 2 * hh, 2 * ww, Fd // 2)
         P.add(ops.upsample2x(g4(c1), g4(c1u), B=Bp, H=hh, W=ww, C=Fd // 2))
-        c2 = e(4, Bp, 2 * hh, 2 * ww, Fd // 2)
-        P.add(self._conv(g4(c1u), w.h2_w, g4(c2), Bp, 2 * hh, 2 * ww, Fd // 2, Fd // 2, 3, 1, 1,
-                         bias=g4(w.h2_b), act="relu"))
+        # conv3x3 + ReLU with the final 1x1 conv fused into its epilogue: the
+        # 128-channel full-resolution activation never goes to memory
         self.dpt_out = e(4, Bp * H * W, w.NOUT, dt=F32)
-        P.add(ops.gemm(g4(c2), g4(w.h4_w), g4(self.dpt_out), Bp * H * W, w.NOUT, Fd // 2,
-                       lda=Fd // 2, bias=g4(w.h4_b)))
+        P.add(self._conv(g4(c1u), w.h2_w, [None] * 4, Bp, 2 * hh, 2 * ww, Fd // 2, Fd // 2, 3, 1,
+                         1, bias=g4(w.h2_b), act="relu",
+                         tail=(g4(w.h4_w), g4(w.h4_b), g4(self.dpt_out), w.NOUT, w.NOUT)))
+        c2 = None
         # gaussian_postprocess per head
         n = Bp * H * W
         self.res = []
@@ -439,20 +440,20 @@ class PairPlan:
         self._head_bufs = (um, t0, l0, t1, l1, l2, t3, l3, rs, c1, c1u, c2)
         # named stage outputs (group 0 = head 1 pts DPT), for parity diagnostics
         self.stages = dict(ap0=l0[0], ap1=l1[0], ap2=l2[0], ap3=l3[0], rn0=rs[0][0], rn1=rs[1][0],
-                           rn2=rs[2][0], rn3=rs[3][0], head0=c1[0], head3=c2[0],
+                           rn2=rs[2][0], rn3=rs[3][0], head0=c1[0],
                            head4=self.dpt_out[0].view(Bp, H, W, -1)[..., :4], mlp=self.feat25[0])
         self.stages.update(self._ref_outs)
         return P
 
     @staticmethod
     def _conv(A, Wt, C, Bp, H, W, Cin, Cout, k, stride, pad, bias=None, relu_in=False, act="none",
-              R1=None, R2=None):
+              R1=None, R2=None, tail=None):
         oh = (H + 2 * pad - k) // stride + 1
         ow = (W + 2 * pad - k) // stride + 1
         M = Bp * oh * ow
         conv = dict(H=H, W=W, C=Cin, k=k, stride=stride, pad=pad, oH=oh, oW=ow, relu_in=relu_in)
         return ops.gemm(A, _g(Wt, len(A)), C, M, Cout, k * k * Cin, lda=0, bias=bias, act=act,
-                        R1=R1, ldr1=Cout, R2=R2, ldr2=Cout, conv=conv)
+                        R1=R1, ldr1=Cout, R2=R2, ldr2=Cout, conv=conv, tail=tail)
 
     def run(self):
         self.decoder_plan.replay()

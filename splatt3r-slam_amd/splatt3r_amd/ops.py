@@ -38,6 +38,8 @@ class GemmArgs(ctypes.Structure):
         ("split_k", ctypes.c_int), ("tile", ctypes.c_int), ("workspace", P),
         ("rope_cos", P), ("rope_sin", P), ("rope_maxpos", ctypes.c_int),
         ("rope_ncols", ctypes.c_int), ("rope_pos", P * G),
+        ("tail_w", P * G), ("tail_b", P * G), ("tail_out", P * G), ("tail_n", ctypes.c_int),
+        ("ld_tail", I64),
     ]
 
 
@@ -152,15 +154,17 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
 def _tune_key(a):
     f = ("M", "N", "K", "groups", "lda", "ldb", "ldc", "act", "r1_f16", "r2_f16", "c_f16",
          "ldr1", "ldr2", "ldc2", "store_mode", "sS", "sCout", "a_mode", "cH", "cW", "cC", "ksize",
-         "stride", "pad", "oH", "oW", "relu_in", "rope_ncols")
+         "stride", "pad", "oH", "oW", "relu_in", "rope_ncols", "tail_n", "ld_tail")
     return tuple(getattr(a, k) for k in f) + (bool(a.R1[0]), bool(a.R2[0]), bool(a.C2[0]),
-                                               bool(a.bias[0]))
+                                               bool(a.bias[0]), bool(a.C[0]))
 
 
 def _tune_candidates(a, split_ok):
     kt = -(-a.K // 64)
     out = []
     for tile, (bm, bn) in _TILE_SHAPES.items():
+        if a.tail_n and bn != a.N:
+            continue
         tiles = a.groups * -(-a.M // bm) * -(-a.N // bn)
         for sk in (1, 2, 3, 4, 6, 8):
             if sk > 1 and (not split_ok or kt // sk < 4 or tiles * sk > 4096):
@@ -196,9 +200,16 @@ def _tuned(a, A, B, bias, rope, rope_pos, split_ok):
     keep = []
     for i in range(g):
         sa = scratch(a_elems, torch.float16)
-        sc = scratch(c_elems, torch.float16 if a.c_f16 else torch.float32)
-        keep += [sa, sc]
-        t.A[i], t.C[i] = sa.data_ptr(), sc.data_ptr()
+        keep.append(sa)
+        t.A[i] = sa.data_ptr()
+        if a.C[i]:
+            sc = scratch(c_elems, torch.float16 if a.c_f16 else torch.float32)
+            keep.append(sc)
+            t.C[i] = sc.data_ptr()
+        if a.tail_n:
+            so = scratch((a.M - 1) * a.ld_tail + a.tail_n, torch.float32)
+            keep.append(so)
+            t.tail_out[i] = so.data_ptr()
         if a.R1[i]:
             r = scratch((a.M - 1) * a.ldr1 + a.N, torch.float16 if a.r1_f16 else torch.float32)
             keep.append(r)
@@ -245,11 +256,13 @@ def _tuned(a, A, B, bias, rope, rope_pos, split_ok):
 
 def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1=None,
          ldr1=0, R2=None, ldr2=0, C2=None, ldc2=0, conv=None, store=None, split_k=None,
-         tile=0, rope=None, rope_pos=None, rope_ncols=0) -> Call:
+         tile=0, rope=None, rope_pos=None, rope_ncols=0, tail=None) -> Call:
     """Grouped GEMM: A, B, C, bias, R1, R2, C2 are lists (one entry per group)
     of tensors / raw pointers.  conv = dict(H, W, C, k, stride, pad, oH, oW,
     relu_in) switches A to implicit im2col of an NHWC image.  store =
-    ("convt"|"pixshuf", sH, sW, s, Cout)."""
+    ("convt"|"pixshuf", sH, sW, s, Cout).  tail = (W [tail_n, N] fp16, bias fp32,
+    out fp32 [M, ld], tail_n, ld) lists per group: the fused 1x1 tail (s3n.h);
+    C entries may then be None."""
     a = GemmArgs()
     groups = len(A)
     a.M, a.N, a.K, a.groups = int(M), int(N), int(K), groups
@@ -273,7 +286,12 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         a.R2 = _parr(R2)
         a.ldr2 = int(ldr2)
         a.r2_f16 = int(dtype_f16(R2[0]))
-    a.c_f16 = int(dtype_f16(C[0]))
+    a.c_f16 = int(dtype_f16(C[0])) if C[0] is not None else 0
+    if tail is not None:
+        tw, tb, to, tn, tld = tail
+        a.tail_w, a.tail_b, a.tail_out = _parr(tw), _parr(tb), _parr(to)
+        a.tail_n, a.ld_tail = int(tn), int(tld)
+        split_k = 1
     if C2 is not None:
         a.C2 = _parr(C2)
         a.ldc2 = int(ldc2)
@@ -305,7 +323,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
         a.workspace = ws.data_ptr()
     return Call("s3n_gemm", ctypes.byref(a), keep=(a, A, B, C, bias, R1, R2, C2, ws, rope,
-                                                    rope_pos),
+                                                    rope_pos, tail),
                 kind="gemm.conv" if conv is not None else "gemm.dense",
                 flops=2 * int(M) * int(N) * int(K) * groups,
                 desc=f"gemm{'.conv' if conv is not None else ''} {M}x{N}x{K} g{groups}"

@@ -393,3 +393,30 @@ def test_gemm_vector_epilogue_matches_register_epilogue(case):
             assert rel_err(y, x.float()) < 2e-3
         else:
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("tile,tn,store_c", [(3, 16, False), (2, 16, True), (4, 8, False),
+                                             (0, 16, False)])
+def test_gemm_conv_fused_1x1_tail(tile, tn, store_c):
+    """conv3x3 + bias + ReLU with the 1x1 conv fused in the epilogue (the DPT
+    head's last two convs, dpt_block.py:321-323) vs torch fp32."""
+    from splatt3r_amd import ops, _lib
+    B, H, W, Cin, Cout, g = 1, 20, 28, 128, 128, 2
+    xs = [_rand(B, H, W, Cin, seed=31 + i) for i in range(g)]
+    ws = [_rand(Cout, Cin, 3, 3, scale=(Cin * 9) ** -0.5, seed=41 + i) for i in range(g)]
+    bs = [_rand(Cout, dtype=torch.float32, seed=51 + i) for i in range(g)]
+    tw = [_rand(tn, Cout, scale=Cout ** -0.5, seed=61 + i) for i in range(g)]
+    tb = [_rand(tn, dtype=torch.float32, seed=71 + i) for i in range(g)]
+    out = [torch.empty(B * H * W, tn, device="cuda") for _ in range(g)]
+    C = [torch.empty(B, H, W, Cout, device="cuda", dtype=torch.float16) if store_c else None
+         for _ in range(g)]
+    wk = [w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous() for w in ws]
+    conv = dict(H=H, W=W, C=Cin, k=3, stride=1, pad=1, oH=H, oW=W)
+    ops.gemm(xs, wk, C, B * H * W, Cout, 9 * Cin, lda=0, conv=conv, bias=bs, act="relu",
+             tile=tile, tail=(tw, tb, out, tn, tn))(_lib.stream())
+    for i in range(g):
+        y = F.relu(F.conv2d(xs[i].float().permute(0, 3, 1, 2), ws[i].float(), bs[i], padding=1))
+        ref = y.permute(0, 2, 3, 1).reshape(-1, Cout) @ tw[i].float().T + tb[i]
+        assert rel_err(out[i], ref) < 2e-3, (i, rel_err(out[i], ref))
+        if store_c:
+            assert rel_err(C[i], y.permute(0, 2, 3, 1)) < 2e-3
