@@ -621,13 +621,16 @@ k_gemm(GemmP p) {
 
   // ---- epilogue ----
   if (p.debug & 4) return;
-  if (p.vec_epi) {
-    // row pitch BN + 4 floats where it fits (rows 16 B apart in the banks)
-    constexpr int LDT = BM * (BN + 4) * 4 <= kStages * STAGE * 2 ? BN + 4 : BN;
-    static_assert(BM * LDT * 4 <= kStages * STAGE * 2, "epilogue staging must fit the ring");
-    epilogue_vec<BM, BN, NWM, NWN, FM, FN, LDT, kStages * STAGE * 2>(
-        p, g, m0, n0, acc, reinterpret_cast<float*>(smem));
-    return;
+  // the LDS-staged vector epilogue where the fp32 tile fits the ring
+  constexpr bool kVecFits = BM * BN * 4 <= kStages * STAGE * 2;
+  if constexpr (kVecFits) {
+    if (p.vec_epi) {
+      // row pitch BN + 4 floats where it fits (rows 16 B apart in the banks)
+      constexpr int LDT = BM * (BN + 4) * 4 <= kStages * STAGE * 2 ? BN + 4 : BN;
+      epilogue_vec<BM, BN, NWM, NWN, FM, FN, LDT, kStages * STAGE * 2>(
+          p, g, m0, n0, acc, reinterpret_cast<float*>(smem));
+      return;
+    }
   }
   const int s_idx = blockIdx.y;
   if (p.rope_pos[g]) {
@@ -707,6 +710,8 @@ template <int BM, int BN, int S, int NWM = 2, int NWN = 2, int BK = 64>
 int launch(const GemmP& p, hipStream_t st) {
   S3_REQUIRE(!p.tail_w[0] || p.N == BN,
              "s3n_gemm: the fused tail needs N == the tile width (%d, N = %d)", BN, p.N);
+  S3_REQUIRE(!p.tail_w[0] || BM * BN * 4 <= S * (BM + BN) * BK * 2,
+             "s3n_gemm: the fused tail needs a tile whose fp32 image fits its LDS ring");
   constexpr int NT = 64 * NWM * NWN;
   GemmP q = p;
   q.tiles_m = (p.M + BM - 1) / BM;
@@ -845,6 +850,9 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   if (a->tile == 10) return launch<64, 64, 2, 2, 2, 128>(p, st);
   if (a->tile == 11) return launch<64, 128, 2, 2, 2, 128>(p, st);
   if (a->tile == 12) return launch<128, 128, 2, 2, 2, 128>(p, st);
+  // 256x256 output tiles, 8 waves of 128x64 (half the operand bytes per MFMA
+  // of 128x128; only 2 stages fit, so it wins only on some large shapes)
+  if (a->tile == 14) return launch<256, 256, 2, 2, 4>(p, st);
   // the fused tail needs one column tile per row block
   if (tail) {
     S3_REQUIRE(a->N == 64 || a->N == 128, "s3n_gemm: the fused tail needs N of 64 or 128");

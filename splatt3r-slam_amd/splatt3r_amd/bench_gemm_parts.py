@@ -11,7 +11,7 @@ import torch
 from splatt3r_amd import _lib, ops
 from splatt3r_amd.bench_gemm import timeit
 
-SHAPES = [(768, 1024, 1024), (768, 4096, 1024), (768, 1024, 4096)]
+SHAPES = [(4096, 4096, 4096), (1536, 6400, 7168), (196608, 128, 1152), (12288 * 4, 256, 2304)]
 
 
 def main():
@@ -21,7 +21,7 @@ def main():
         B = torch.randn(N, K, device="cuda").half() * K ** -0.5
         C = torch.empty(M, N, device="cuda", dtype=torch.float16)
         fl = 2 * M * N * K
-        for tile in (1, 10, 2, 3):
+        for tile in (3, 4, 13, 14):
             c = ops.gemm([A], [B], [C], M, N, K, lda=K, split_k=1, tile=tile)
             r = []
             for dbg in (0, 1, 2, 3, 8, 12):

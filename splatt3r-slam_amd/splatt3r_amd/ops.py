@@ -148,7 +148,7 @@ _TUNE_CACHE: dict = {}
 TUNE_LOG = os.environ.get("S3_GEMM_TUNE_LOG", "0") == "1"
 _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128, 128),
                 6: (64, 64), 8: (64, 128), 9: (64, 64), 10: (64, 64), 11: (64, 128),
-                12: (128, 128)}
+                12: (128, 128), 14: (256, 256)}
 
 
 def _tune_key(a):

@@ -43,7 +43,8 @@ def test_gemm_dense_bias_residual(M, N, K, groups):
     (700, 200, 960, 2, 1, 4), (520, 384, 640, 1, 2, 5), (768, 6400, 512, 2, 1, 4),
     (300, 200, 1000, 1, 1, 6), (130, 96, 2000, 2, 1, 7), (600, 256, 200, 1, 1, 8),
     (768, 1024, 1000, 1, 1, 9), (300, 200, 1000, 2, 3, 10), (130, 300, 968, 1, 2, 11),
-    (700, 256, 2304, 2, 1, 12), (64, 64, 136, 1, 1, 9)])
+    (700, 256, 2304, 2, 1, 12), (64, 64, 136, 1, 1, 9), (700, 256, 1000, 2, 2, 14),
+    (520, 300, 640, 1, 1, 14), (300, 500, 1000, 1, 3, 14)])
 def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
     """Split-K partials + ordered reduce + the full epilogue (bias, GELU,
     fp32 residual, fp16 out + fp16 copy) for every tile shape."""
