@@ -275,12 +275,11 @@ class PairPlan:
         P.add(ops.gemm(g2(self.cat), [w.emb_w, w.emb_w], g2(X), M, D, E, lda=ED,
                        bias=[w.emb_b, w.emb_b]))
         for li, blk in enumerate(w.dec):
-            # y_ = norm_y(other branch's previous output), before X changes
-            P.add(ops.layernorm([X[1], X[0]], g2(blk["nyw"]), g2(blk["nyb"]), rows=M, C=D, ldx=D,
-                                eps=cfg.ln_eps, out16=g2(yh), ld16=D))
-            # self attention
-            P.add(ops.layernorm(g2(X), g2(blk["n1w"]), g2(blk["n1b"]), rows=M, C=D, ldx=D,
-                                eps=cfg.ln_eps, out16=g2(h), ld16=D))
+            # y_ = norm_y(other branch's previous output), before X changes, and
+            # norm1(x) for self attention: one 4-group launch (same input state)
+            P.add(ops.layernorm([X[1], X[0], X[0], X[1]],
+                                g2(blk["nyw"]) + g2(blk["n1w"]), g2(blk["nyb"]) + g2(blk["n1b"]),
+                                rows=M, C=D, ldx=D, eps=cfg.ln_eps, out16=g2(yh) + g2(h), ld16=D))
             P.add(ops.gemm(g2(h), g2(blk["qkv_w"]), g2(qkv), M, 3 * D, D, lda=D, bias=g2(blk["qkv_b"]),
                            rope=net.rope, rope_pos=pos, rope_ncols=2 * D))
             P.add(ops.attention(g2(qkv), [qkv[0][:, D:], qkv[1][:, D:]],
