@@ -233,9 +233,15 @@ k_refine_coop(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21
       cidx[t] = ii * side + jj;
       const int64_t u = u0 - rd + (int64_t)ii * d, v = v0 - rd + (int64_t)jj * d;
       ok[t] = live && s < ncand && v >= 0 && v < h && u >= 0 && u < w;
-      const h8* r8 = reinterpret_cast<const h8*>(d11 + (ok[t] ? (v * w + u) * F : 0));
+      // empty slots (past the window, outside the image) issue no loads
+      if (ok[t]) {
+        const h8* r8 = reinterpret_cast<const h8*>(d11 + (v * w + u) * F);
 #pragma unroll
-      for (int cc = 0; cc < NC; ++cc) row[t][cc] = r8[cc];
+        for (int cc = 0; cc < NC; ++cc) row[t][cc] = r8[cc];
+      } else {
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc) row[t][cc] = h8{};
+      }
     }
     float best = -INFINITY;
     int best_c = 1 << 30;
