@@ -60,6 +60,11 @@ def _args():
     ap.add_argument("--pairs-per-rank", type=int, default=4)
     ap.add_argument("--no-kprof", action="store_true",
                     help="skip the per-launch network profile (roofline object)")
+    ap.add_argument("--enc-batch", type=int, default=1,
+                    help="frames per encoder replay (lookahead over the sequence); "
+                         "the timed region then holds steps/enc-batch encoder replays")
+    ap.add_argument("--main-priority", type=int, default=None,
+                    help="HIP stream priority of the frame's main chain (e.g. -1 = high)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="encode each frame inside its own step (no side-stream overlap)")
     return ap.parse_args()
@@ -173,11 +178,15 @@ def main():
     seed = 1234
     model = load_splatt3r(None, device=dev, cfg=FULL, seed=seed, symmetric=True)
     nfr = a.warmup + a.steps + 1
-    # one frame past the last timed one: its encoder is queued (pipelined)
-    # by the last timed step, so the timed region holds exactly K encodes
-    frames = tum_like_sequence(nfr + 1, H, W, seed=rank, step_px=2.0, device=dev)
-    fe = Frontend(model, device=dev, spatial_stride=4, render=True)
-    nxt = (lambda i: None) if a.no_pipeline else (lambda i: frames[i + 1])
+    # kb frames past the last timed one: their encoder is queued (pipelined)
+    # by a timed step, so the timed region holds exactly K image encodes
+    kb = a.enc_batch
+    if a.steps % kb:
+        raise SystemExit(f"--steps {a.steps} must be a multiple of --enc-batch {kb}")
+    frames = tum_like_sequence(nfr + kb, H, W, seed=rank, step_px=2.0, device=dev)
+    fe = Frontend(model, device=dev, spatial_stride=4, render=True, enc_batch=kb,
+                  main_priority=a.main_priority)
+    nxt = (lambda i: None) if a.no_pipeline else (lambda i: [frames[j] for j in range(i + 1, i + 1 + kb)])
 
     for i in range(a.warmup + 1):          # frame 0 = INIT, then W tracked frames
         fe.step(i, frames[i], next_img=nxt(i))
@@ -211,7 +220,8 @@ def main():
         "config": {"workload": "C2 per-frame SLAM tracking, 512x384, config/base.yaml, --no-viz, "
                                "render on, spatial stride 4", "model": "Splatt3R (MASt3RGaussians)",
                    "global_batch": ws, "seq_len": 768,
-                   "parallelism": f"replicas x{ws} (tracker path does not shard)"},
+                   "parallelism": f"replicas x{ws} (tracker path does not shard)",
+                   "encoder_batch": kb},
         "msplats_per_s": P_frame * st["rendered"] * ws / t_max / 1e6,
         "frame_breakdown": {"network_ms": net_ms,
                             "rest_ms": t_max / a.steps * 1e3 - net_ms,

@@ -424,6 +424,79 @@ __device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int 
   }
 }
 
+// Per-register epilogue (scatter stores, unaligned operands, split-K
+// partial planes, RoPE via lane shuffles) of a BM x BN tile of NWM x NWN
+// waves, each holding FM x FN 32x32 accumulators.
+template <int BM, int BN, int NWM, int NWN, int FM, int FN>
+__device__ __forceinline__ void epilogue_regs(const GemmP& p, int g, int m0, int n0,
+                                              f32x16 (&acc)[FM][FN]) {
+  constexpr int WM = BM / NWM, WN = BN / NWN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / NWN, wn = wave % NWN;
+  const int M = p.M, N = p.N;
+  const int s_idx = blockIdx.y;
+  if (p.rope_pos[g]) {
+    // bias, then RoPE: the partner column (col ^ 16, same rows) sits in lane
+    // ^ 16 of the same 32x32 accumulator, so one xor-shuffle fetches it.
+    // Positions, then the cos/sin rows, are loaded for all 16 rows at once.
+    const int64_t* __restrict__ pos = p.rope_pos[g];
+    const float* __restrict__ bias = p.bias[g];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int col = n0 + wn * WN + fn * 32 + (lane & 31);
+        const int row0 = m0 + wm * WM + fm * 32 + 4 * (lane >> 5);
+        const float bv = (bias && col < N) ? bias[col] : 0.0f;
+        const int d = col & 63, j = col & 15;
+        const bool lo = (col & 31) < 16, rot = col < p.rope_ncols;
+        float x[16], xp[16];
+        int64_t ps[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          x[r] = acc[fm][fn][r] + bv;
+          xp[r] = __shfl_xor(x[r], 16, 64);
+          const int row = row0 + acc_row(r);
+          ps[r] = (rot && row < M) ? pos[(int64_t)row * 2 + (d >> 5)] : 0;
+        }
+        if (rot) {
+          float cs[16], sn[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            cs[r] = p.rope_cos[ps[r] * 16 + j];
+            sn[r] = p.rope_sin[ps[r] * 16 + j];
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            x[r] = lo ? x[r] * cs[r] - xp[r] * sn[r] : x[r] * cs[r] + xp[r] * sn[r];
+        }
+        epilogue_block<false>(p, g, row0, col, x);
+      }
+    return;
+  }
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int col = n0 + wn * WN + fn * 32 + (lane & 31);
+      const int row0 = m0 + wm * WM + fm * 32 + 4 * (lane >> 5);
+      if (col >= N) continue;
+      if (p.split_k > 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = row0 + acc_row(r);
+          if (row < M) p.ws[(((int64_t)g * p.split_k + s_idx) * M + row) * N + col] = acc[fm][fn][r];
+        }
+      } else {
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[fm][fn][r];
+        epilogue_block(p, g, row0, col, v);
+      }
+    }
+}
+
 // Waves per SIMD the LDS footprint allows (the register budget the
 // compiler may use without costing occupancy).
 constexpr int lds_waves_per_simd(int BM, int BN, int NW, int S, int BK) {
@@ -632,66 +705,7 @@ k_gemm(GemmP p) {
       return;
     }
   }
-  const int s_idx = blockIdx.y;
-  if (p.rope_pos[g]) {
-    // bias, then RoPE: the partner column (col ^ 16, same rows) sits in lane
-    // ^ 16 of the same 32x32 accumulator, so one xor-shuffle fetches it.
-    // Positions, then the cos/sin rows, are loaded for all 16 rows at once.
-    const int64_t* __restrict__ pos = p.rope_pos[g];
-    const float* __restrict__ bias = p.bias[g];
-#pragma unroll
-    for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        const int col = n0 + wn * WN + fn * 32 + (lane & 31);
-        const int row0 = m0 + wm * WM + fm * 32 + 4 * (lane >> 5);
-        const float bv = (bias && col < N) ? bias[col] : 0.0f;
-        const int d = col & 63, j = col & 15;
-        const bool lo = (col & 31) < 16, rot = col < p.rope_ncols;
-        float x[16], xp[16];
-        int64_t ps[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          x[r] = acc[fm][fn][r] + bv;
-          xp[r] = __shfl_xor(x[r], 16, 64);
-          const int row = row0 + acc_row(r);
-          ps[r] = (rot && row < M) ? pos[(int64_t)row * 2 + (d >> 5)] : 0;
-        }
-        if (rot) {
-          float cs[16], sn[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            cs[r] = p.rope_cos[ps[r] * 16 + j];
-            sn[r] = p.rope_sin[ps[r] * 16 + j];
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            x[r] = lo ? x[r] * cs[r] - xp[r] * sn[r] : x[r] * cs[r] + xp[r] * sn[r];
-        }
-        epilogue_block<false>(p, g, row0, col, x);
-      }
-    return;
-  }
-#pragma unroll
-  for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      const int col = n0 + wn * WN + fn * 32 + (lane & 31);
-      const int row0 = m0 + wm * WM + fm * 32 + 4 * (lane >> 5);
-      if (col >= N) continue;
-      if (p.split_k > 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = row0 + acc_row(r);
-          if (row < M) p.ws[(((int64_t)g * p.split_k + s_idx) * M + row) * N + col] = acc[fm][fn][r];
-        }
-      } else {
-        float v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = acc[fm][fn][r];
-        epilogue_block(p, g, row0, col, v);
-      }
-    }
+  epilogue_regs<BM, BN, NWM, NWN, FM, FN>(p, g, m0, n0, acc);
 }
 
 // Split-K combine: sum the partial planes in split order, then the epilogue.
@@ -738,6 +752,7 @@ int launch(const GemmP& p, hipStream_t st) {
   }
   return S3_OK;
 }
+
 
 }  // namespace
 

@@ -11,17 +11,26 @@ import torch
 from splatt3r_amd import _lib, ops
 from splatt3r_amd.bench_gemm import timeit
 
+import argparse
+
 SHAPES = [(4096, 4096, 4096), (1536, 6400, 7168), (196608, 128, 1152), (12288 * 4, 256, 2304)]
+SMALL = [(768, 1024, 1024), (768, 4096, 1024), (768, 1024, 4096), (768, 3072, 1024),
+         (1536, 768, 768), (1536, 3072, 768), (1536, 768, 3072)]
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--small", action="store_true", help="the 768-row network shapes")
+    ap.add_argument("--tiles", default="3,4,13,14")
+    a = ap.parse_args()
+    tiles = [int(t) for t in a.tiles.split(",")]
     L = _lib.lib()
-    for M, N, K in SHAPES:
+    for M, N, K in (SMALL if a.small else SHAPES):
         A = torch.randn(M, K, device="cuda").half()
         B = torch.randn(N, K, device="cuda").half() * K ** -0.5
         C = torch.empty(M, N, device="cuda", dtype=torch.float16)
         fl = 2 * M * N * K
-        for tile in (3, 4, 13, 14):
+        for tile in tiles:
             c = ops.gemm([A], [B], [C], M, N, K, lda=K, split_k=1, tile=tile)
             r = []
             for dbg in (0, 1, 2, 3, 8, 12):

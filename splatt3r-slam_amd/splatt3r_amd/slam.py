@@ -18,8 +18,11 @@ dataset[i + 1]), the encoder of frame i + 1 is queued on a side HIP stream
 before frame i's decoder, matching, GN and render are queued on the main
 stream, so the two chains share the chip (the 768-token GEMMs fill only a
 part of the 256 CUs) and the encoder also fills the host-sync gaps of the
-tracker.  Every frame is still encoded exactly once, from its own image;
-the outputs are identical.
+tracker.  With a lookahead list (`next_img=[img_{i+1}, img_{i+2}, ...]`)
+and `enc_batch=k`, frames i+1..i+k are encoded as one image batch when
+frame i+1 is not queued yet (dataset playback; a live camera uses k = 1):
+the encoder is per-image (no op mixes images), so every frame is still
+encoded exactly once from its own image, with M = 768k-row GEMMs.
 """
 from __future__ import annotations
 
@@ -49,7 +52,7 @@ def should_append_gaussians(add_new_kf, frame_idx, current_T_WC, last_append_T_W
 class Frontend:
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
-                 readback=True):
+                 readback=True, enc_batch=1, main_priority=None):
         self.model = model
         self.device = device
         self.K = K
@@ -71,31 +74,45 @@ class Frontend:
         self.last_render = None
         self.fps_timer = None
         self.enc_stream = torch.cuda.Stream(device=device) if torch.cuda.is_available() else None
-        self._next = None          # (frame index, Frame whose encoder is queued, done event)
+        self._queue = {}           # frame index -> (Frame whose encoder is queued, done event)
+        self.enc_batch = enc_batch # images per encoder replay when lookahead frames are given
+        self.spans = None          # list -> per-frame GPU events (encoder, main chain)
+        # main chain on a stream of its own priority (the encoder side stream
+        # keeps the default one): the dispatcher then prefers the frame's
+        # critical path and the encoder fills the CUs it leaves idle
+        self.main_stream = (torch.cuda.Stream(device=device, priority=main_priority)
+                            if main_priority is not None and self.enc_stream is not None else None)
 
-    def _prefetch(self, i, img):
-        """Create frame i and queue its encoder on the side stream."""
+    def _prefetch(self, i, imgs):
+        """Create frames i, i+1, ... for `imgs` and queue their encoder on
+        the side stream as one image batch (one plan replay: the ViT-L
+        GEMMs at M = 768 * len(imgs) fill the chip better than one image)."""
         main = torch.cuda.current_stream(self.device)
-        frame = create_frame(i, img, None, device=self.device)
+        frames = [create_frame(i + j, im, None, device=self.device) for j, im in enumerate(imgs)]
         ready = torch.cuda.Event()
         ready.record(main)                       # the image upload / producer
         with torch.cuda.stream(self.enc_stream):
             self.enc_stream.wait_event(ready)
-            frame.feat, frame.pos, _ = self.model.encoder._encode_image(frame.img,
-                                                                         frame.img_true_shape)
-            done = torch.cuda.Event()
+            e0 = self._event()
+            img = (frames[0].img if len(frames) == 1
+                   else torch.cat([f.img for f in frames], 0))
+            feat, pos, _ = self.model.encoder._encode_image(img, frames[0].img_true_shape)
+            done = torch.cuda.Event(enable_timing=self.spans is not None)
             done.record(self.enc_stream)
+        if self.spans is not None:
+            self.spans.append(("enc", i, e0, done))
         # allocated on the side stream, read on the main one
-        frame.feat.record_stream(main)
-        frame.pos.record_stream(main)
-        frame.img.record_stream(self.enc_stream)
-        self._next = (i, frame, done)
+        feat.record_stream(main)
+        pos.record_stream(main)
+        for j, f in enumerate(frames):
+            f.feat, f.pos = feat[j:j + 1], pos[j:j + 1]
+            f.img.record_stream(self.enc_stream)
+            self._queue[i + j] = (f, done)
 
     def _take_prefetched(self, i, T_WC):
-        if self._next is None or self._next[0] != i:
+        if i not in self._queue:
             return None
-        _, frame, done = self._next
-        self._next = None
+        frame, done = self._queue.pop(i)
         torch.cuda.current_stream(self.device).wait_event(done)
         frame.T_WC = T_WC
         return frame
@@ -116,7 +133,32 @@ class Frontend:
             self.stats["gaussians_world"] += int(gs[0].shape[0])
         return gs
 
+    def _event(self):
+        if self.spans is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
     def step(self, i: int, img, next_img=None) -> Frame:
+        if self.main_stream is not None:
+            caller = torch.cuda.current_stream(self.device)
+            self.main_stream.wait_stream(caller)
+            with torch.cuda.stream(self.main_stream):
+                frame = self._step_timed(i, img, next_img)
+            caller.wait_stream(self.main_stream)
+            return frame
+        return self._step_timed(i, img, next_img)
+
+    def _step_timed(self, i, img, next_img):
+        if self.spans is None:
+            return self._step(i, img, next_img)
+        e0 = [None]
+        frame = self._step(i, img, next_img, e0)
+        self.spans.append(("main", i, e0[0], self._event()))
+        return frame
+
+    def _step(self, i: int, img, next_img=None, e0=None) -> Frame:
         if self.fps_timer is None:
             self.fps_timer = time.time()
         T_WC = (lietorch.Sim3.Identity(1, device=self.device) if self.last_T_WC is None
@@ -125,12 +167,17 @@ class Frontend:
         if frame is None and self.enc_stream is not None:
             # every encode goes through the side stream (one encoder plan,
             # one stream: no two replays of its buffers can overlap)
-            self._prefetch(i, img)
+            self._prefetch(i, [img])
             frame = self._take_prefetched(i, T_WC)
         if frame is None:
             frame = create_frame(i, img, T_WC, device=self.device)
-        if next_img is not None and self.enc_stream is not None:
-            self._prefetch(i + 1, next_img)
+        if next_img is not None and self.enc_stream is not None and (i + 1) not in self._queue:
+            # next_img: the next frame's image, or a list of the next frames'
+            # images (lookahead); up to enc_batch of them are encoded together
+            nxt = list(next_img) if isinstance(next_img, (list, tuple)) else [next_img]
+            self._prefetch(i + 1, nxt[:max(1, self.enc_batch)])
+        if e0 is not None:
+            e0[0] = self._event()
         self.stats["frames"] += 1
         add_new_kf = False
         if self.mode == Mode.INIT:
