@@ -1,8 +1,9 @@
 // Tile-binned Gaussian splat rasterizer (include/gsr.h), written for gfx950.
 //
 // Forward:  preprocess (1 lane / Gaussian) -> inclusive scan of tiles touched
-//           -> duplicate (tile<<32 | depth) keys -> radix sort (stable)
-//           -> tile ranges -> blend (one 256-lane workgroup per 16x16 tile,
+//           -> stable depth sort of the P Gaussians (32-bit keys) -> duplicate
+//           in depth order -> stable sort of the instances by tile id alone
+//           (tile_bits passes, 32-bit keys) -> tile ranges -> blend (one 256-lane workgroup per 16x16 tile,
 //           Gaussians staged through LDS in 256-record batches, block-wide
 //           early exit).
 // Backward: per-tile back-to-front replay; per-Gaussian gradients are
@@ -48,12 +49,28 @@ struct GeomState {
   uint32_t* offsets;
   void* scan_tmp;
   size_t scan_bytes;
+  // depth-ordered duplication (gsr_render)
+  uint32_t* dkey;          // depth bits (visible) / ~0u, index order
+  uint32_t* dkey_sorted;
+  uint32_t* iota;
+  uint32_t* order;         // Gaussian index per depth rank (stable)
+  uint32_t* tiles_sorted;  // tiles touched per depth rank
+  uint32_t* offsets_sorted;
+  void* dsort_tmp;
+  size_t dsort_bytes;
 };
 
 size_t scan_temp_bytes(int64_t P) {
   size_t bytes = 0;
   hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                    (int)P);
+  return bytes;
+}
+
+size_t key32_sort_temp_bytes(int64_t n) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                     (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
   return bytes;
 }
 
@@ -70,6 +87,14 @@ GeomState carve_geom(void* base, int64_t P) {
   g.offsets = c.take<uint32_t>(P);
   g.scan_bytes = scan_temp_bytes(P);
   g.scan_tmp = c.take<char>(g.scan_bytes);
+  g.dkey = c.take<uint32_t>(P);
+  g.dkey_sorted = c.take<uint32_t>(P);
+  g.iota = c.take<uint32_t>(P);
+  g.order = c.take<uint32_t>(P);
+  g.tiles_sorted = c.take<uint32_t>(P);
+  g.offsets_sorted = c.take<uint32_t>(P);
+  g.dsort_bytes = key32_sort_temp_bytes(P);
+  g.dsort_tmp = c.take<char>(g.dsort_bytes);
   return g;
 }
 size_t geom_bytes(int64_t P) {
@@ -77,30 +102,27 @@ size_t geom_bytes(int64_t P) {
   c.take<float>(P); c.take<float4>(P); c.take<float4>(P); c.take<float>(P * 3);
   c.take<float>(P * 6); c.take<uint8_t>(P * 3); c.take<uint32_t>(P); c.take<uint32_t>(P);
   c.take<char>(scan_temp_bytes(P));
+  for (int k = 0; k < 6; ++k) c.take<uint32_t>(P);
+  c.take<char>(key32_sort_temp_bytes(P));
   return c.off;
 }
 
 struct BinningState {
-  uint64_t* keys_unsorted;
-  uint64_t* keys;
+  uint32_t* keys_unsorted;   // tile id per instance (depth order)
+  uint32_t* keys;
   uint32_t* vals_unsorted;
   uint32_t* vals;  // point_list: Gaussian index per sorted instance
   void* sort_tmp;
   size_t sort_bytes;
 };
 
-size_t sort_temp_bytes(int64_t R) {
-  size_t bytes = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                                     (uint32_t*)nullptr, (uint32_t*)nullptr, (int)R);
-  return bytes;
-}
+size_t sort_temp_bytes(int64_t R) { return key32_sort_temp_bytes(R); }
 
 BinningState carve_binning(void* base, int64_t R) {
   Carver c{static_cast<char*>(base)};
   BinningState b;
-  b.keys_unsorted = c.take<uint64_t>(R);
-  b.keys = c.take<uint64_t>(R);
+  b.keys_unsorted = c.take<uint32_t>(R);
+  b.keys = c.take<uint32_t>(R);
   b.vals_unsorted = c.take<uint32_t>(R);
   b.vals = c.take<uint32_t>(R);
   b.sort_bytes = sort_temp_bytes(R);
@@ -109,7 +131,7 @@ BinningState carve_binning(void* base, int64_t R) {
 }
 size_t binning_bytes(int64_t R) {
   Carver c{nullptr};
-  c.take<uint64_t>(R); c.take<uint64_t>(R); c.take<uint32_t>(R); c.take<uint32_t>(R);
+  c.take<uint32_t>(R); c.take<uint32_t>(R); c.take<uint32_t>(R); c.take<uint32_t>(R);
   c.take<char>(sort_temp_bytes(R));
   return c.off;
 }
@@ -229,33 +251,55 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
 }
 
 // ------------------------------------------------------------- binning ----
+// Depth keys for the stable depth sort: positive depth bits order like the
+// floats; Gaussians that touch no tile sort last (they emit nothing).
+__global__ void __launch_bounds__(kThreads)
+k_depth_keys(int64_t P, GeomState g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  g.dkey[i] = g.tiles[i] > 0 ? __float_as_uint(g.depth[i]) : 0xFFFFFFFFu;
+  g.iota[i] = (uint32_t)i;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_gather_tiles(int64_t P, GeomState g) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < P) g.tiles_sorted[k] = g.tiles[g.order[k]];
+}
+
+// One lane per depth rank k: the instances of Gaussian order[k], one per
+// touched tile, written at its depth-ordered offset.  A stable sort by tile
+// id then yields the reference's (tile, depth, index) order
+// (rasterizer_impl.cu duplicateWithKeys + SortPairs over tile<<32 | depth):
+// equal depths keep index order from the stable depth sort.
 __global__ void __launch_bounds__(kThreads)
 k_duplicate(int64_t P, int gx, int gy, const int32_t* __restrict__ radii, GeomState g,
-            uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P || radii[i] <= 0) return;
-  uint32_t off = i == 0 ? 0u : g.offsets[i - 1];
+            uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= P) return;
+  const uint32_t i = g.order[k];
+  if (radii[i] <= 0) return;
+  uint32_t off = k == 0 ? 0u : g.offsets_sorted[k - 1];
   const float4 r0 = g.rec0[i];
   int x0, y0, x1, y1;
   get_rect(r0.x, r0.y, radii[i], gx, gy, &x0, &y0, &x1, &y1);
-  const uint64_t dbits = (uint64_t)__float_as_uint(g.depth[i]);
   for (int y = y0; y < y1; ++y)
     for (int x = x0; x < x1; ++x) {
-      keys[off] = ((uint64_t)(y * gx + x) << 32) | dbits;
-      vals[off] = (uint32_t)i;
+      keys[off] = (uint32_t)(y * gx + x);
+      vals[off] = i;
       ++off;
     }
 }
 
 __global__ void __launch_bounds__(kThreads)
-k_ranges(int64_t R, const uint64_t* __restrict__ keys, uint2* __restrict__ ranges) {
+k_ranges(int64_t R, const uint32_t* __restrict__ keys, uint2* __restrict__ ranges) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R) return;
-  const uint32_t cur = (uint32_t)(keys[i] >> 32);
+  const uint32_t cur = keys[i];
   if (i == 0) {
     ranges[cur].x = 0;
   } else {
-    const uint32_t prev = (uint32_t)(keys[i - 1] >> 32);
+    const uint32_t prev = keys[i - 1];
     if (cur != prev) {
       ranges[prev].y = (uint32_t)i;
       ranges[cur].x = (uint32_t)i;
@@ -711,13 +755,24 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
   tmark(3, st);
   S3_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * ntiles, st));
   if (R > 0) {
-    k_duplicate<<<(unsigned)s3::cdiv(P, kThreads), kThreads, 0, st>>>(
-        P, gx, gy, radii, g, b.keys_unsorted, b.vals_unsorted);
+    const unsigned pb = (unsigned)s3::cdiv(P, kThreads);
+    k_depth_keys<<<pb, kThreads, 0, st>>>(P, g);
+    S3_LAUNCH_CHECK();
+    size_t db = g.dsort_bytes;
+    S3_HIP(hipcub::DeviceRadixSort::SortPairs(g.dsort_tmp, db, g.dkey, g.dkey_sorted, g.iota,
+                                              g.order, (int)P, 0, 32, st));
+    k_gather_tiles<<<pb, kThreads, 0, st>>>(P, g);
+    S3_LAUNCH_CHECK();
+    size_t sb = g.scan_bytes;
+    S3_HIP(hipcub::DeviceScan::InclusiveSum(g.scan_tmp, sb, g.tiles_sorted, g.offsets_sorted,
+                                            (int)P, st));
+    k_duplicate<<<pb, kThreads, 0, st>>>(P, gx, gy, radii, g, b.keys_unsorted,
+                                         b.vals_unsorted);
     S3_LAUNCH_CHECK();
     size_t tb = b.sort_bytes;
     S3_HIP(hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, tb, b.keys_unsorted, b.keys,
                                               b.vals_unsorted, b.vals, (int)R, 0,
-                                              32 + tile_bits(ntiles), st));
+                                              tile_bits(ntiles), st));
   }
   tmark(4, st);
   if (R > 0) {
