@@ -382,6 +382,36 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Transposed wave reduction of 8 values: each halving step keeps half of
+// the values and trades the other half with the partner lane, so 8 sums
+// cost 4 + 2 + 1 + 3 shuffles instead of 8 x 6.  Lane l ends with the full
+// sum of value ((l >> 5) & 1) * 4 + ((l >> 4) & 1) * 2 + ((l >> 3) & 1).
+__device__ __forceinline__ float wave_sum8_t(const float (&v)[8], int lane) {
+  float w[4], x[2];
+  const bool b32 = lane & 32, b16 = lane & 16, b8 = lane & 8;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float send = b32 ? v[k] : v[k + 4];
+    const float keep = b32 ? v[k + 4] : v[k];
+    w[k] = keep + __shfl_xor(send, 32, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float send = b16 ? w[k] : w[k + 2];
+    const float keep = b16 ? w[k + 2] : w[k];
+    x[k] = keep + __shfl_xor(send, 16, 64);
+  }
+  float y = (b8 ? x[1] : x[0]) + __shfl_xor(b8 ? x[0] : x[1], 8, 64);
+  y += __shfl_xor(y, 4, 64);
+  y += __shfl_xor(y, 2, 64);
+  y += __shfl_xor(y, 1, 64);
+  return y;
+}
+
+// Gradient slots per Gaussian in the LDS batch accumulator: mean2D x/y,
+// conic x/y/w, opacity, colour r/g/b.
+constexpr int kGS = 9;
+
 __global__ void __launch_bounds__(BS)
 k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
                  const uint32_t* __restrict__ point_list, GeomState g,
@@ -393,6 +423,11 @@ k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ran
   __shared__ float4 s_r1[BS];
   __shared__ float s_b[BS];
   __shared__ uint32_t s_id[BS];
+  // per-batch block sums: the 4 waves' reduced gradients meet in LDS and
+  // each (Gaussian, tile) pair issues its 9 global atomics once, from the
+  // lane that owns the Gaussian, instead of once per wave from lane 0
+  __shared__ float s_acc[BS * kGS];
+  __shared__ int s_hit[BS];
   const int tile = xcd_tile(blockIdx.x, ntiles);
   const int tx = tile % gx, ty = tile / gx;
   const int lx = threadIdx.x % BX, ly = threadIdx.x / BX;
@@ -400,13 +435,28 @@ k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ran
   const bool inside = px < W && py < H;
   const int pid = py * W + px;
   const float pxf = (float)px, pyf = (float)py;
+  __shared__ uint32_t s_maxlc;
   const uint2 range = ranges[tile];
-  const int todo_total = (int)(range.y - range.x);
+  const uint32_t last_contributor = inside ? n_contrib[pid] : 0;
+  // Entries at or past every pixel's last contributor (the forward pass
+  // stopped before them) contribute nothing: the replay starts at the
+  // tile's largest n_contrib instead of the back of the list.
+  const int lane = threadIdx.x & 63;
+  {
+    uint32_t m = last_contributor;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    if (threadIdx.x == 0) s_maxlc = 0;
+    __syncthreads();
+    if (lane == 0) atomicMax(&s_maxlc, m);
+    __syncthreads();
+  }
+  const int todo_total = (int)min(range.y - range.x, s_maxlc);
+  const uint32_t end = range.x + (uint32_t)todo_total;
   const int rounds = (todo_total + BS - 1) / BS;
   const float T_final = inside ? final_Ts[pid] : 0.0f;
   float T = T_final;
   uint32_t contributor = (uint32_t)todo_total;
-  const uint32_t last_contributor = inside ? n_contrib[pid] : 0;
   float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
   if (inside) {
     dpix0 = dL_dpix[pid];
@@ -417,19 +467,41 @@ k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ran
   float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
   float last_alpha = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
-  const int lane = threadIdx.x & 63;
+  const int vslot = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
   int todo = todo_total;
+  auto flush = [&](int n) {
+    // one lane per Gaussian of the finished batch
+    const int t = threadIdx.x;
+    if (t < n && s_hit[t]) {
+      const uint32_t id = s_id[t];
+      const float* a = s_acc + t * kGS;
+      atomicAdd(&dL_dmean2D[id * 3 + 0], a[0]);
+      atomicAdd(&dL_dmean2D[id * 3 + 1], a[1]);
+      atomicAdd(&dL_dconic[id * 4 + 0], a[2]);
+      atomicAdd(&dL_dconic[id * 4 + 1], a[3]);
+      atomicAdd(&dL_dconic[id * 4 + 3], a[4]);
+      atomicAdd(&dL_dopacity[id], a[5]);
+      atomicAdd(&dL_dcolors[id * 3 + 0], a[6]);
+      atomicAdd(&dL_dcolors[id * 3 + 1], a[7]);
+      atomicAdd(&dL_dcolors[id * 3 + 2], a[8]);
+    }
+  };
   for (int rd = 0; rd < rounds; ++rd, todo -= BS) {
+    __syncthreads();
+    if (rd > 0) flush(BS);
     __syncthreads();
     const int prog = rd * BS + threadIdx.x;
     if (prog < todo_total) {
-      const uint32_t id = point_list[range.y - prog - 1];
+      const uint32_t id = point_list[end - prog - 1];
       const float4 r1 = g.rec1[id];
       s_id[threadIdx.x] = id;
       s_r0[threadIdx.x] = g.rec0[id];
       s_r1[threadIdx.x] = make_float4(r1.x, r1.y, g.rgb[id * 3 + 0], g.rgb[id * 3 + 1]);
       s_b[threadIdx.x] = g.rgb[id * 3 + 2];
     }
+#pragma unroll
+    for (int k = 0; k < kGS; ++k) s_acc[threadIdx.x * kGS + k] = 0.f;
+    s_hit[threadIdx.x] = 0;
     __syncthreads();
     const int n = todo < BS ? todo : BS;
     for (int j = 0; j < n; ++j) {
@@ -444,8 +516,8 @@ k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ran
       const float alpha = fminf(0.99f, b.y * G);
       ok = ok && !(alpha < 1.0f / 255.0f);
       if (!__any(ok)) continue;
-      float gm_x = 0.f, gm_y = 0.f, gc_x = 0.f, gc_y = 0.f, gc_w = 0.f, go = 0.f;
-      float gr = 0.f, gg = 0.f, gb = 0.f;
+      float gv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      float gb = 0.f;
       if (ok) {
         T = T / (1.0f - alpha);
         const float dchannel_dcolor = alpha * T;
@@ -455,8 +527,8 @@ k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ran
         acc2 = last_alpha * lc2 + (1.0f - last_alpha) * acc2;
         lc0 = c0; lc1 = c1; lc2 = c2;
         float dL_dalpha = (c0 - acc0) * dpix0 + (c1 - acc1) * dpix1 + (c2 - acc2) * dpix2;
-        gr = dchannel_dcolor * dpix0;
-        gg = dchannel_dcolor * dpix1;
+        gv[6] = dchannel_dcolor * dpix0;
+        gv[7] = dchannel_dcolor * dpix1;
         gb = dchannel_dcolor * dpix2;
         dL_dalpha = dL_dalpha * T;
         last_alpha = alpha;
@@ -465,31 +537,24 @@ k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ran
         const float gdx = G * dx, gdy = G * dy;
         const float dG_ddelx = -gdx * a.z - gdy * a.w;
         const float dG_ddely = -gdy * b.x - gdx * a.w;
-        gm_x = dL_dG * dG_ddelx * ddelx_dx;
-        gm_y = dL_dG * dG_ddely * ddely_dy;
-        gc_x = -0.5f * gdx * dx * dL_dG;
-        gc_y = -0.5f * gdx * dy * dL_dG;
-        gc_w = -0.5f * gdy * dy * dL_dG;
-        go = G * dL_dalpha;
+        gv[0] = dL_dG * dG_ddelx * ddelx_dx;
+        gv[1] = dL_dG * dG_ddely * ddely_dy;
+        gv[2] = -0.5f * gdx * dx * dL_dG;
+        gv[3] = -0.5f * gdx * dy * dL_dG;
+        gv[4] = -0.5f * gdy * dy * dL_dG;
+        gv[5] = G * dL_dalpha;
       }
-      gm_x = wave_sum(gm_x); gm_y = wave_sum(gm_y);
-      gc_x = wave_sum(gc_x); gc_y = wave_sum(gc_y); gc_w = wave_sum(gc_w);
-      go = wave_sum(go);
-      gr = wave_sum(gr); gg = wave_sum(gg); gb = wave_sum(gb);
+      const float r8 = wave_sum8_t(gv, lane);
+      gb = wave_sum(gb);
+      if ((lane & 7) == 0) atomicAdd(&s_acc[j * kGS + vslot], r8);
       if (lane == 0) {
-        const uint32_t id = s_id[j];
-        atomicAdd(&dL_dmean2D[id * 3 + 0], gm_x);
-        atomicAdd(&dL_dmean2D[id * 3 + 1], gm_y);
-        atomicAdd(&dL_dconic[id * 4 + 0], gc_x);
-        atomicAdd(&dL_dconic[id * 4 + 1], gc_y);
-        atomicAdd(&dL_dconic[id * 4 + 3], gc_w);
-        atomicAdd(&dL_dopacity[id], go);
-        atomicAdd(&dL_dcolors[id * 3 + 0], gr);
-        atomicAdd(&dL_dcolors[id * 3 + 1], gg);
-        atomicAdd(&dL_dcolors[id * 3 + 2], gb);
+        atomicAdd(&s_acc[j * kGS + 8], gb);
+        s_hit[j] = 1;
       }
     }
   }
+  __syncthreads();
+  if (rounds > 0) flush(todo_total - (rounds - 1) * BS);
 }
 
 // Per-Gaussian chain rule: conic -> 2-D cov -> (3-D cov, view mean) and
