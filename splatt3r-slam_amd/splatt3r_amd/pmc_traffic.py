@@ -1,0 +1,134 @@
+"""HBM traffic of the network kernels from rocprofv3 PMC counters.
+
+Two steps (gpurun_traffic.sh runs both):
+
+  rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d D1 -- \\
+      python3 -m splatt3r_amd.pmc_traffic run
+  rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d D2 -- \\
+      python3 -m splatt3r_amd.pmc_traffic run
+  python -m splatt3r_amd.pmc_traffic summarize D1 D2 --out traffic.json
+
+`run` builds the full-size network plans (512x384, the bench's model),
+warms them, then replays one frame's network (encoder plan + pair plan)
+`--reps` times eagerly, each replay bracketed by a GPU sleep (`spin`)
+kernel so the summary can cut the dispatch stream into frames.
+
+`summarize` applies the gfx950 corrections of
+/opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE reports
+half the bytes of wide coalesced reads -> x2; WRITE_SIZE is exact for
+16-B/lane stores.  FETCH_SIZE/WRITE_SIZE are in KiB.  Output: per kernel
+family, HBM bytes per frame and per launch (mean over the replays).
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+from collections import defaultdict
+
+
+def _family(name: str) -> str:
+    m = re.search(r"k_gemm<(\d+), (\d+), \d+, \d+, (\d+),", name)
+    if m:
+        return "gemm_dense" if m.group(3) == "0" else "gemm_conv"
+    m = re.search(r"\b(k_\w+)", name)
+    return m.group(1) if m else name[:40]
+
+
+def run(reps: int) -> None:
+    import torch
+    from splatt3r_amd import weights as W
+    from splatt3r_amd.net import Splatt3RNet
+    H, Wd = 384, 512
+    net = Splatt3RNet(W.FULL, seed=1234, graphs=False)
+    img = torch.rand(1, 3, H, Wd, device="cuda") * 2 - 1
+    f, p, _ = net._encode_image(img)
+    net.infer_pair(f, p, f, p, (H, Wd))
+    torch.cuda.synchronize()
+    for plan in net.plans():
+        plan.run()
+    torch.cuda.synchronize()
+    for _ in range(reps):
+        torch.cuda._sleep(1000)
+        for plan in net.plans():
+            plan.run()
+    torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
+    print("pmc_traffic run: done", reps, "frames")
+
+
+def _load(d: str, counter: str):
+    paths = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not paths:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    disp = {}
+    for path in paths:
+        with open(path) as fh:
+            for r in csv.DictReader(fh):
+                if r["Counter_Name"] != counter:
+                    continue
+                key = int(r["Dispatch_Id"])
+                v = disp.setdefault(key, [r["Kernel_Name"], 0.0])
+                v[1] += float(r["Counter_Value"])
+    return [disp[k] for k in sorted(disp)]
+
+
+def _frames(rows, reps: int, marker: str):
+    idx = [i for i, (n, _) in enumerate(rows) if re.search(marker, n)]
+    if len(idx) < reps + 1:
+        names = sorted({n for n, _ in rows})
+        raise SystemExit(f"found {len(idx)} marker dispatches; kernel names: {names[:60]}")
+    idx = idx[-(reps + 1):]
+    return [rows[a + 1:b] for a, b in zip(idx[:-1], idx[1:])]
+
+
+def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str):
+    out = {}
+    for counter, d, scale in (("FETCH_SIZE", fetch_dir, 2.0), ("WRITE_SIZE", write_dir, 1.0)):
+        frames = _frames(_load(d, counter), reps, marker)
+        agg = defaultdict(lambda: [0, 0.0])
+        for fr in frames:
+            for name, kib in fr:
+                a = agg[_family(name)]
+                a[0] += 1
+                a[1] += kib * 1024.0 * scale
+        for fam, (n, b) in agg.items():
+            o = out.setdefault(fam, {"launches_per_frame": n // reps})
+            o[("read" if counter == "FETCH_SIZE" else "write") + "_bytes_per_frame"] = b / reps
+    for o in out.values():
+        o["bytes_per_frame"] = o.get("read_bytes_per_frame", 0.0) + o.get("write_bytes_per_frame", 0.0)
+        o["bytes_per_launch"] = o["bytes_per_frame"] / max(1, o["launches_per_frame"])
+    return {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                      "FETCH_SIZE x2 (gfx950 correction), KiB -> bytes",
+            "workload": "one 512x384 frame of the network (encoder + decoder + 2 heads), eager",
+            "frames": reps, "families": dict(sorted(out.items(), key=lambda kv: -kv[1]["bytes_per_frame"]))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    r = sub.add_parser("run")
+    r.add_argument("--reps", type=int, default=3)
+    s = sub.add_parser("summarize")
+    s.add_argument("fetch_dir")
+    s.add_argument("write_dir")
+    s.add_argument("--reps", type=int, default=3)
+    s.add_argument("--marker", default=r"spin|sleep")
+    s.add_argument("--out", default=None)
+    a = ap.parse_args()
+    if a.cmd == "run":
+        run(a.reps)
+        return
+    res = summarize(a.fetch_dir, a.write_dir, a.reps, a.marker)
+    txt = json.dumps(res, indent=1)
+    if a.out:
+        with open(a.out, "w") as fh:
+            fh.write(txt + "\n")
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()
