@@ -111,6 +111,28 @@ def _kernel_profile(net, reps=3):
     return {k: [v[0] // reps, v[1] / reps, v[2] / reps] for k, v in agg.items()}
 
 
+def _pmc_traffic(kind: str):
+    """HBM bytes per launch of the roofline kernel family, from the newest
+    committed PMC summary (profiles/*_pmc_traffic.json, written by
+    gpurun_traffic.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes over one-frame replays, FETCH_SIZE x2 per the gfx950 note).
+    PMC counters cannot be read inside a timed run, so this is the
+    counter pass of the same kernels, named by file."""
+    import glob
+    fam = {"gemm.dense": "gemm_dense", "gemm.conv": "gemm_conv"}.get(kind)
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
+    if not fam or not paths:
+        return None
+    with open(paths[-1]) as fh:
+        d = json.load(fh)["families"].get(fam)
+    if not d:
+        return None
+    return {"bytes_per_launch": d["bytes_per_launch"], "bytes_per_frame": d["bytes_per_frame"],
+            "read_bytes_per_frame": d["read_bytes_per_frame"],
+            "write_bytes_per_frame": d["write_bytes_per_frame"],
+            "source": os.path.relpath(paths[-1], REPO)}
+
+
 def cpu_baseline(model_cfg, seed, frames, n_frames):
     """The CPU restatement (oracle/, `port`) of one tracked frame: torch-CPU
     network forward (oracle/net_ref.py) + C matching + C rasterizer on its
@@ -236,12 +258,16 @@ def main():
         dom = max((k for k in prof if prof[k][1] > 0), key=lambda k: prof[k][2])
         n_l, fl, ms = prof[dom]
         achieved = fl / (ms * 1e-3) / 1e12
+        tr = _pmc_traffic(dom)
         result["roofline"] = {
             "bound": "mfma", "kernel": f"s3n {dom} (all launches of one frame)",
             "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / PEAK_F16_TFLOPS, "traffic": None,
+            "frac": achieved / PEAK_F16_TFLOPS,
+            "traffic": tr["bytes_per_launch"] if tr else None,
             "launches_per_frame": n_l, "avg_launch_us": ms / n_l * 1e3,
             "algorithmic_gflop_per_frame": fl / 1e9}
+        if tr:
+            result["roofline"]["traffic_detail"] = tr
         result["network"] = {"kernels": {k: {"launches": v[0], "gflop": v[1] / 1e9, "ms": v[2]}
                                          for k, v in sorted(prof.items(), key=lambda x: -x[1][2])},
                              "tflops_in_kernels": net_tflops,
