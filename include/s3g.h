@@ -48,6 +48,31 @@ int s3g_gauss_newton_rays(float* Twc, int n_poses, const float* Xs, const float*
                           int max_iter, float delta_thresh, int num_fix, void* workspace,
                           float* dx, float* stats, void* stream);
 
+/* Calibrated variant (replaces mast3r_slam_backends.gauss_newton_calib:
+ * gn.cpp:54-80 -> gn_kernels.cu:1545-1637 gauss_newton_calib_cuda,
+ * calib_proj_kernel :1230-1542; caller global_opt.py:160-215
+ * FactorGraph.solve_GN_calib).  Residuals per correspondence: projected
+ * pixel (u, v) of T_ij X_j under K minus the matched pixel (idx % width,
+ * idx / width), and log z_j - log z_i; valid only inside pixel_border and
+ * with both depths > z_eps.  K: DEVICE pointer to the 3x3 row-major
+ * intrinsics (the reference reads K[0][0], K[1][1], K[0][2], K[1][2] on the
+ * device).  n_points must equal height * width.  Same workspace
+ * (s3g_workspace_bytes), outputs and stop rule as the rays solve. */
+int s3g_calib_system(const float* Twc, int n_poses, const float* Xs, const float* Cs,
+                     int64_t n_points, const float* K, const int32_t* ii, const int32_t* jj,
+                     int n_edges, const int64_t* idx_ii2jj, const uint8_t* valid_match,
+                     const float* Q, int height, int width, int pixel_border, float z_eps,
+                     float sigma_pixel, float sigma_depth, float C_thresh, float Q_thresh,
+                     int num_fix, void* workspace, double* H, double* b, void* stream);
+
+int s3g_gauss_newton_calib(float* Twc, int n_poses, const float* Xs, const float* Cs,
+                           int64_t n_points, const float* K, const int32_t* ii, const int32_t* jj,
+                           int n_edges, const int64_t* idx_ii2jj, const uint8_t* valid_match,
+                           const float* Q, int height, int width, int pixel_border, float z_eps,
+                           float sigma_pixel, float sigma_depth, float C_thresh, float Q_thresh,
+                           int max_iter, float delta_thresh, int num_fix, void* workspace,
+                           float* dx, float* stats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,7 @@
-// Backend pose-graph Gauss-Newton on rays (include/s3g.h), restating
-// splatt3r_slam/backend/src/gn_kernels.cu:812-1227 (ray_align_kernel +
-// gauss_newton_rays_cuda) MI355X-first:
+// Backend pose-graph Gauss-Newton on rays and on calibrated pixel/log-depth
+// residuals (include/s3g.h), restating splatt3r_slam/backend/src/
+// gn_kernels.cu:812-1227 (ray_align_kernel + gauss_newton_rays_cuda) and
+// :1230-1637 (calib_proj_kernel + gauss_newton_calib_cuda) MI355X-first:
 //  * an edge's h*w correspondences are split over many workgroups (the
 //    reference runs ONE 256-thread block per edge, i.e. a handful of CUs);
 //  * the 14-dof Jacobian of an edge is [-Jj, Jj] (ray_align_kernel sets
@@ -55,6 +56,8 @@ __device__ __forceinline__ void adj_inv(const float* T, const float* X, float* Y
   Y[6] = X[6] + s_inv * (t[0] * Ra[0] + t[1] * Ra[1] + t[2] * Ra[2]);
 }
 
+enum { kRays = 0, kCalib = 1 };
+
 struct EdgeP {
   const float* Twc;
   const float* Xs;
@@ -68,10 +71,33 @@ struct EdgeP {
   float inv_sr, inv_sd, C_thresh, Q_thresh;
   float* partial;   // [E, S, NA]
   const double* state;
+  // calib (calib_proj_kernel): K [3,3] row-major on the device, image size,
+  // border and depth floor; inv_sr / inv_sd are then 1/sigma_pixel, 1/sigma_depth
+  const float* K;
+  int height, width, pixel_border;
+  float z_eps;
 };
 
-// grid (S, E): slice s of edge e.
-__global__ void __launch_bounds__(kThreads) k_ray_align(EdgeP p) {
+// Accumulate one residual row: A += w Jj^T Jj (upper), u += w r Jj.
+__device__ __forceinline__ void accum_row(const float* Ti, const float* Jl, float w, float r,
+                                          float* acc) {
+  float Jj[7];
+  adj_inv(Ti, Jl, Jj);
+  int c = 0;
+#pragma unroll
+  for (int a = 0; a < 7; ++a)
+#pragma unroll
+    for (int b = a; b < 7; ++b) acc[c++] += w * Jj[a] * Jj[b];
+#pragma unroll
+  for (int a = 0; a < 7; ++a) acc[28 + a] += w * r * Jj[a];
+}
+
+// grid (S, E): slice s of edge e.  MODE kRays: ray_align_kernel
+// (gn_kernels.cu:812-1137, 4 rows: ray direction + distance); kCalib:
+// calib_proj_kernel (:1230-1542, 3 rows: pixel u, v + log depth).  Both set
+// Ji = -Jj, so both reduce to the same 35 accumulators.
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) k_edge_align(EdgeP p) {
   if (p.state && p.state[0] != 0.0) return;
   const int s = blockIdx.x, S = gridDim.x, e = blockIdx.y;
   const int ix = p.ii[e], jx = p.jj[e];
@@ -92,52 +118,75 @@ __global__ void __launch_bounds__(kThreads) k_ray_align(EdgeP p) {
   const int64_t* idx = p.idx + (int64_t)e * n;
   const uint8_t* vm = p.valid + (int64_t)e * n;
   const float* Qe = p.Q + (int64_t)e * n;
+  float fx = 0.f, fy = 0.f, cx = 0.f, cy = 0.f;
+  if constexpr (MODE == kCalib) { fx = p.K[0]; fy = p.K[4]; cx = p.K[2]; cy = p.K[5]; }
   for (int64_t k = k0 + threadIdx.x; k < k1; k += kThreads) {
     const bool vmk = vm[k] != 0;
     const int64_t ind = vmk ? idx[k] : 0;
     const float Xi[3] = {Xi_all[ind * 3], Xi_all[ind * 3 + 1], Xi_all[ind * 3 + 2]};
     const float Xj[3] = {Xj_all[k * 3], Xj_all[k * 3 + 1], Xj_all[k * 3 + 2]};
-    const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
-    const float n1i = sqrtf(n2i);
-    const float n1i_inv = 1.0f / n1i;
-    const float ri[3] = {n1i_inv * Xi[0], n1i_inv * Xi[1], n1i_inv * Xi[2]};
-    float P[3];
-    s3lie::act_sim3(Tij, Xj, P);
-    const float n2j = P[0] * P[0] + P[1] * P[1] + P[2] * P[2];
-    const float n1j = sqrtf(n2j);
-    const float n1j_inv = 1.0f / n1j;
-    const float rj[3] = {n1j_inv * P[0], n1j_inv * P[1], n1j_inv * P[2]};
-    const float err[4] = {rj[0] - ri[0], rj[1] - ri[1], rj[2] - ri[2], n1j - n1i};
-    const float q = Qe[k];
-    const float ci = Ci_all[ind], cj = Cj_all[k];
-    const bool valid = vmk & (q > p.Q_thresh) & (ci > p.C_thresh) & (cj > p.C_thresh);
-    const float sq = sqrtf(q);
-    const float swr = valid ? p.inv_sr * sq : 0.f;
-    const float swd = valid ? p.inv_sd * sq : 0.f;
-    float w[4];
-    w[0] = huber_w(swr * err[0]) * (swr * swr);
-    w[1] = huber_w(swr * err[1]) * (swr * swr);
-    w[2] = huber_w(swr * err[2]) * (swr * swr);
-    w[3] = huber_w(swd * err[3]) * (swd * swd);
-    const float n3 = n1j_inv / n2j;
-    const float dxx = n1j_inv - P[0] * P[0] * n3, dyy = n1j_inv - P[1] * P[1] * n3;
-    const float dzz = n1j_inv - P[2] * P[2] * n3;
-    const float dxy = -P[0] * P[1] * n3, dxz = -P[0] * P[2] * n3, dyz = -P[1] * P[2] * n3;
-    const float Jl[4][7] = {{dxx, dxy, dxz, 0.f, rj[2], -rj[1], 0.f},
-                            {dxy, dyy, dyz, -rj[2], 0.f, rj[0], 0.f},
-                            {dxz, dyz, dzz, rj[1], -rj[0], 0.f, 0.f},
-                            {rj[0], rj[1], rj[2], 0.f, 0.f, 0.f, n1j}};
+    if constexpr (MODE == kRays) {
+      const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
+      const float n1i = sqrtf(n2i);
+      const float n1i_inv = 1.0f / n1i;
+      const float ri[3] = {n1i_inv * Xi[0], n1i_inv * Xi[1], n1i_inv * Xi[2]};
+      float P[3];
+      s3lie::act_sim3(Tij, Xj, P);
+      const float n2j = P[0] * P[0] + P[1] * P[1] + P[2] * P[2];
+      const float n1j = sqrtf(n2j);
+      const float n1j_inv = 1.0f / n1j;
+      const float rj[3] = {n1j_inv * P[0], n1j_inv * P[1], n1j_inv * P[2]};
+      const float err[4] = {rj[0] - ri[0], rj[1] - ri[1], rj[2] - ri[2], n1j - n1i};
+      const float q = Qe[k];
+      const float ci = Ci_all[ind], cj = Cj_all[k];
+      const bool valid = vmk & (q > p.Q_thresh) & (ci > p.C_thresh) & (cj > p.C_thresh);
+      const float sq = sqrtf(q);
+      const float swr = valid ? p.inv_sr * sq : 0.f;
+      const float swd = valid ? p.inv_sd * sq : 0.f;
+      float w[4];
+      w[0] = huber_w(swr * err[0]) * (swr * swr);
+      w[1] = huber_w(swr * err[1]) * (swr * swr);
+      w[2] = huber_w(swr * err[2]) * (swr * swr);
+      w[3] = huber_w(swd * err[3]) * (swd * swd);
+      const float n3 = n1j_inv / n2j;
+      const float dxx = n1j_inv - P[0] * P[0] * n3, dyy = n1j_inv - P[1] * P[1] * n3;
+      const float dzz = n1j_inv - P[2] * P[2] * n3;
+      const float dxy = -P[0] * P[1] * n3, dxz = -P[0] * P[2] * n3, dyz = -P[1] * P[2] * n3;
+      const float Jl[4][7] = {{dxx, dxy, dxz, 0.f, rj[2], -rj[1], 0.f},
+                              {dxy, dyy, dyz, -rj[2], 0.f, rj[0], 0.f},
+                              {dxz, dyz, dzz, rj[1], -rj[0], 0.f, 0.f},
+                              {rj[0], rj[1], rj[2], 0.f, 0.f, 0.f, n1j}};
+  #pragma unroll
+      for (int r = 0; r < 4; ++r) accum_row(Ti, Jl[r], w[r], err[r], acc);
+    } else {
+      // calib_proj_kernel:1359-1495
+      const int u_target = (int)(ind % p.width), v_target = (int)(ind / p.width);
+      float P[3];
+      s3lie::act_sim3(Tij, Xj, P);
+      const bool valid_z = (P[2] > p.z_eps) && (Xi[2] > p.z_eps);
+      const float zj_inv = valid_z ? 1.0f / P[2] : 0.f;
+      const float zj_log = valid_z ? logf(P[2]) : 0.f;
+      const float zi_log = valid_z ? logf(Xi[2]) : 0.f;
+      const float xz = P[0] * zj_inv, yz = P[1] * zj_inv;
+      const float u = fx * xz + cx, v = fy * yz + cy;
+      const bool valid_u = (u > (float)p.pixel_border) && (u < (float)(p.width - 1 - p.pixel_border));
+      const bool valid_v = (v > (float)p.pixel_border) && (v < (float)(p.height - 1 - p.pixel_border));
+      const float err[3] = {u - (float)u_target, v - (float)v_target, zj_log - zi_log};
+      const float q = Qe[k];
+      const float ci = Ci_all[ind], cj = Cj_all[k];
+      const bool valid = vmk & (q > p.Q_thresh) & (ci > p.C_thresh) & (cj > p.C_thresh) &
+                         valid_u & valid_v & valid_z;
+      const float sq = sqrtf(q);
+      const float swp = valid ? p.inv_sr * sq : 0.f;
+      const float swd = valid ? p.inv_sd * sq : 0.f;
+      const float w[3] = {huber_w(swp * err[0]) * (swp * swp), huber_w(swp * err[1]) * (swp * swp),
+                          huber_w(swd * err[2]) * (swd * swd)};
+      const float Jl[3][7] = {
+          {fx * zj_inv, 0.f, -fx * xz * zj_inv, -fx * xz * yz, fx * (1 + xz * xz), -fx * yz, 0.f},
+          {0.f, fy * zj_inv, -fy * yz * zj_inv, -fy * (1 + yz * yz), fy * xz * yz, fy * xz, 0.f},
+          {0.f, 0.f, zj_inv, yz, -xz, 0.f, 1.0f}};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float Jj[7];
-      adj_inv(Ti, Jl[r], Jj);
-      int c = 0;
-#pragma unroll
-      for (int a = 0; a < 7; ++a)
-#pragma unroll
-        for (int b = a; b < 7; ++b) acc[c++] += w[r] * Jj[a] * Jj[b];
-#pragma unroll
-      for (int a = 0; a < 7; ++a) acc[28 + a] += w[r] * err[r] * Jj[a];
+      for (int r = 0; r < 3; ++r) accum_row(Ti, Jl[r], w[r], err[r], acc);
     }
   }
   __shared__ float red[kThreads / 64][NA];
@@ -339,15 +388,26 @@ int check_args(int n_poses, int n_edges, int64_t n_points, int num_fix) {
   return S3_OK;
 }
 
+// Calib extras of EdgeP (null K = rays).
+struct CalibArgs {
+  const float* K = nullptr;
+  int height = 0, width = 0, pixel_border = 0;
+  float z_eps = 0.f;
+};
+
 int queue_system(const float* Twc, const float* Xs, const float* Cs, int64_t n_points,
                  const int32_t* ii, const int32_t* jj, int n_edges, const int64_t* idx,
-                 const uint8_t* valid, const float* Q, float sigma_ray, float sigma_dist,
+                 const uint8_t* valid, const float* Q, float sigma_a, float sigma_b,
                  float C_thresh, float Q_thresh, int num_fix, int n, const Ws& w,
-                 const double* state, hipStream_t st) {
+                 const double* state, hipStream_t st, const CalibArgs& cal = CalibArgs()) {
   if (n_edges > 0) {
-    EdgeP p{Twc, Xs, Cs, n_points, ii, jj, idx, valid, Q, 1.0f / sigma_ray, 1.0f / sigma_dist,
-            C_thresh, Q_thresh, w.partial, state};
-    k_ray_align<<<dim3(w.S, n_edges), kThreads, 0, st>>>(p);
+    EdgeP p{Twc, Xs, Cs, n_points, ii, jj, idx, valid, Q, 1.0f / sigma_a, 1.0f / sigma_b,
+            C_thresh, Q_thresh, w.partial, state, cal.K, cal.height, cal.width,
+            cal.pixel_border, cal.z_eps};
+    if (cal.K)
+      k_edge_align<kCalib><<<dim3(w.S, n_edges), kThreads, 0, st>>>(p);
+    else
+      k_edge_align<kRays><<<dim3(w.S, n_edges), kThreads, 0, st>>>(p);
     S3_LAUNCH_CHECK();
     k_edge_sum<<<(unsigned)s3::cdiv((int64_t)n_edges * NA, kThreads), kThreads, 0, st>>>(
         w.partial, w.S, n_edges, w.esum, state);
@@ -386,24 +446,20 @@ extern "C" int s3g_ray_system(const float* Twc, int n_poses, const float* Xs, co
                       sigma_ray, sigma_dist, C_thresh, Q_thresh, num_fix, n, w, nullptr, st);
 }
 
-extern "C" int s3g_gauss_newton_rays(float* Twc, int n_poses, const float* Xs, const float* Cs,
-                                     int64_t n_points, const int32_t* ii, const int32_t* jj,
-                                     int n_edges, const int64_t* idx_ii2jj,
-                                     const uint8_t* valid_match, const float* Q, float sigma_ray,
-                                     float sigma_dist, float C_thresh, float Q_thresh,
-                                     int max_iter, float delta_thresh, int num_fix,
-                                     void* workspace, float* dx, float* stats, void* stream) {
-  if (int r = check_args(n_poses, n_edges, n_points, num_fix)) return r;
-  S3_REQUIRE(workspace && dx && stats && max_iter >= 0, "s3g_gauss_newton_rays: bad arguments");
-  hipStream_t st = s3::as_stream(stream);
+namespace {
+int solve(float* Twc, int n_poses, const float* Xs, const float* Cs, int64_t n_points,
+          const int32_t* ii, const int32_t* jj, int n_edges, const int64_t* idx_ii2jj,
+          const uint8_t* valid_match, const float* Q, float sigma_a, float sigma_b,
+          float C_thresh, float Q_thresh, int max_iter, float delta_thresh, int num_fix,
+          void* workspace, float* dx, float* stats, hipStream_t st, const CalibArgs& cal) {
   Ws w = carve(workspace, n_poses, n_edges, n_points, num_fix);
   const int n = 7 * (n_poses - num_fix);
   S3_HIP(hipMemsetAsync(w.state, 0, sizeof(double) * 4, st));
   S3_HIP(hipMemsetAsync(dx, 0, sizeof(float) * n, st));
   for (int it = 0; it < max_iter; ++it) {
     if (int r = queue_system(Twc, Xs, Cs, n_points, ii, jj, n_edges, idx_ii2jj, valid_match, Q,
-                             sigma_ray, sigma_dist, C_thresh, Q_thresh, num_fix, n, w, w.state,
-                             st))
+                             sigma_a, sigma_b, C_thresh, Q_thresh, num_fix, n, w, w.state, st,
+                             cal))
       return r;
     k_chol_solve<<<1, kThreads, 0, st>>>(w.H, w.b, n, dx, w.state);
     S3_LAUNCH_CHECK();
@@ -417,4 +473,73 @@ extern "C" int s3g_gauss_newton_rays(float* Twc, int n_poses, const float* Xs, c
   stats[0] = (float)host_state[1];
   stats[1] = (float)host_state[2];
   return S3_OK;
+}
+}  // namespace
+
+extern "C" int s3g_gauss_newton_rays(float* Twc, int n_poses, const float* Xs, const float* Cs,
+                                     int64_t n_points, const int32_t* ii, const int32_t* jj,
+                                     int n_edges, const int64_t* idx_ii2jj,
+                                     const uint8_t* valid_match, const float* Q, float sigma_ray,
+                                     float sigma_dist, float C_thresh, float Q_thresh,
+                                     int max_iter, float delta_thresh, int num_fix,
+                                     void* workspace, float* dx, float* stats, void* stream) {
+  if (int r = check_args(n_poses, n_edges, n_points, num_fix)) return r;
+  S3_REQUIRE(workspace && dx && stats && max_iter >= 0, "s3g_gauss_newton_rays: bad arguments");
+  return solve(Twc, n_poses, Xs, Cs, n_points, ii, jj, n_edges, idx_ii2jj, valid_match, Q,
+               sigma_ray, sigma_dist, C_thresh, Q_thresh, max_iter, delta_thresh, num_fix,
+               workspace, dx, stats, s3::as_stream(stream), CalibArgs());
+}
+
+namespace {
+int check_calib(const float* K, int height, int width, int pixel_border, int64_t n_points) {
+  S3_REQUIRE(K != nullptr, "s3g calib: null K");
+  S3_REQUIRE(height > 0 && width > 0 && pixel_border >= 0, "s3g calib: bad image size %dx%d",
+             height, width);
+  S3_REQUIRE((int64_t)height * width == n_points,
+             "s3g calib: points per pose (%lld) must be height*width (%d x %d)",
+             (long long)n_points, height, width);
+  return S3_OK;
+}
+}  // namespace
+
+extern "C" int s3g_calib_system(const float* Twc, int n_poses, const float* Xs, const float* Cs,
+                                int64_t n_points, const float* K, const int32_t* ii,
+                                const int32_t* jj, int n_edges, const int64_t* idx_ii2jj,
+                                const uint8_t* valid_match, const float* Q, int height, int width,
+                                int pixel_border, float z_eps, float sigma_pixel,
+                                float sigma_depth, float C_thresh, float Q_thresh, int num_fix,
+                                void* workspace, double* H, double* b, void* stream) {
+  if (int r = check_args(n_poses, n_edges, n_points, num_fix)) return r;
+  if (int r = check_calib(K, height, width, pixel_border, n_points)) return r;
+  S3_REQUIRE(workspace && H && b, "s3g_calib_system: null workspace/output");
+  hipStream_t st = s3::as_stream(stream);
+  Ws w = carve(workspace, n_poses, n_edges, n_points, num_fix);
+  w.H = H;
+  w.b = b;
+  const int n = 7 * (n_poses - num_fix);
+  CalibArgs cal;
+  cal.K = K; cal.height = height; cal.width = width; cal.pixel_border = pixel_border;
+  cal.z_eps = z_eps;
+  return queue_system(Twc, Xs, Cs, n_points, ii, jj, n_edges, idx_ii2jj, valid_match, Q,
+                      sigma_pixel, sigma_depth, C_thresh, Q_thresh, num_fix, n, w, nullptr, st,
+                      cal);
+}
+
+extern "C" int s3g_gauss_newton_calib(float* Twc, int n_poses, const float* Xs, const float* Cs,
+                                      int64_t n_points, const float* K, const int32_t* ii,
+                                      const int32_t* jj, int n_edges, const int64_t* idx_ii2jj,
+                                      const uint8_t* valid_match, const float* Q, int height,
+                                      int width, int pixel_border, float z_eps, float sigma_pixel,
+                                      float sigma_depth, float C_thresh, float Q_thresh,
+                                      int max_iter, float delta_thresh, int num_fix,
+                                      void* workspace, float* dx, float* stats, void* stream) {
+  if (int r = check_args(n_poses, n_edges, n_points, num_fix)) return r;
+  if (int r = check_calib(K, height, width, pixel_border, n_points)) return r;
+  S3_REQUIRE(workspace && dx && stats && max_iter >= 0, "s3g_gauss_newton_calib: bad arguments");
+  CalibArgs cal;
+  cal.K = K; cal.height = height; cal.width = width; cal.pixel_border = pixel_border;
+  cal.z_eps = z_eps;
+  return solve(Twc, n_poses, Xs, Cs, n_points, ii, jj, n_edges, idx_ii2jj, valid_match, Q,
+               sigma_pixel, sigma_depth, C_thresh, Q_thresh, max_iter, delta_thresh, num_fix,
+               workspace, dx, stats, s3::as_stream(stream), cal);
 }

@@ -13,8 +13,10 @@ Non-contiguous inputs raise RuntimeError (reference CHECK_CONTIGUOUS).
                     C_thresh, Q_thresh, max_iter, delta_thresh) -> [dx f32 [N-1,7]]
     (gn.cpp:28-52 -> gn_kernels.cu:1139-1227; include/s3g.h; the whole
     iteration loop runs on the device, pose 0 fixed as in the reference).
-gauss_newton_calib (calibrated backend, config use_calib) is not built: it
-raises NotImplementedError.
+  gauss_newton_calib(Twc, Xs, Cs, K f32 [3,3], ii, jj, idx_ii2jj, valid_match, Q,
+                     height, width, pixel_border, z_eps, sigma_pixel, sigma_depth,
+                     C_thresh, Q_thresh, max_iter, delta_thresh) -> [dx f32 [N-1,7]]
+    (gn.cpp:54-80 -> gn_kernels.cu:1545-1637; same device loop as the rays solve)
 """
 from __future__ import annotations
 
@@ -73,6 +75,25 @@ _lib.register({
                                       ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p]),
+    "s3g_calib_system": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                        ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p]),
+    "s3g_gauss_newton_calib": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                              ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                              ctypes.c_float, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
+                                              ctypes.c_void_p]),
     "s3g_gauss_newton_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
@@ -151,6 +172,52 @@ def ray_system(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, sigma_ray, sigma_
     return H, b
 
 
-def gauss_newton_calib(*args, **kwargs):
-    raise NotImplementedError(
-        "gauss_newton_calib: the calibrated backend solver (config use_calib) is not built")
+def _calib_K(name, K):
+    _lib.require_cuda(K)
+    if tuple(K.shape) != (3, 3) or K.dtype != torch.float32:
+        raise RuntimeError(f"{name}: K must be float32 [3,3]")
+    return K.contiguous()
+
+
+def gauss_newton_calib(Twc, Xs, Cs, K, ii, jj, idx_ii2jj, valid_match, Q, height, width,
+                       pixel_border, z_eps, sigma_pixel, sigma_depth, C_thresh, Q_thresh,
+                       max_iter, delta_thresh):
+    N, hw, E, ii_l, jj_l = _gn_inputs("gauss_newton_calib", Twc, Xs, Cs, ii, jj, idx_ii2jj,
+                                      valid_match, Q)
+    K = _calib_K("gauss_newton_calib", K)
+    dev = Twc.device
+    L = _lib.lib()
+    ws = torch.empty(int(L.s3g_workspace_bytes(N, E, hw, NUM_FIX)), dtype=torch.uint8,
+                     device=dev)
+    dx = torch.zeros(N - NUM_FIX, 7, device=dev, dtype=torch.float32)
+    stats = (ctypes.c_float * 2)()
+    _lib.call("s3g_gauss_newton_calib", Twc.data_ptr(), N, Xs.data_ptr(), Cs.data_ptr(), hw,
+              K.data_ptr(), ii_l.data_ptr(), jj_l.data_ptr(), E, idx_ii2jj.data_ptr(),
+              valid_match.data_ptr(), Q.data_ptr(), int(height), int(width), int(pixel_border),
+              float(z_eps), float(sigma_pixel), float(sigma_depth), float(C_thresh),
+              float(Q_thresh), int(max_iter), float(delta_thresh), NUM_FIX, ws.data_ptr(),
+              dx.data_ptr(), stats, _lib.stream(dev))
+    gauss_newton_calib.last_stats = (int(stats[0]), float(stats[1]))
+    return [dx]
+
+
+def calib_system(Twc, Xs, Cs, K, ii, jj, idx_ii2jj, valid_match, Q, height, width, pixel_border,
+                 z_eps, sigma_pixel, sigma_depth, C_thresh, Q_thresh):
+    """One iteration's dense (H, b) of the calibrated solve (diagnostics/tests)."""
+    N, hw, E, ii_l, jj_l = _gn_inputs("calib_system", Twc, Xs, Cs, ii, jj, idx_ii2jj,
+                                      valid_match, Q)
+    K = _calib_K("calib_system", K)
+    dev = Twc.device
+    n = 7 * (N - NUM_FIX)
+    L = _lib.lib()
+    ws = torch.empty(int(L.s3g_workspace_bytes(N, E, hw, NUM_FIX)), dtype=torch.uint8,
+                     device=dev)
+    H = torch.empty(n, n, device=dev, dtype=torch.float64)
+    b = torch.empty(n, device=dev, dtype=torch.float64)
+    _lib.call("s3g_calib_system", Twc.data_ptr(), N, Xs.data_ptr(), Cs.data_ptr(), hw,
+              K.data_ptr(), ii_l.data_ptr(), jj_l.data_ptr(), E, idx_ii2jj.data_ptr(),
+              valid_match.data_ptr(), Q.data_ptr(), int(height), int(width), int(pixel_border),
+              float(z_eps), float(sigma_pixel), float(sigma_depth), float(C_thresh),
+              float(Q_thresh), NUM_FIX, ws.data_ptr(), H.data_ptr(), b.data_ptr(),
+              _lib.stream(dev))
+    return H, b

@@ -17,8 +17,10 @@ Same function names, argument meaning and file bytes as the reference:
 * `save_keyframes` (evaluate.py:74-85): `{t}.png` per keyframe (PIL instead
   of cv2; cv2's BGR swap followed by its BGR->RGB write is the identity).
 
-The calibrated branch (`intrinsics` / config use_calib) is not built
-(DESIGN.md §7): it raises NotImplementedError.
+save_reconstruction's use_calib branch constrains points to their pixel
+rays first (evaluate.py:55-59); save_traj's `intrinsics` pose refinement
+(Intrinsics.refine_pose_with_calibration, dataloader) is not built and
+raises NotImplementedError.
 """
 from __future__ import annotations
 
@@ -94,13 +96,15 @@ def load_ply(filename):
 
 
 def save_reconstruction(savedir, filename, keyframes, c_conf_threshold):
-    if config.get("use_calib", False):
-        raise NotImplementedError("constrain_points_to_ray (use_calib) is not built")
     savedir = pathlib.Path(savedir)
     savedir.mkdir(exist_ok=True, parents=True)
     pts, cols = [], []
     for i in range(len(keyframes)):
         kf = keyframes[i]
+        if config.get("use_calib", False):
+            from splatt3r_amd.geometry import constrain_points_to_ray
+            kf.X_canon = constrain_points_to_ray(kf.img_shape.flatten()[:2], kf.X_canon[None],
+                                                 kf.K).squeeze(0)
         pW = kf.T_WC.act(kf.X_canon).cpu().numpy().reshape(-1, 3)
         color = (kf.uimg.cpu().numpy() * 255).astype(np.uint8).reshape(-1, 3)
         valid = kf.get_average_conf().cpu().numpy().astype(np.float32).reshape(-1) > c_conf_threshold

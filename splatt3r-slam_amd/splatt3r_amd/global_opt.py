@@ -5,7 +5,9 @@ edges -> the device-resident Gauss-Newton of include/s3g.h
 (mast3r_slam_backends.gauss_newton_rays).
 
 Same attribute names, edge bookkeeping and acceptance rule as the
-reference; the calibrated solve (config use_calib) is not built.
+reference; solve_GN_calib (config use_calib) runs the calibrated device
+solve (mast3r_slam_backends.gauss_newton_calib) on points constrained to
+their pixel rays.
 """
 from __future__ import annotations
 
@@ -107,4 +109,26 @@ class FactorGraph:
         return dx
 
     def solve_GN_calib(self):
-        raise NotImplementedError("calibrated backend GN (gauss_newton_calib) is not built")
+        """global_opt.py:160-215."""
+        from splatt3r_amd.geometry import constrain_points_to_ray
+        K = self.K
+        pin = self.cfg["pin"]
+        unique = self.get_unique_kf_idx()
+        if unique.numel() <= pin:
+            return None
+        Xs, T_WCs, Cs = self.get_poses_points(unique)
+        img_size = self.frames[0].img.shape[-2:]
+        Xs = constrain_points_to_ray(img_size, Xs, K)
+        ii, jj, idx, valid, Q = self.prep_two_way_edges()
+        height, width = img_size
+        pose_data = T_WCs.data[:, 0, :].contiguous()
+        (dx,) = mast3r_slam_backends.gauss_newton_calib(
+            pose_data, Xs.contiguous().float(), Cs.contiguous().float(), K.float(),
+            ii.contiguous(), jj.contiguous(), idx.contiguous(), valid.contiguous(),
+            Q.contiguous().float(), height, width, self.cfg["pixel_border"],
+            self.cfg["depth_eps"], self.cfg["sigma_pixel"], self.cfg["sigma_depth"],
+            self.cfg["C_conf"], self.cfg["Q_conf"], self.cfg["max_iters"],
+            self.cfg["delta_norm"])
+        for k in range(pin, unique.numel()):
+            self.frames[int(unique[k])].T_WC = lietorch.Sim3(pose_data[k:k + 1].clone())
+        return dx

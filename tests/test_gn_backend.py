@@ -176,3 +176,150 @@ def test_hip_gauss_newton_rays_global_ids():
     be.gauss_newton_rays(Tl, *rest, *CFG.values(), 5, 1e-8)
     be.gauss_newton_rays(Tg, *restg, *CFG.values(), 5, 1e-8)
     assert torch.equal(Tl, Tg)
+
+
+# ---- calibrated backend (gauss_newton_calib, gn_kernels.cu:1230-1637) ----
+
+CAL = dict(sigma_pixel=1.0, sigma_depth=10.0, C_thresh=0.0, Q_thresh=1.5)   # config/base.yaml
+KC = np.array([[30.0, 0, 15.5], [0, 30.0, 11.5], [0, 0, 1]], np.float32)
+
+
+def calib_scene(N=4, h=24, w=32, edges=((0, 1), (1, 2), (2, 3), (0, 2), (1, 3)), seed=0):
+    """Keyframes looking at the world plane z = 4 + 0.3 x - 0.2 y; each
+    keyframe's pointmap is its pixel rays cut by the plane (points on their
+    own rays, as constrain_points_to_ray leaves them); matches = the pixel of
+    i that T_ij X_j projects to, rounded (sub-pixel residuals remain)."""
+    rng = np.random.default_rng(seed)
+    T = np.zeros((N, 8), np.float32)
+    for k in range(N):
+        T[k, :3] = rng.normal(size=3) * 0.1 if k else 0.0
+        T[k, 3:7] = _quat(rng) * [0.02, 0.02, 0.02, 1.0] if k else [0, 0, 0, 1]
+        T[k, 3:7] /= np.linalg.norm(T[k, 3:7])
+        T[k, 7] = 1.0 + 0.05 * rng.normal() if k else 1.0
+    n_w, c_w = np.array([-0.3, 0.2, 1.0]), 4.0
+    v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    d = np.stack([(u - KC[0, 2]) / KC[0, 0], (v - KC[1, 2]) / KC[1, 1], np.ones_like(u, float)],
+                 -1).reshape(-1, 3)
+    Xs = np.zeros((N, h * w, 3), np.float32)
+    for k in range(N):
+        R = oracle.sim3_act(np.array([[0, 0, 0, *T[k, 3:7], 1]], np.float32),
+                            np.eye(3, dtype=np.float32)).T.astype(np.float64)   # columns = R e_i
+        n_c = T[k, 7] * R.T @ n_w
+        c_c = c_w - n_w @ T[k, :3]
+        Xs[k] = (c_c / (d @ n_c))[:, None] * d
+    Cs = np.full((N, h * w, 1), 3.0, np.float32)
+    E = len(edges)
+    ii = np.array([e[0] for e in edges], np.int64)
+    jj = np.array([e[1] for e in edges], np.int64)
+    idx = np.zeros((E, h * w), np.int64)
+    valid = np.zeros((E, h * w, 1), bool)
+    for e, (i, j) in enumerate(edges):
+        Tij = oracle.sim3_mul(oracle.sim3_inv(T[i:i + 1]), T[j:j + 1])[0]
+        P = oracle.sim3_act(Tij, Xs[j]).astype(np.float64)
+        pu = np.rint(KC[0, 0] * P[:, 0] / P[:, 2] + KC[0, 2]).astype(np.int64)
+        pv = np.rint(KC[1, 1] * P[:, 1] / P[:, 2] + KC[1, 2]).astype(np.int64)
+        inside = (pu >= 0) & (pu < w) & (pv >= 0) & (pv < h)
+        idx[e] = np.where(inside, pv * w + pu, 0)
+        valid[e, :, 0] = inside
+    valid[:, ::13] = False
+    Q = np.full((E, h * w, 1), 2.0, np.float32)
+    Q[:, ::11] = 1.0
+    return T, Xs, Cs, ii, jj, idx, valid, Q, h, w
+
+
+def _cal_kw(h, w):
+    return dict(K=KC, height=h, width=w, pixel_border=-10, z_eps=1e-6)
+
+
+def test_oracle_calib_converges_to_one_optimum():
+    """Rounded matches leave +-0.5 px residuals and the pixel rows are blind
+    to a per-edge scale (only the sigma_depth = 10 log-depth row sees it), so
+    the least-squares optimum is not the generating poses: check that the
+    solve converges (|dx| -> 0) to the same poses from the truth and from a
+    perturbed start."""
+    T, Xs, Cs, ii, jj, idx, valid, Q, h, w = calib_scene()
+    assert valid.mean() > 0.6
+    args = (Xs, Cs, KC, ii, jj, idx, valid, Q, h, w, -10, 1e-6, *CAL.values(), 10, 1e-8)
+    Ta, dxa, _ = G.gauss_newton_calib(T, *args)
+    T0 = perturb(T, mag=0.005)
+    Tb, dxb, _ = G.gauss_newton_calib(T0, *args)
+    assert np.linalg.norm(dxa) < 1e-4 and np.linalg.norm(dxb) < 1e-4
+    assert np.abs(Ta - Tb).max() < 1e-4
+    assert np.abs(Tb[0] - T0[0]).max() == 0
+
+
+def test_oracle_calib_gradient_matches_finite_differences():
+    T, Xs, Cs, ii, jj, idx, valid, Q, h, w = calib_scene()
+    T = perturb(T, mag=0.002).astype(np.float64)
+    e, i, j = 0, ii[0], jj[0]
+    kw = _cal_kw(h, w)
+    cfg = dict(sigma_pixel=50.0, sigma_depth=10.0, C_thresh=0.0, Q_thresh=1.5)  # Huber inactive
+    _, v = G.edge_system_calib(T[i], T[j], Xs[i], Cs[i, :, 0], Xs[j], Cs[j, :, 0], idx[e],
+                               valid[e, :, 0], Q[e, :, 0], *cfg.values(), **kw)
+
+    def cost(Ti, Tj):
+        vm = valid[e, :, 0]
+        ind = np.where(vm, idx[e], 0)
+        Xi = Xs[i][ind].astype(np.float64)
+        tij, qij, sij = G.rel_sim3(Ti, Tj)
+        P = sij * G.act_so3(qij, Xs[j].astype(np.float64)) + tij
+        u = KC[0, 0] * P[:, 0] / P[:, 2] + KC[0, 2]
+        vv = KC[1, 1] * P[:, 1] / P[:, 2] + KC[1, 2]
+        err = np.stack([u - ind % w, vv - ind // w, np.log(P[:, 2]) - np.log(Xi[:, 2])], -1)
+        q = Q[e, :, 0]
+        ok = vm & (q > 1.5)
+        sw = np.stack([np.where(ok, np.sqrt(q) / 50.0, 0)] * 2 + [np.where(ok, np.sqrt(q) / 10, 0)],
+                      -1)
+        return 0.5 * np.sum((sw * err) ** 2)
+
+    hstep = 1e-6
+    for side, k0 in ((0, 0), (1, 7)):
+        for k in range(7):
+            xi = np.zeros(7)
+            xi[k] = hstep
+            Tp = [T[i].copy(), T[j].copy()]
+            Tm = [T[i].copy(), T[j].copy()]
+            Tp[side] = oracle.sim3_retr(Tp[side].astype(np.float32), xi)[0].astype(np.float64)
+            Tm[side] = oracle.sim3_retr(Tm[side].astype(np.float32), -xi)[0].astype(np.float64)
+            num = (cost(*Tp) - cost(*Tm)) / (2 * hstep)
+            assert abs(num - v[k0 + k]) <= 2e-2 * np.abs(v).max() + 1e-3, (side, k, num, v[k0 + k])
+
+
+@pytest.mark.gpu
+def test_hip_calib_system_vs_oracle():
+    import mast3r_slam_backends as be
+    T, Xs, Cs, ii, jj, idx, valid, Q, h, w = calib_scene(h=48, w=64)
+    T = perturb(T, mag=0.003)
+    H_ref, b_ref = G.build_system(T, Xs, Cs, ii, jj, idx, valid, Q, *CAL.values(),
+                                  calib=_cal_kw(h, w))
+    Td, Xd, Cd, iid, jjd, idxd, vd, Qd, Kd = _dev(T, Xs, Cs, ii, jj, idx, valid, Q, KC)
+    H, b = be.calib_system(Td, Xd, Cd, Kd, iid, jjd, idxd, vd, Qd, h, w, -10, 1e-6,
+                           *CAL.values())
+    H, b = H.cpu().numpy(), b.cpu().numpy()
+    assert np.abs(H - H_ref).max() <= 1e-4 * np.abs(H_ref).max()
+    assert np.abs(b - b_ref).max() <= 1e-4 * np.abs(b_ref).max()
+
+
+@pytest.mark.gpu
+def test_hip_gauss_newton_calib_vs_oracle():
+    import mast3r_slam_backends as be
+    T, Xs, Cs, ii, jj, idx, valid, Q, h, w = calib_scene(h=48, w=64)
+    T0 = perturb(T, mag=0.005)
+    Tn_ref, dx_ref, it_ref = G.gauss_newton_calib(T0, Xs, Cs, KC, ii, jj, idx, valid, Q, h, w,
+                                                  -10, 1e-6, *CAL.values(), 10, 1e-8)
+    Td, Xd, Cd, iid, jjd, idxd, vd, Qd, Kd = _dev(T0, Xs, Cs, ii, jj, idx, valid, Q, KC)
+    (dx,) = be.gauss_newton_calib(Td, Xd, Cd, Kd, iid, jjd, idxd, vd, Qd, h, w, -10, 1e-6,
+                                  *CAL.values(), 10, 1e-8)
+    Tn = Td.cpu().numpy()
+    assert np.abs(Tn - Tn_ref).max() < 1e-4
+    assert np.abs(Tn[0] - T0[0]).max() == 0
+    assert dx.shape == (3, 7)
+
+
+@pytest.mark.gpu
+def test_hip_calib_rejects_bad_size():
+    import mast3r_slam_backends as be
+    T, Xs, Cs, ii, jj, idx, valid, Q, h, w = calib_scene()
+    with pytest.raises(RuntimeError):
+        be.gauss_newton_calib(*_dev(T, Xs, Cs, KC, ii, jj, idx, valid, Q), h + 1, w, -10, 1e-6,
+                              *CAL.values(), 10, 1e-8)
