@@ -493,7 +493,7 @@ extern "C" int s3g_gauss_newton_rays(float* Twc, int n_poses, const float* Xs, c
 namespace {
 int check_calib(const float* K, int height, int width, int pixel_border, int64_t n_points) {
   S3_REQUIRE(K != nullptr, "s3g calib: null K");
-  S3_REQUIRE(height > 0 && width > 0 && pixel_border >= 0, "s3g calib: bad image size %dx%d",
+  S3_REQUIRE(height > 0 && width > 0, "s3g calib: bad image size %dx%d",
              height, width);
   S3_REQUIRE((int64_t)height * width == n_points,
              "s3g calib: points per pose (%lld) must be height*width (%d x %d)",
