@@ -42,6 +42,7 @@ SOURCES = {
     "net_attn.hip": FAST,
     "net_ops.hip": STRICT,
     "gn_backend.hip": STRICT,
+    "retrieval.hip": STRICT,
 }
 
 

@@ -1,0 +1,160 @@
+"""Keyframe retrieval, device half —
+splatt3r_slam/retrieval_database.py over include/s3q.h.
+
+`RetrievalDatabase.prep_features` (retrieval_database.py:24-41) and
+`quantize_custom` (:95-104) keep their names, inputs and outputs; both run
+as HIP kernels (fp64 whiteners, fp32 projector, 'l2norm' attention + top-nfeat
+token selection, fused L2-distance + top-k over the codebook).  The weights
+come from the MASt3R retrieval checkpoint (`Retriever`, mast3r/retrieval/
+processor.py:62-96: prewhiten / projector / postwhiten, nfeat, and the ASMK
+codebook centroids); `RetrievalWeights` holds them as device tensors.
+
+The ASMK inverted file (`asmk` package: aggregate_image, ivf.search; CPU)
+is third-party and absent here, so `update` / `query` / `add_to_database`
+raise NotImplementedError; the GEMM + top-k that feeds them is here.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional, Tuple
+
+import torch
+
+from splatt3r_amd import _lib
+
+_lib.register({
+    "s3q_whiten": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_int] * 3 + [ctypes.c_void_p]),
+    "s3q_linear": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_void_p]),
+    "s3q_select_local": (ctypes.c_int, [ctypes.c_void_p] * 2 + [ctypes.c_int] * 4 +
+                         [ctypes.c_void_p] * 4),
+    "s3q_row_sqnorm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "s3q_l2_topk_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int] * 3),
+    "s3q_l2_topk": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 +
+                    [ctypes.c_void_p] * 4),
+})
+
+# asmk_params of Retriever (processor.py:84-89)
+ASMK_PARAMS = {"build_ivf": {"quantize": {"multiple_assignment": 1}},
+               "query_ivf": {"quantize": {"multiple_assignment": 5}}}
+
+
+@dataclasses.dataclass
+class RetrievalWeights:
+    proj_W: torch.Tensor                    # [dim, 1024] f32 (nn.Linear weight)
+    proj_b: torch.Tensor                    # [dim] f32
+    centroids: torch.Tensor                 # [n_clusters, dim] f32 (ASMK codebook)
+    prewhiten: Optional[Tuple[torch.Tensor, torch.Tensor]] = None    # (m [1,1024] f64, P f64)
+    postwhiten: Optional[Tuple[torch.Tensor, torch.Tensor]] = None   # (m [1,dim] f64, P f64)
+    residual: bool = False
+    nfeat: int = 300
+
+
+def _chk(t, dtype, name):
+    _lib.require_cuda(t)
+    if t.dtype != dtype:
+        raise RuntimeError(f"{name}: expected {dtype}, got {t.dtype}")
+    return t.contiguous()
+
+
+def whiten(x, m, P):
+    """Whitener.forward (model.py:62-75): ((x - m) @ P) in fp64, cast back."""
+    x = _chk(x, torch.float32, "whiten")
+    P = _chk(P, torch.float64, "whiten")
+    K, N = P.shape
+    M = x.numel() // K
+    out = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
+    mp = _chk(m, torch.float64, "whiten").data_ptr() if m is not None else None
+    _lib.call("s3q_whiten", x.data_ptr(), mp, P.data_ptr(), out.data_ptr(), M, K, N,
+              _lib.stream(x.device))
+    return out
+
+
+def linear(x, W, b, residual=False):
+    x = _chk(x, torch.float32, "linear")
+    W = _chk(W, torch.float32, "linear")
+    N, K = W.shape
+    M = x.numel() // K
+    out = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
+    bp = _chk(b, torch.float32, "linear").data_ptr() if b is not None else None
+    _lib.call("s3q_linear", x.data_ptr(), W.data_ptr(), bp, out.data_ptr(), M, K, N,
+              int(bool(residual)), _lib.stream(x.device))
+    return out
+
+
+def how_select_local(feat, attn_src, nfeat):
+    """how_select_local (model.py:89-103) with attention = ||attn_src||_2:
+    -> (topk_features [B,k,D], topk_attn [B,k], topk_indices [B,k])."""
+    feat = _chk(feat, torch.float32, "how_select_local")
+    attn_src = _chk(attn_src, torch.float32, "how_select_local")
+    B, T, D = feat.shape
+    if nfeat < 0:
+        nfeat = int(-nfeat * T)
+    k = min(int(nfeat), T)
+    fo = torch.empty(B, k, D, device=feat.device, dtype=torch.float32)
+    ao = torch.empty(B, k, device=feat.device, dtype=torch.float32)
+    io = torch.empty(B, k, device=feat.device, dtype=torch.int64)
+    _lib.call("s3q_select_local", attn_src.data_ptr(), feat.data_ptr(), B, T, D, k,
+              fo.data_ptr(), ao.data_ptr(), io.data_ptr(), _lib.stream(feat.device))
+    return fo, ao, io
+
+
+def row_sqnorm(x):
+    x = _chk(x, torch.float32, "row_sqnorm")
+    R, D = x.shape
+    out = torch.empty(R, device=x.device, dtype=torch.float32)
+    _lib.call("s3q_row_sqnorm", x.data_ptr(), R, D, out.data_ptr(), _lib.stream(x.device))
+    return out
+
+
+def l2_topk(q, centroids, c_sqnorm, k):
+    """Indices [M,k] i64 and distances [M,k] of the k nearest centroids."""
+    q = _chk(q, torch.float32, "l2_topk")
+    c = _chk(centroids, torch.float32, "l2_topk")
+    M, D = q.shape
+    C = c.shape[0]
+    if c.shape[1] != D:
+        raise RuntimeError("l2_topk: dim mismatch")
+    idx = torch.empty(M, k, device=q.device, dtype=torch.int64)
+    dist = torch.empty(M, k, device=q.device, dtype=torch.float32)
+    L = _lib.lib()
+    ws = torch.empty(int(L.s3q_l2_topk_workspace_bytes(M, C, k)), device=q.device,
+                     dtype=torch.uint8)
+    _lib.call("s3q_l2_topk", q.data_ptr(), c.data_ptr(), c_sqnorm.data_ptr(), M, C, D, int(k),
+              idx.data_ptr(), dist.data_ptr(), ws.data_ptr(), _lib.stream(q.device))
+    return idx, dist
+
+
+class RetrievalDatabase:
+    """retrieval_database.py:9-22 minus the ASMK IVF builder."""
+
+    def __init__(self, weights: RetrievalWeights, device="cuda"):
+        self.w = weights
+        self.kf_counter = 0
+        self.kf_ids = []
+        self.query_dtype = torch.float32
+        self.query_device = device
+        self.centroids = weights.centroids.to(device=device, dtype=torch.float32).contiguous()
+        self._c_sq = row_sqnorm(self.centroids)
+
+    def prep_features(self, backbone_feat):
+        """retrieval_database.py:24-41 -> topk_features [B, nfeat, dim]."""
+        w = self.w
+        x = backbone_feat.float().contiguous()
+        if w.prewhiten is not None:
+            x = whiten(x, *w.prewhiten)
+        proj = linear(x, w.proj_W, w.proj_b, w.residual)
+        post = whiten(proj, *w.postwhiten) if w.postwhiten is not None else proj
+        feats, _, _ = how_select_local(post, proj, w.nfeat)
+        return feats
+
+    def quantize_custom(self, qvecs, params):
+        """retrieval_database.py:95-104 -> indices [M, multiple_assignment]."""
+        k = params["quantize"]["multiple_assignment"]
+        idx, _ = l2_topk(qvecs.to(self.query_dtype), self.centroids, self._c_sq, k)
+        return idx
+
+    def update(self, frame, add_after_query, k, min_thresh=0.0):
+        raise NotImplementedError("RetrievalDatabase.update needs the ASMK inverted file "
+                                  "(third-party `asmk`, CPU), which is not available")

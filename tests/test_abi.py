@@ -41,7 +41,8 @@ def test_every_declared_symbol_has_a_ctypes_signature():
     from splatt3r_amd import _lib
     import importlib
     for mod in ("splatt3r_amd.net", "splatt3r_amd.tracker", "diff_gaussian_rasterization",
-                "splatt3r_amd.render", "splatt3r_amd.splatt3r_utils", "mast3r_slam_backends"):
+                "splatt3r_amd.render", "splatt3r_amd.splatt3r_utils", "mast3r_slam_backends",
+                "splatt3r_amd.retrieval_database"):
         try:
             importlib.import_module(mod)  # registers its signatures
         except ModuleNotFoundError:
@@ -71,7 +72,8 @@ def test_ctypes_signatures_match_header_arity():
     from splatt3r_amd import _lib
     import importlib
     for mod in ("splatt3r_amd.net", "splatt3r_amd.tracker", "diff_gaussian_rasterization",
-                "splatt3r_amd.render", "splatt3r_amd.splatt3r_utils", "mast3r_slam_backends"):
+                "splatt3r_amd.render", "splatt3r_amd.splatt3r_utils", "mast3r_slam_backends",
+                "splatt3r_amd.retrieval_database"):
         try:
             importlib.import_module(mod)
         except ModuleNotFoundError:
