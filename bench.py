@@ -281,12 +281,16 @@ def main():
         from splatt3r_amd.bench_raster import run as raster_run
         r = raster_run(4_194_304, iters=5, warmup=2, backward=True, device=dev)
         result["raster_c3"] = {k: r[k] for k in ("P", "fwd_ms", "msplats_per_s", "fwd_GBps",
-                                                 "phases_ms", "bwd_ms", "bwd_GBps")}
+                                                 "phases_ms", "bwd_ms", "bwd_GBps",
+                                                 "num_rendered", "visible")}
         result["raster_c3"]["hbm_frac"] = r["fwd_GBps"] / PEAK_HBM_GBPS
         # BASELINE config 3 is forward + backward
         result["raster_c3"]["fwd_bwd_ms"] = r["fwd_ms"] + r["bwd_ms"]
         result["raster_c3"]["msplats_per_s_fwd_bwd"] = r["P"] / ((r["fwd_ms"] + r["bwd_ms"])
                                                                  * 1e-3) / 1e6
+    if rank == 0 and not a.no_c3:
+        from splatt3r_amd.retrieval_database import bench as retrieval_bench
+        result["retrieval"] = retrieval_bench(dev)
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(FULL, seed, frames, a.cpu_frames)
     if rank == 0:

@@ -46,6 +46,7 @@ struct GeomState {
   float* cov3D;  // [P,6] (scale/rotation path)
   uint8_t* clamped;  // [P,3]
   uint32_t* tiles;
+  uint64_t* tmask;   // kept tiles of the rect (bit (y - y0) * w + (x - x0)), rects <= 64 tiles
   uint32_t* offsets;
   void* scan_tmp;
   size_t scan_bytes;
@@ -84,6 +85,7 @@ GeomState carve_geom(void* base, int64_t P) {
   g.cov3D = c.take<float>(P * 6);
   g.clamped = c.take<uint8_t>(P * 3);
   g.tiles = c.take<uint32_t>(P);
+  g.tmask = c.take<uint64_t>(P);
   g.offsets = c.take<uint32_t>(P);
   g.scan_bytes = scan_temp_bytes(P);
   g.scan_tmp = c.take<char>(g.scan_bytes);
@@ -100,7 +102,8 @@ GeomState carve_geom(void* base, int64_t P) {
 size_t geom_bytes(int64_t P) {
   Carver c{nullptr};
   c.take<float>(P); c.take<float4>(P); c.take<float4>(P); c.take<float>(P * 3);
-  c.take<float>(P * 6); c.take<uint8_t>(P * 3); c.take<uint32_t>(P); c.take<uint32_t>(P);
+  c.take<float>(P * 6); c.take<uint8_t>(P * 3); c.take<uint32_t>(P); c.take<uint64_t>(P);
+  c.take<uint32_t>(P);
   c.take<char>(scan_temp_bytes(P));
   for (int k = 0; k < 6; ++k) c.take<uint32_t>(P);
   c.take<char>(key32_sort_temp_bytes(P));
@@ -247,7 +250,25 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
   radii[i] = r;
   g.rec0[i] = make_float4(px, py, c * det_inv, -b * det_inv);
   g.rec1[i] = make_float4(a * det_inv, opac[i], 0.0f, 0.0f);
-  g.tiles[i] = (uint32_t)((y1 - y0) * (x1 - x0));
+  // tiles the blend can actually use (tile_hit); the reference lists every
+  // tile of the rect, whose extra entries are all skipped per pixel
+  // rects of <= 64 tiles: keep only the tiles the blend can use (tile_cull /
+  // tile_hit, raster_math.hpp) as a bit mask; larger rects keep every tile
+  const int rw = x1 - x0, area = rw * (y1 - y0);
+  uint64_t mask = ~0ull;
+  uint32_t n = (uint32_t)area;
+  if (area <= 64) {
+    const float cA = c * det_inv, cB = -b * det_inv, cC = a * det_inv;
+    const TileCull tc = tile_cull(px, py, cA, cB, cC, opac[i], x0, y0, x1, y1);
+    mask = 0;
+    for (int y = tc.y0; y < tc.y1; ++y)
+      for (int x = tc.x0; x < tc.x1; ++x)
+        if (tile_hit(tc, px, py, cA, cB, cC, x, y, cam.W, cam.H))
+          mask |= 1ull << ((y - y0) * rw + (x - x0));
+    n = (uint32_t)__popcll(mask);
+  }
+  g.tmask[i] = mask;
+  g.tiles[i] = n;
 }
 
 // ------------------------------------------------------------- binning ----
@@ -267,28 +288,75 @@ k_gather_tiles(int64_t P, GeomState g) {
   if (k < P) g.tiles_sorted[k] = g.tiles[g.order[k]];
 }
 
-// One lane per depth rank k: the instances of Gaussian order[k], one per
-// touched tile, written at its depth-ordered offset.  A stable sort by tile
-// id then yields the reference's (tile, depth, index) order
-// (rasterizer_impl.cu duplicateWithKeys + SortPairs over tile<<32 | depth):
-// equal depths keep index order from the stable depth sort.
+// Position of the j-th set bit of m (j < popcount(m)).
+__device__ __forceinline__ int select_bit(uint64_t m, uint32_t j) {
+  int base = 0;
+  uint32_t w = (uint32_t)m;
+  const uint32_t pc = (uint32_t)__popc(w);
+  if (j >= pc) { j -= pc; w = (uint32_t)(m >> 32); base = 32; }
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const uint32_t c = (uint32_t)__popc(w & 0xFFu);
+    if (j < c) break;
+    j -= c; w >>= 8; base += 8;
+  }
+  for (uint32_t t = 0; t < j; ++t) w &= w - 1;
+  return base + __builtin_ctz(w);
+}
+
+// Instances in depth order: the wave's 64 depth ranks k own the contiguous
+// output range [start(k0), end(k0 + 63)); each lane writes every 64th slot
+// of it (coalesced stores), finding the owning rank by a shuffle binary
+// search over the lanes' start offsets and its tile from the rank's kept-
+// tile mask.  A stable sort by tile id then yields the reference's
+// (tile, depth, index) order (rasterizer_impl.cu duplicateWithKeys +
+// SortPairs over tile<<32 | depth): equal depths keep index order from the
+// stable depth sort.
 __global__ void __launch_bounds__(kThreads)
 k_duplicate(int64_t P, int gx, int gy, const int32_t* __restrict__ radii, GeomState g,
             uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= P) return;
-  const uint32_t i = g.order[k];
-  if (radii[i] <= 0) return;
-  uint32_t off = k == 0 ? 0u : g.offsets_sorted[k - 1];
-  const float4 r0 = g.rec0[i];
-  int x0, y0, x1, y1;
-  get_rect(r0.x, r0.y, radii[i], gx, gy, &x0, &y0, &x1, &y1);
-  for (int y = y0; y < y1; ++y)
-    for (int x = x0; x < x1; ++x) {
-      keys[off] = (uint32_t)(y * gx + x);
-      vals[off] = i;
-      ++off;
+  const int lane = threadIdx.x & 63;
+  uint32_t i = 0, cnt = 0, start = g.offsets_sorted[P - 1];
+  int x0 = 0, y0 = 0, rw = 1;
+  uint64_t mask = 0;
+  int use_mask = 0;
+  if (k < P) {
+    i = g.order[k];
+    cnt = g.tiles_sorted[k];
+    start = k == 0 ? 0u : g.offsets_sorted[k - 1];
+    if (cnt > 0) {
+      const float4 r0 = g.rec0[i];
+      int x1, y1;
+      get_rect(r0.x, r0.y, radii[i], gx, gy, &x0, &y0, &x1, &y1);
+      rw = x1 - x0;
+      use_mask = rw * (y1 - y0) <= 64;
+      mask = g.tmask[i];
     }
+  }
+  const uint32_t lo = __shfl(start, 0, 64);
+  const uint32_t hi = __shfl(start + cnt, 63, 64);
+  const uint32_t mlo = (uint32_t)mask, mhi = (uint32_t)(mask >> 32);
+  // wave-uniform trip count: every lane takes part in every shuffle
+  for (uint32_t base = lo; base < hi; base += 64) {
+    const uint32_t s = base + lane;
+    int L = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1)
+      if (__shfl(start, L + step, 64) <= s) L += step;
+    const uint32_t oi = __shfl(i, L, 64);
+    const uint32_t j = s - __shfl(start, L, 64);
+    const int ox0 = __shfl(x0, L, 64), oy0 = __shfl(y0, L, 64), orw = __shfl(rw, L, 64);
+    int pos = (int)j;
+    if (__shfl(use_mask, L, 64)) {
+      const uint64_t m = (uint64_t)__shfl(mlo, L, 64) | ((uint64_t)__shfl(mhi, L, 64) << 32);
+      if (s < hi) pos = select_bit(m, j);
+    }
+    if (s < hi) {
+      keys[s] = (uint32_t)((oy0 + pos / orw) * gx + ox0 + pos % orw);
+      vals[s] = oi;
+    }
+  }
 }
 
 __global__ void __launch_bounds__(kThreads)

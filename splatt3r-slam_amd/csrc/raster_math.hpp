@@ -54,6 +54,79 @@ GSR_HD void get_rect(float px, float py, int r, int gx, int gy, int* xmin, int* 
   *ymax = d < 0 ? 0 : (d > gy ? gy : d);
 }
 
+// Conservative tile culling.  A (Gaussian, tile) pair may be dropped only
+// when the blend skips the Gaussian at EVERY pixel of the tile, i.e.
+// o * exp(power) < 1/255 there (the reference's own per-pixel skip), with
+// power = -q/2, q = A dx^2 + 2B dx dy + C dy^2 (conic A, B, C).  Keeping a
+// pair is always safe, so every approximation below errs towards keeping:
+//  * thr = 2 ln(255 o) + 0.05: keep iff q_min <= thr (0.05 = 5 % in alpha,
+//    far above fexp's 2 ulp);
+//  * the blend's fp32 q is off by at most ~1e-6 (A dx^2 + C dy^2) <=
+//    1e-6 q / (1 - rho), rho = |B| / sqrt(AC); this test's own fp32 q_min
+//    has the same order of error, so q_min is scaled down by
+//    1e-4 / (1 - rho) (50x the sum) before comparing; rho >= 0.99 keeps all;
+//  * q_min is taken over the continuous pixel rectangle of the tile (a
+//    superset of its pixel centres): 0 if the mean lies inside, else the
+//    least of the four clamped edge minima;
+//  * the tiles tested are those of the reference rect that meet the
+//    ellipse's bounding box q <= thr / shrink (half-widths
+//    sqrt(t C / det), sqrt(t A / det)).
+// A dropped pair therefore contributes nothing at any pixel: image, final_T
+// and gradients stay bit-identical; only num_rendered shrinks.
+struct TileCull {
+  float thr, shrink;
+  int mode;   // 0 = test tiles, 1 = keep every rect tile, 2 = drop all
+  int x0, y0, x1, y1;   // candidate tile rect (subset of the reference rect)
+};
+
+GSR_HD TileCull tile_cull(float mx, float my, float A, float B, float C, float o, int rx0,
+                          int ry0, int rx1, int ry1) {
+  TileCull t;
+  t.x0 = rx0; t.y0 = ry0; t.x1 = rx1; t.y1 = ry1;
+  t.thr = 0.0f; t.shrink = 1.0f; t.mode = 1;
+  if (!(A > 0.0f) || !(C > 0.0f) || !(o > 0.0f)) return t;
+  const float rho = fabsf(B) / sqrtf(A * C);
+  if (!(rho < 0.99f)) return t;
+  const float thr = 2.0f * logf(255.0f * o) + 0.05f;
+  if (thr < 0.0f) { t.mode = 2; return t; }   // o < ~1/262: never blended
+  t.mode = 0;
+  t.thr = thr;
+  t.shrink = 1.0f - 1e-4f / (1.0f - rho);
+  const float det = A * C - B * B;
+  const float tt = thr / t.shrink * 1.001f;
+  const float hx = sqrtf(tt * C / det) + 1.0f, hy = sqrtf(tt * A / det) + 1.0f;
+  const int bx0 = (int)floorf((mx - hx) / BX), bx1 = (int)floorf((mx + hx) / BX) + 1;
+  const int by0 = (int)floorf((my - hy) / BY), by1 = (int)floorf((my + hy) / BY) + 1;
+  t.x0 = bx0 > rx0 ? bx0 : rx0;
+  t.x1 = bx1 < rx1 ? bx1 : rx1;
+  t.y0 = by0 > ry0 ? by0 : ry0;
+  t.y1 = by1 < ry1 ? by1 : ry1;
+  if (t.x1 < t.x0) t.x1 = t.x0;
+  if (t.y1 < t.y0) t.y1 = t.y0;
+  return t;
+}
+
+GSR_HD bool tile_hit(const TileCull& t, float mx, float my, float A, float B, float C, int tx,
+                     int ty, int W, int H) {
+  if (t.mode != 0) return t.mode == 1;
+  const float x0 = (float)(tx * BX), y0 = (float)(ty * BY);
+  const float x1 = fminf(x0 + (BX - 1), (float)(W - 1)), y1 = fminf(y0 + (BY - 1), (float)(H - 1));
+  // d = mean - pixel over [mx - x1, mx - x0] x [my - y1, my - y0]
+  const float ux0 = mx - x1, ux1 = mx - x0, vy0 = my - y1, vy1 = my - y0;
+  if (ux0 <= 0.0f && ux1 >= 0.0f && vy0 <= 0.0f && vy1 >= 0.0f) return true;
+  float qmin = 3.0e38f;
+  const float ux[2] = {ux0, ux1}, vy[2] = {vy0, vy1};
+  for (int e = 0; e < 2; ++e) {
+    const float u = ux[e];
+    const float v = fminf(fmaxf(-B * u / C, vy0), vy1);
+    qmin = fminf(qmin, A * u * u + 2.0f * B * u * v + C * v * v);
+    const float w = vy[e];
+    const float x = fminf(fmaxf(-B * w / A, ux0), ux1);
+    qmin = fminf(qmin, A * x * x + 2.0f * B * x * w + C * w * w);
+  }
+  return qmin * t.shrink <= t.thr;
+}
+
 // p (3) through a column-major 4x4 stored as the reference passes it.
 GSR_HD void xform43(const float* m, float x, float y, float z, float* o) {
   o[0] = m[0] * x + m[4] * y + m[8] * z + m[12];

@@ -150,6 +150,8 @@ class _RasterizeGaussians(torch.autograd.Function):
                    "gsr_render")
         ctx.raster_settings = raster_settings
         ctx.num_rendered = R
+        global last_num_rendered
+        last_num_rendered = R
         ctx.M = M
         ctx.has = (shc is not None, col is not None, sc is not None, cov is not None)
         ctx.save_for_backward(m3, shc if shc is not None else m3.new_empty(0),
@@ -225,6 +227,10 @@ class GaussianRasterizer(nn.Module):
         cov3D_precomp = e if cov3D_precomp is None else cov3D_precomp
         return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales,
                                    rotations, cov3D_precomp, rs)
+
+
+# tile instances (num_rendered) of the most recent forward (bench/diagnostics)
+last_num_rendered = 0
 
 
 def set_timing(enabled: bool) -> None:

@@ -38,6 +38,7 @@ def prepare(P, device="cuda", seed=0):
 
 
 def run(P=4_194_304, iters=10, warmup=3, backward=True, device="cuda"):
+    import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import GaussianRasterizer, last_timing, set_timing
     sc, rs, inputs, grad = prepare(P, device)
     H, W = sc["H"], sc["W"]
@@ -89,7 +90,7 @@ def run(P=4_194_304, iters=10, warmup=3, backward=True, device="cuda"):
     out = dict(P=P, H=H, W=W, fwd_ms=fwd, msplats_per_s=P / (fwd * 1e-3) / 1e6,
                fwd_GBps=fwd_bytes(P, H, W) / (fwd * 1e-3) / 1e9,
                phases_ms=dict(zip(["preprocess", "scan", "dup_sort", "ranges", "blend"], ph)),
-               num_rendered=None, visible=int((radii > 0).sum()))
+               num_rendered=int(dgr.last_num_rendered), visible=int((radii > 0).sum()))
     if backward:
         bwd = float(np.median(b_ms))
         out.update(bwd_ms=bwd, bwd_GBps=bwd_bytes(P, H, W) / (bwd * 1e-3) / 1e9)

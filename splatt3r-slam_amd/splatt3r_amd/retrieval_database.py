@@ -158,3 +158,40 @@ class RetrievalDatabase:
     def update(self, frame, add_after_query, k, min_thresh=0.0):
         raise NotImplementedError("RetrievalDatabase.update needs the ASMK inverted file "
                                   "(third-party `asmk`, CPU), which is not available")
+
+
+def bench(device, iters=20, C=65536, dim=1024, nfeat=300, k=5):
+    """Per-keyframe retrieval device work at the checkpoint's shapes
+    (synthetic weights): prep_features on [1,768,1024] and the query
+    quantisation of nfeat vectors against C centroids (k = 5)."""
+    g = torch.Generator(device="cpu").manual_seed(0)
+    W = (torch.randn(dim, 1024, generator=g) / 32.0).to(device)
+    b = torch.zeros(dim, device=device)
+    cen = torch.nn.functional.normalize(torch.randn(C, dim, generator=g), dim=1).to(device)
+    P = (torch.randn(1024, 1024, generator=g, dtype=torch.float64) / 32.0).to(device)
+    m = torch.zeros(1, 1024, dtype=torch.float64, device=device)
+    db = RetrievalDatabase(RetrievalWeights(W, b, cen, (m, P), (m, P), nfeat=nfeat), device)
+    feat = torch.randn(1, 768, 1024, device=device)
+    q = db.prep_features(feat)[0]
+    prm = {"quantize": {"multiple_assignment": k}}
+    for _ in range(3):
+        db.prep_features(feat)
+        db.quantize_custom(q, prm)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    t_prep = t_q = 0.0
+    for _ in range(iters):
+        ev[0].record()
+        db.prep_features(feat)
+        ev[1].record()
+        db.quantize_custom(q, prm)
+        ev[2].record()
+        torch.cuda.synchronize()
+        t_prep += ev[0].elapsed_time(ev[1])
+        t_q += ev[1].elapsed_time(ev[2])
+    t_prep /= iters
+    t_q /= iters
+    flops_q = 2.0 * nfeat * C * dim
+    return {"prep_features_ms": t_prep, "quantize_ms": t_q,
+            "quantize_tflops_fp32": flops_q / (t_q * 1e-3) / 1e12,
+            "shape": f"prep [1,768,1024]; quantize {nfeat}x{C}x{dim}, k={k}"}

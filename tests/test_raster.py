@@ -158,6 +158,10 @@ def test_hip_forward_c3_resolution_vs_oracle():
                         cov3D_precomp=sc["cov6"] * scale * scale, nthreads=16)
     np.testing.assert_array_equal(radii.cpu().numpy(), ref["radii"])
     np.testing.assert_array_equal(img.detach().cpu().numpy(), ref["color"])
+    # tile culling (raster_math.hpp tile_cull/tile_hit) drops only (Gaussian,
+    # tile) pairs the blend skips at every pixel: same image, fewer instances
+    import diff_gaussian_rasterization as dgr
+    assert 0 < dgr.last_num_rendered < ref["num_rendered"]
 
 
 @pytest.mark.gpu
