@@ -46,15 +46,20 @@ struct GeomState {
   float* cov3D;  // [P,6] (scale/rotation path)
   uint8_t* clamped;  // [P,3]
   uint32_t* tiles;
-  uint64_t* tmask;   // kept tiles of the rect (bit (y - y0) * w + (x - x0)), rects <= 64 tiles
+  // duplication record per Gaussian: x = x0 | y0 << 16, y = rect w | h << 16,
+  // z/w = kept-tile mask (bit (y - y0) * w + (x - x0)) for rects of 2..64
+  // tiles; one 16-B gather serves the depth-ordered passes
+  uint4* dup;
   uint32_t* offsets;
   void* scan_tmp;
   size_t scan_bytes;
   // depth-ordered duplication (gsr_render)
   uint32_t* dkey;          // depth bits (visible) / ~0u, index order
   uint32_t* dkey_sorted;
-  uint32_t* iota;
-  uint32_t* order;         // Gaussian index per depth rank (stable)
+  // sort values: Gaussian index | kept-tile count << 32, so the depth-ordered
+  // tile counts come out of the sort instead of a random gather
+  uint64_t* iota;
+  uint64_t* order;         // (index | count << 32) per depth rank (stable)
   uint32_t* tiles_sorted;  // tiles touched per depth rank
   uint32_t* offsets_sorted;
   void* dsort_tmp;
@@ -75,6 +80,13 @@ size_t key32_sort_temp_bytes(int64_t n) {
   return bytes;
 }
 
+size_t depth_sort_temp_bytes(int64_t n) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                     (uint64_t*)nullptr, (uint64_t*)nullptr, (int)n);
+  return bytes;
+}
+
 GeomState carve_geom(void* base, int64_t P) {
   Carver c{static_cast<char*>(base)};
   GeomState g;
@@ -85,28 +97,29 @@ GeomState carve_geom(void* base, int64_t P) {
   g.cov3D = c.take<float>(P * 6);
   g.clamped = c.take<uint8_t>(P * 3);
   g.tiles = c.take<uint32_t>(P);
-  g.tmask = c.take<uint64_t>(P);
+  g.dup = c.take<uint4>(P);
   g.offsets = c.take<uint32_t>(P);
   g.scan_bytes = scan_temp_bytes(P);
   g.scan_tmp = c.take<char>(g.scan_bytes);
   g.dkey = c.take<uint32_t>(P);
   g.dkey_sorted = c.take<uint32_t>(P);
-  g.iota = c.take<uint32_t>(P);
-  g.order = c.take<uint32_t>(P);
+  g.iota = c.take<uint64_t>(P);
+  g.order = c.take<uint64_t>(P);
   g.tiles_sorted = c.take<uint32_t>(P);
   g.offsets_sorted = c.take<uint32_t>(P);
-  g.dsort_bytes = key32_sort_temp_bytes(P);
+  g.dsort_bytes = depth_sort_temp_bytes(P);
   g.dsort_tmp = c.take<char>(g.dsort_bytes);
   return g;
 }
 size_t geom_bytes(int64_t P) {
   Carver c{nullptr};
   c.take<float>(P); c.take<float4>(P); c.take<float4>(P); c.take<float>(P * 3);
-  c.take<float>(P * 6); c.take<uint8_t>(P * 3); c.take<uint32_t>(P); c.take<uint64_t>(P);
+  c.take<float>(P * 6); c.take<uint8_t>(P * 3); c.take<uint32_t>(P); c.take<uint4>(P);
   c.take<uint32_t>(P);
   c.take<char>(scan_temp_bytes(P));
-  for (int k = 0; k < 6; ++k) c.take<uint32_t>(P);
-  c.take<char>(key32_sort_temp_bytes(P));
+  c.take<uint32_t>(P); c.take<uint32_t>(P); c.take<uint64_t>(P); c.take<uint64_t>(P);
+  c.take<uint32_t>(P); c.take<uint32_t>(P);
+  c.take<char>(depth_sort_temp_bytes(P));
   return c.off;
 }
 
@@ -194,6 +207,7 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
   if (i >= P) return;
   radii[i] = 0;
   g.tiles[i] = 0;
+  g.dup[i] = make_uint4(0u, 0u, 0u, 0u);
   const float mx = means[i * 3 + 0], my = means[i * 3 + 1], mz = means[i * 3 + 2];
   float pv[3];
   xform43(vm, mx, my, mz, pv);
@@ -255,9 +269,9 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
   // rects of <= 64 tiles: keep only the tiles the blend can use (tile_cull /
   // tile_hit, raster_math.hpp) as a bit mask; larger rects keep every tile
   const int rw = x1 - x0, area = rw * (y1 - y0);
-  uint64_t mask = ~0ull;
+  uint64_t mask = area == 1 ? 1ull : ~0ull;
   uint32_t n = (uint32_t)area;
-  if (area <= 64) {
+  if (area > 1 && area <= 64) {
     const float cA = c * det_inv, cB = -b * det_inv, cC = a * det_inv;
     const TileCull tc = tile_cull(px, py, cA, cB, cC, opac[i], x0, y0, x1, y1);
     mask = 0;
@@ -267,7 +281,9 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
           mask |= 1ull << ((y - y0) * rw + (x - x0));
     n = (uint32_t)__popcll(mask);
   }
-  g.tmask[i] = mask;
+  g.dup[i] = make_uint4((uint32_t)x0 | ((uint32_t)y0 << 16),
+                        (uint32_t)rw | ((uint32_t)(y1 - y0) << 16), (uint32_t)mask,
+                        (uint32_t)(mask >> 32));
   g.tiles[i] = n;
 }
 
@@ -279,83 +295,95 @@ k_depth_keys(int64_t P, GeomState g) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
   g.dkey[i] = g.tiles[i] > 0 ? __float_as_uint(g.depth[i]) : 0xFFFFFFFFu;
-  g.iota[i] = (uint32_t)i;
+  g.iota[i] = (uint64_t)i | ((uint64_t)g.tiles[i] << 32);
+}
+
+// tiles kept by Gaussian d (its duplication record)
+__device__ __forceinline__ uint32_t dup_count(const uint4 d) {
+  const uint32_t w = d.y & 0xFFFFu, h = d.y >> 16;
+  return w * h <= 64u ? (uint32_t)__popcll((uint64_t)d.z | ((uint64_t)d.w << 32)) : w * h;
 }
 
 __global__ void __launch_bounds__(kThreads)
 k_gather_tiles(int64_t P, GeomState g) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < P) g.tiles_sorted[k] = g.tiles[g.order[k]];
-}
-
-// Position of the j-th set bit of m (j < popcount(m)).
-__device__ __forceinline__ int select_bit(uint64_t m, uint32_t j) {
-  int base = 0;
-  uint32_t w = (uint32_t)m;
-  const uint32_t pc = (uint32_t)__popc(w);
-  if (j >= pc) { j -= pc; w = (uint32_t)(m >> 32); base = 32; }
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    const uint32_t c = (uint32_t)__popc(w & 0xFFu);
-    if (j < c) break;
-    j -= c; w >>= 8; base += 8;
-  }
-  for (uint32_t t = 0; t < j; ++t) w &= w - 1;
-  return base + __builtin_ctz(w);
+  if (k < P) g.tiles_sorted[k] = (uint32_t)(g.order[k] >> 32);
 }
 
 // Instances in depth order: the wave's 64 depth ranks k own the contiguous
-// output range [start(k0), end(k0 + 63)); each lane writes every 64th slot
-// of it (coalesced stores), finding the owning rank by a shuffle binary
-// search over the lanes' start offsets and its tile from the rank's kept-
-// tile mask.  A stable sort by tile id then yields the reference's
-// (tile, depth, index) order (rasterizer_impl.cu duplicateWithKeys +
-// SortPairs over tile<<32 | depth): equal depths keep index order from the
-// stable depth sort.
+// output range [start(k0), end(k0 + 63)).  It is produced in chunks of DCH
+// slots: every lane enumerates its own instances that fall in the chunk
+// (kept-tile mask bits in rect order, or the plain rect for rects of more
+// than 64 tiles) into the wave's LDS slice, then the wave copies the slice
+// out with coalesced stores.  A stable sort by tile id then yields the
+// reference's (tile, depth, index) order (rasterizer_impl.cu
+// duplicateWithKeys + SortPairs over tile<<32 | depth): equal depths keep
+// index order from the stable depth sort.
+constexpr int DCH = 512;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ void __launch_bounds__(kThreads)
 k_duplicate(int64_t P, int gx, int gy, const int32_t* __restrict__ radii, GeomState g,
             uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  __shared__ uint32_t s_key[kThreads / 64][DCH];
+  __shared__ uint32_t s_val[kThreads / 64][DCH];
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t i = 0, cnt = 0, start = g.offsets_sorted[P - 1];
   int x0 = 0, y0 = 0, rw = 1;
   uint64_t mask = 0;
-  int use_mask = 0;
+  bool use_mask = false;
   if (k < P) {
-    i = g.order[k];
-    cnt = g.tiles_sorted[k];
+    const uint64_t o = g.order[k];
+    i = (uint32_t)o;
+    cnt = (uint32_t)(o >> 32);
     start = k == 0 ? 0u : g.offsets_sorted[k - 1];
     if (cnt > 0) {
-      const float4 r0 = g.rec0[i];
-      int x1, y1;
-      get_rect(r0.x, r0.y, radii[i], gx, gy, &x0, &y0, &x1, &y1);
-      rw = x1 - x0;
-      use_mask = rw * (y1 - y0) <= 64;
-      mask = g.tmask[i];
+      const uint4 d = g.dup[i];
+      x0 = (int)(d.x & 0xFFFFu);
+      y0 = (int)(d.x >> 16);
+      rw = (int)(d.y & 0xFFFFu);
+      use_mask = rw * (int)(d.y >> 16) <= 64;
+      mask = (uint64_t)d.z | ((uint64_t)d.w << 32);
     }
   }
   const uint32_t lo = __shfl(start, 0, 64);
   const uint32_t hi = __shfl(start + cnt, 63, 64);
-  const uint32_t mlo = (uint32_t)mask, mhi = (uint32_t)(mask >> 32);
-  // wave-uniform trip count: every lane takes part in every shuffle
-  for (uint32_t base = lo; base < hi; base += 64) {
-    const uint32_t s = base + lane;
-    int L = 0;
-#pragma unroll
-    for (int step = 32; step > 0; step >>= 1)
-      if (__shfl(start, L + step, 64) <= s) L += step;
-    const uint32_t oi = __shfl(i, L, 64);
-    const uint32_t j = s - __shfl(start, L, 64);
-    const int ox0 = __shfl(x0, L, 64), oy0 = __shfl(y0, L, 64), orw = __shfl(rw, L, 64);
-    int pos = (int)j;
-    if (__shfl(use_mask, L, 64)) {
-      const uint64_t m = (uint64_t)__shfl(mlo, L, 64) | ((uint64_t)__shfl(mhi, L, 64) << 32);
-      if (s < hi) pos = select_bit(m, j);
+  uint32_t* sk = s_key[w];
+  uint32_t* sv = s_val[w];
+  for (uint32_t c0 = lo; c0 < hi; c0 += DCH) {
+    const uint32_t c1 = min(c0 + (uint32_t)DCH, hi);
+    if (cnt > 0 && start < c1 && start + cnt > c0) {
+      if (use_mask) {
+        uint64_t m = mask;
+        const uint32_t e = min(c1, start + cnt);
+        for (uint32_t s = start; m && s < e; ++s) {
+          const int pos = __builtin_ctzll(m);
+          m &= m - 1;
+          if (s >= c0) {
+            sk[s - c0] = (uint32_t)((y0 + pos / rw) * gx + x0 + pos % rw);
+            sv[s - c0] = i;
+          }
+        }
+      } else {
+        const uint32_t j0 = max(c0, start) - start, j1 = min(c1, start + cnt) - start;
+        for (uint32_t j = j0; j < j1; ++j) {
+          sk[start + j - c0] = (uint32_t)((y0 + (int)j / rw) * gx + x0 + (int)j % rw);
+          sv[start + j - c0] = i;
+        }
+      }
     }
-    if (s < hi) {
-      keys[s] = (uint32_t)((oy0 + pos / orw) * gx + ox0 + pos % orw);
-      vals[s] = oi;
+    wave_lds_sync();
+    for (uint32_t t = lane; t < c1 - c0; t += 64) {
+      keys[c0 + t] = sk[t];
+      vals[c0 + t] = sv[t];
     }
+    wave_lds_sync();
   }
 }
 

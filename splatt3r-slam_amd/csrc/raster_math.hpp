@@ -74,7 +74,7 @@ GSR_HD void get_rect(float px, float py, int r, int gx, int gy, int* xmin, int* 
 // A dropped pair therefore contributes nothing at any pixel: image, final_T
 // and gradients stay bit-identical; only num_rendered shrinks.
 struct TileCull {
-  float thr, shrink;
+  float thr, shrink, inv_a, inv_c;
   int mode;   // 0 = test tiles, 1 = keep every rect tile, 2 = drop all
   int x0, y0, x1, y1;   // candidate tile rect (subset of the reference rect)
 };
@@ -84,6 +84,7 @@ GSR_HD TileCull tile_cull(float mx, float my, float A, float B, float C, float o
   TileCull t;
   t.x0 = rx0; t.y0 = ry0; t.x1 = rx1; t.y1 = ry1;
   t.thr = 0.0f; t.shrink = 1.0f; t.mode = 1;
+  t.inv_a = 0.0f; t.inv_c = 0.0f;
   if (!(A > 0.0f) || !(C > 0.0f) || !(o > 0.0f)) return t;
   const float rho = fabsf(B) / sqrtf(A * C);
   if (!(rho < 0.99f)) return t;
@@ -91,6 +92,10 @@ GSR_HD TileCull tile_cull(float mx, float my, float A, float B, float C, float o
   if (thr < 0.0f) { t.mode = 2; return t; }   // o < ~1/262: never blended
   t.mode = 0;
   t.thr = thr;
+  // reciprocals for the edge minimisers: an inexact minimiser location
+  // changes q only to second order (C dv^2), far inside the 0.05 margin
+  t.inv_a = 1.0f / A;
+  t.inv_c = 1.0f / C;
   t.shrink = 1.0f - 1e-4f / (1.0f - rho);
   const float det = A * C - B * B;
   const float tt = thr / t.shrink * 1.001f;
@@ -118,10 +123,10 @@ GSR_HD bool tile_hit(const TileCull& t, float mx, float my, float A, float B, fl
   const float ux[2] = {ux0, ux1}, vy[2] = {vy0, vy1};
   for (int e = 0; e < 2; ++e) {
     const float u = ux[e];
-    const float v = fminf(fmaxf(-B * u / C, vy0), vy1);
+    const float v = fminf(fmaxf(-B * u * t.inv_c, vy0), vy1);
     qmin = fminf(qmin, A * u * u + 2.0f * B * u * v + C * v * v);
     const float w = vy[e];
-    const float x = fminf(fmaxf(-B * w / A, ux0), ux1);
+    const float x = fminf(fmaxf(-B * w * t.inv_a, ux0), ux1);
     qmin = fminf(qmin, A * x * x + 2.0f * B * x * w + C * w * w);
   }
   return qmin * t.shrink <= t.thr;

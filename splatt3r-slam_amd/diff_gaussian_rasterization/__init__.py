@@ -132,8 +132,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         s, keep = _settings_struct(raster_settings, dev)
         stream = _lib.stream(dev)
         L = _lib.lib()
-        color = torch.zeros(3, H, W, device=dev, dtype=torch.float32)
-        radii = torch.zeros(P, device=dev, dtype=torch.int32)
+        # every pixel / radius is written by gsr_render / gsr_preprocess
+        color = torch.empty(3, H, W, device=dev, dtype=torch.float32)
+        radii = torch.empty(P, device=dev, dtype=torch.int32)
         geom = torch.empty(int(L.gsr_geom_bytes(P)), device=dev, dtype=torch.uint8)
         img = torch.empty(int(L.gsr_image_bytes(H, W)), device=dev, dtype=torch.uint8)
         nr = ctypes.c_int64(0)
