@@ -472,6 +472,26 @@ k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
 }
 
 // ----------------------------------------------------------- backward -----
+struct ZeroList {
+  float* p[10];
+  int64_t n[10];
+  int cnt;
+};
+
+// grid (chunks, list entries): zero every listed array, 16 B per store
+// where the base is 16-B aligned
+__global__ void __launch_bounds__(kThreads) k_zero_multi(ZeroList z) {
+  float* __restrict__ p = z.p[blockIdx.y];
+  const int64_t n = z.n[blockIdx.y];
+  const int64_t i0 = ((int64_t)blockIdx.x * kThreads + threadIdx.x) * 4;
+  if (i0 >= n) return;
+  if (i0 + 4 <= n && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    *reinterpret_cast<float4*>(p + i0) = make_float4(0.f, 0.f, 0.f, 0.f);
+  } else {
+    for (int64_t e = i0; e < n && e < i0 + 4; ++e) p[e] = 0.0f;
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -668,7 +688,24 @@ k_preprocess_backward(int64_t P, Cam cam, const float* __restrict__ means,
                       float* __restrict__ dL_dsh, float* __restrict__ dL_dscale,
                       float* __restrict__ dL_drot) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P || !(radii[i] > 0)) return;
+  if (i >= P) return;
+  if (!(radii[i] > 0)) {
+    // culled: every per-Gaussian gradient is zero (written here, so the
+    // caller's buffers need no memset)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dL_dmeans[i * 3 + k] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) dL_dcov[i * 6 + k] = 0.f;
+    if (shs)
+      for (int k = 0; k < cam.M * 3; ++k) dL_dsh[i * (int64_t)cam.M * 3 + k] = 0.f;
+    if (scales && dL_dscale) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dL_dscale[i * 3 + k] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dL_drot[i * 4 + k] = 0.f;
+    }
+    return;
+  }
   const float mx = means[i * 3 + 0], my = means[i * 3 + 1], mz = means[i * 3 + 2];
   const float* cov3 = cov_pre ? cov_pre + i * 6 : g.cov3D + i * 6;
   Ewa e = ewa_project(mx, my, mz, cov3, vm, cam.fx, cam.fy, cam.tanfx, cam.tanfy);
@@ -960,19 +997,22 @@ int gsr_backward(const gsr_settings* s, int64_t P, int M, int64_t R, const float
   (void)colors_precomp;
   (void)opacities;
   hipStream_t st = s3::as_stream(stream);
-  auto zero = [&](float* p, size_t n) -> hipError_t {
-    return p ? hipMemsetAsync(p, 0, n * sizeof(float), st) : hipSuccess;
+  // the accumulated gradient outputs start at zero: one launch for all
+  ZeroList zl{};
+  auto add = [&](float* p, int64_t n) {
+    if (p && n > 0) { zl.p[zl.cnt] = p; zl.n[zl.cnt] = n; ++zl.cnt; }
   };
-  S3_HIP(zero(dL_dmeans2D, P * 3));
-  S3_HIP(zero(dL_dconic, P * 4));
-  S3_HIP(zero(dL_dopacity, P));
-  S3_HIP(zero(dL_dcolors, P * 3));
-  S3_HIP(zero(dL_dmeans3D, P * 3));
-  S3_HIP(zero(dL_dcov3D, P * 6));
-  if (shs) S3_HIP(zero(dL_dsh, P * (size_t)M * 3));
-  if (scales) {
-    S3_HIP(zero(dL_dscales, P * 3));
-    S3_HIP(zero(dL_drotations, P * 4));
+  // (only the blend's atomic accumulators: k_preprocess_backward writes
+  // every element of the per-Gaussian outputs, zeros for culled ones)
+  add(dL_dmeans2D, P * 3);
+  add(dL_dconic, P * 4);
+  add(dL_dopacity, P);
+  add(dL_dcolors, P * 3);
+  if (zl.cnt > 0) {
+    int64_t nmax = 0;
+    for (int k = 0; k < zl.cnt; ++k) nmax = zl.n[k] > nmax ? zl.n[k] : nmax;
+    k_zero_multi<<<dim3((unsigned)s3::cdiv(nmax, kThreads * 4), zl.cnt), kThreads, 0, st>>>(zl);
+    S3_LAUNCH_CHECK();
   }
   if (P == 0) return S3_OK;
   const int W = s->image_width, H = s->image_height;

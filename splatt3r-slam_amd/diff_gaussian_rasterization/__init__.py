@@ -177,7 +177,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         P, M, R = m3.shape[0], ctx.M, ctx.num_rendered
         s, keep = _settings_struct(ctx.raster_settings, dev)
         g = grad_out_color.detach().to(torch.float32).contiguous()
-        z = lambda *shape: torch.zeros(*shape, device=dev, dtype=torch.float32)
+        # gsr_backward zeroes every gradient output itself (one launch)
+        z = lambda *shape: torch.empty(*shape, device=dev, dtype=torch.float32)
         dm2, dconic, dop, dcol = z(P, 3), z(P, 4), z(P, 1), z(P, 3)
         dm3, dcov = z(P, 3), z(P, 6)
         dsh = z(P, M, 3) if has_sh else None
