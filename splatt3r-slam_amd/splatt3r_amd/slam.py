@@ -71,7 +71,15 @@ class Frontend:
         self.new_kf_frames: list[int] = []
         self.stats = dict(frames=0, tracked=0, reloc=0, keyframes=0, gn_iters=0,
                           gaussians_world=0, rendered=0)
-        self.last_render = None
+        self._last_render = None
+        # host read-back of the render: double-buffered pinned images filled by
+        # async D2H copies; `last_render` waits for the copy on access, so the
+        # host is not stalled inside the frame (the reference writes the PNG
+        # synchronously, main.py:501-506)
+        self._rb_bufs = None
+        self._rb_events = [None, None]
+        self._rb_i = 0
+        self._rb_event = None
         self.fps_timer = None
         self.enc_stream = torch.cuda.Stream(device=device) if torch.cuda.is_available() else None
         self._queue = {}           # frame index -> (Frame whose encoder is queued, done event)
@@ -117,15 +125,36 @@ class Frontend:
         frame.T_WC = T_WC
         return frame
 
+    @property
+    def last_render(self):
+        if self._rb_event is not None:
+            self._rb_event.synchronize()
+        return self._last_render
+
     def _render(self, frame, ref, target):
         if not self.render:
             return
         img = splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=target)
         if img is not None:
             self.stats["rendered"] += 1
-            self.last_render = img[0, 0].clamp(0, 1).permute(1, 2, 0)
-            if self.readback:
-                self.last_render = self.last_render.cpu()
+            out = img[0, 0].clamp(0, 1).permute(1, 2, 0)
+            if not self.readback:
+                self._last_render, self._rb_event = out, None
+                return
+            if self._rb_bufs is None or self._rb_bufs[0].shape != out.shape:
+                self._rb_bufs = [torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
+                                 for _ in range(2)]
+                self._rb_events = [None, None]
+            k = self._rb_i
+            self._rb_i ^= 1
+            if self._rb_events[k] is not None:      # copy of two frames ago
+                self._rb_events[k].synchronize()
+            host = self._rb_bufs[k]
+            host.copy_(out, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._rb_events[k] = ev
+            self._last_render, self._rb_event = host, ev
 
     def _to_world(self, frame):
         gs = gaussians_to_world(frame, **self.gs_args)
