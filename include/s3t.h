@@ -46,6 +46,32 @@ int s3t_gn_iterations(const float* Xf, const float* Xk, const float* Q, const ui
                       int max_iters, float rel_error, float delta_norm, float* T /* device [8] */,
                       double* state, void* workspace, float* out36, void* stream);
 
+/* Calibrated tracker (FrameTracker.opt_pose_calib_sim3, tracker.py:216-270;
+ * residuals of geometry.project_calib :63-104).  Per keyframe pixel i
+ * (n = h*w, pixel (i % w, i / w)):
+ *   p = T . Xf_i,  pz = (K p).xy / (K p).z, log p.z   (log z := 0 if z <= depth_eps)
+ *   meas = (i % w, i / w, log Xk_i.z), zeroed where Xk_i.z <= depth_eps
+ *   r = meas - pz,  J = -dpz/dp [I, -[p]x, p]
+ *   sqrt_info = (1/sigma_pixel x2, 1/sigma_depth) * valid_i * sqrt(Q_i)
+ *               * [border < u < w-1-border, border < v < h-1-border,
+ *                  p.z > depth_eps, Xk_i.z > depth_eps]
+ * Xf is the ray-constrained frame pointmap gathered by idx_f2k, Xk the
+ * keyframe pointmap (only its z is read).  K is a HOST float[9] (row-major
+ * 3x3).  Output layout and the device GN loop are those of the ray variant
+ * above. */
+int s3t_calib_normal_eqs(const float* T /* device [8] */, const float* Xf, const float* Xk,
+                         const float* Q, const uint8_t* valid, int64_t n, const float* K,
+                         int h, int w, float pixel_border, float depth_eps, float sigma_pixel,
+                         float sigma_depth, float huber_k, void* workspace, float* out36,
+                         void* stream);
+
+int s3t_gn_iterations_calib(const float* Xf, const float* Xk, const float* Q,
+                            const uint8_t* valid, int64_t n, const float* K, int h, int w,
+                            float pixel_border, float depth_eps, float sigma_pixel,
+                            float sigma_depth, float huber_k, int iters, int max_iters,
+                            float rel_error, float delta_norm, float* T /* device [8] */,
+                            double* state, void* workspace, float* out36, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

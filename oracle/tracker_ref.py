@@ -6,6 +6,9 @@ check the fused HIP normal-equation kernel (s3t_ray_dist_normal_eqs).
   point_to_ray_dist (+ Jacobian)      geometry.py:17-34
   huber                               nonlinear_optimizer.py:28-33
   solve / opt_pose_ray_dist_sim3      tracker.py:156-214
+  project_calib (+ Jacobian)          geometry.py:63-104
+  get_points_poses (calib branch)     tracker.py:142-151
+  opt_pose_calib_sim3                 tracker.py:216-270
 """
 from __future__ import annotations
 
@@ -62,6 +65,62 @@ def normal_equations(T, Xf, Xk, Q, valid, sigma_ray, sigma_dist, k):
     J = -D @ dXdT
     sq = np.sqrt(Q.astype(np.float64).reshape(-1, 1)) * valid.reshape(-1, 1)
     si = np.concatenate([np.repeat(sq / sigma_ray, 3, 1), sq / sigma_dist], 1)
+    rob = si * np.sqrt(huber(si * r, k))
+    A = (rob[..., None] * J).reshape(-1, 7)
+    b = (rob * r).reshape(-1, 1)
+    return A.T @ A, (-A.T @ b)[:, 0], 0.5 * float((b * b).sum())
+
+
+def project_calib(P, K, img_size, border=0.0, z_eps=0.0):
+    """geometry.py:63-104 -> pz [n,3] (u, v, log z), dpz/dP [n,3,3], valid [n]."""
+    K = np.asarray(K, np.float64)
+    q = P @ K.T
+    uv = q[:, :2] / q[:, 2:3]
+    h, w = img_size
+    z = P[:, 2]
+    valid = ((uv[:, 0] > border) & (uv[:, 0] < w - 1 - border) &
+             (uv[:, 1] > border) & (uv[:, 1] < h - 1 - border) & (z > z_eps))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        logz = np.where(z > z_eps, np.log(np.where(z > z_eps, z, 1.0)), 0.0)
+    fx, fy = K[0, 0], K[1, 1]
+    zi = 1.0 / z
+    D = np.zeros((P.shape[0], 3, 3))
+    D[:, 0, 0] = fx * zi
+    D[:, 1, 1] = fy * zi
+    D[:, 0, 2] = -fx * P[:, 0] * zi * zi
+    D[:, 1, 2] = -fy * P[:, 1] * zi * zi
+    D[:, 2, 2] = zi
+    return np.concatenate([uv, logz[:, None]], 1), D, valid
+
+
+def calib_measurements(Xk, img_size, depth_eps):
+    """tracker.py:145-151: pixel grid (u, v) + log z of the keyframe
+    pointmap, zeroed where z <= depth_eps."""
+    h, w = img_size
+    v, u = np.divmod(np.arange(h * w), w)
+    z = Xk[:, 2].astype(np.float64)
+    ok = z > depth_eps
+    meas = np.stack([u, v, np.log(np.where(ok, z, 1.0))], 1).astype(np.float64)
+    meas[~ok] = 0.0
+    return meas, ok
+
+
+def normal_equations_calib(T, Xf, Xk, Q, valid, K, img_size, pixel_border, depth_eps,
+                           sigma_pixel, sigma_depth, k):
+    """One GN iteration of opt_pose_calib_sim3 (tracker.py:219-246):
+    H (7x7), g (7), cost.  Xf: ray-constrained frame points gathered by
+    idx_f2k; Xk: keyframe pointmap (its z gives the log-depth measurement)."""
+    Xf = Xf.astype(np.float64)
+    p = act_sim3(T, Xf)
+    dXdT = np.concatenate([np.broadcast_to(np.eye(3), (p.shape[0], 3, 3)), -skew(p),
+                           p[:, :, None]], -1)
+    pz, D, vproj = project_calib(p, K, img_size, pixel_border, depth_eps)
+    meas, vmeas = calib_measurements(Xk, img_size, depth_eps)
+    r = meas - pz
+    J = -D @ dXdT
+    sq = np.sqrt(Q.astype(np.float64).reshape(-1, 1)) * valid.reshape(-1, 1)
+    si = np.concatenate([np.repeat(sq / sigma_pixel, 2, 1), sq / sigma_depth], 1)
+    si = si * (vproj & vmeas)[:, None]
     rob = si * np.sqrt(huber(si * r, k))
     A = (rob[..., None] * J).reshape(-1, 7)
     b = (rob * r).reshape(-1, 1)

@@ -14,11 +14,58 @@ constexpr int kThreads = 256;
 constexpr int kMaxBlocks = 1024;
 constexpr int NV = 36;  // 28 (H upper) + 7 (g) + 1 (cost)
 
+// Calibrated variant parameters (tracker.py:216-270, geometry.project_calib
+// :63-104): K row-major 3x3, image size, pixel border, z_eps (projection
+// and keyframe-measurement validity both use it, tracker.py:148-151).
+struct CalibP {
+  float K[9];
+  int h, w;
+  float border, z_eps;
+};
+
+constexpr int kRayDist = 0, kCalib = 1;
+
+// Per-row accumulation of one whitened residual row into the 36 sums.
+__device__ __forceinline__ void accum_row(float* acc, const float* J, float r, float si,
+                                          float hk) {
+  const float wr = si * r;
+  const float aw = fabsf(wr);
+  const float hw = aw < hk ? 1.0f : hk / aw;
+  const float rob = si * sqrtf(hw);
+  const float bb = rob * r;
+  float A[7];
+#pragma unroll
+  for (int c = 0; c < 7; ++c) A[c] = rob * J[c];
+  int q = 0;
+#pragma unroll
+  for (int a = 0; a < 7; ++a)
+#pragma unroll
+    for (int b = a; b < 7; ++b) acc[q++] += A[a] * A[b];
+#pragma unroll
+  for (int a = 0; a < 7; ++a) acc[28 + a] -= A[a] * bb;
+  acc[35] += 0.5f * bb * bb;
+}
+
+// J row = -D [I, -[p]x, p] for one row D (3) of the measurement Jacobian.
+__device__ __forceinline__ void jac_row(const float* D, const float* p, float* J) {
+  const float nsk[3][3] = {{0.f, p[2], -p[1]}, {-p[2], 0.f, p[0]}, {p[1], -p[0], 0.f}};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) J[c] = -D[c];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) J[3 + c] = -(D[0] * nsk[0][c] + D[1] * nsk[1][c] + D[2] * nsk[2][c]);
+  J[6] = -(D[0] * p[0] + D[1] * p[1] + D[2] * p[2]);
+}
+
+// MODE kRayDist: inv_a = 1/sigma_ray, inv_b = 1/sigma_dist (4 rows / point).
+// MODE kCalib:   inv_a = 1/sigma_pixel, inv_b = 1/sigma_depth (3 rows:
+// u, v, log z); Xk is the ray-constrained keyframe pointmap, its pixel grid
+// and log depth are the measurement (tracker.py:143-151).
+template <int MODE>
 __global__ void __launch_bounds__(kThreads)
 k_normal_eqs(const double* __restrict__ state, const float* __restrict__ Tdev,
              const float* __restrict__ Xf, const float* __restrict__ Xk,
              const float* __restrict__ Q, const uint8_t* __restrict__ valid, int64_t n,
-             float inv_sr, float inv_sd, float hk, float* __restrict__ partial) {
+             float inv_a, float inv_b, float hk, CalibP cp, float* __restrict__ partial) {
   if (state && state[2] != 0.0) return;   // the device-side GN loop has finished
   float T[8];
 #pragma unroll
@@ -31,52 +78,62 @@ k_normal_eqs(const double* __restrict__ state, const float* __restrict__ Tdev,
     float x[3] = {Xf[i * 3 + 0], Xf[i * 3 + 1], Xf[i * 3 + 2]};
     float p[3];
     s3lie::act_sim3(T, x, p);
-    const float d = sqrtf(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
-    const float di = 1.0f / d;
-    const float rf[3] = {di * p[0], di * p[1], di * p[2]};
-    const float xk[3] = {Xk[i * 3 + 0], Xk[i * 3 + 1], Xk[i * 3 + 2]};
-    const float dk = sqrtf(xk[0] * xk[0] + xk[1] * xk[1] + xk[2] * xk[2]);
-    const float dki = 1.0f / dk;
-    float r[4] = {dki * xk[0] - rf[0], dki * xk[1] - rf[1], dki * xk[2] - rf[2], dk - d};
-    // drd/dp: rows 0..2 = di (I - di^2 p p^T), row 3 = rf^T
-    const float di2 = di * di;
-    float Dm[4][3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) Dm[a][b] = di * ((a == b ? 1.0f : 0.0f) - di2 * p[a] * p[b]);
-    Dm[3][0] = rf[0]; Dm[3][1] = rf[1]; Dm[3][2] = rf[2];
-    // J = -Dm [I, -[p]x, p]:  -[p]x = [[0, z, -y], [-z, 0, x], [y, -x, 0]]
-    const float nsk[3][3] = {{0.f, p[2], -p[1]}, {-p[2], 0.f, p[0]}, {p[1], -p[0], 0.f}};
     const float sq = sqrtf(Q[i]);
     const float vv = valid[i] ? 1.0f : 0.0f;
-    const float si_r = inv_sr * vv * sq, si_d = inv_sd * vv * sq;
+    if constexpr (MODE == kRayDist) {
+      const float d = sqrtf(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+      const float di = 1.0f / d;
+      const float rf[3] = {di * p[0], di * p[1], di * p[2]};
+      const float xk[3] = {Xk[i * 3 + 0], Xk[i * 3 + 1], Xk[i * 3 + 2]};
+      const float dk = sqrtf(xk[0] * xk[0] + xk[1] * xk[1] + xk[2] * xk[2]);
+      const float dki = 1.0f / dk;
+      float r[4] = {dki * xk[0] - rf[0], dki * xk[1] - rf[1], dki * xk[2] - rf[2], dk - d};
+      // drd/dp: rows 0..2 = di (I - di^2 p p^T), row 3 = rf^T
+      const float di2 = di * di;
+      float Dm[4][3];
 #pragma unroll
-    for (int row = 0; row < 4; ++row) {
-      float J[7];
+      for (int a = 0; a < 3; ++a)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) J[c] = -Dm[row][c];
+        for (int b = 0; b < 3; ++b) Dm[a][b] = di * ((a == b ? 1.0f : 0.0f) - di2 * p[a] * p[b]);
+      Dm[3][0] = rf[0]; Dm[3][1] = rf[1]; Dm[3][2] = rf[2];
+      const float si_r = inv_a * vv * sq, si_d = inv_b * vv * sq;
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-        J[3 + c] = -(Dm[row][0] * nsk[0][c] + Dm[row][1] * nsk[1][c] + Dm[row][2] * nsk[2][c]);
-      J[6] = -(Dm[row][0] * p[0] + Dm[row][1] * p[1] + Dm[row][2] * p[2]);
-      const float si = row < 3 ? si_r : si_d;
-      const float wr = si * r[row];
-      const float aw = fabsf(wr);
-      const float hw = aw < hk ? 1.0f : hk / aw;
-      const float rob = si * sqrtf(hw);
-      const float bb = rob * r[row];
-      float A[7];
+      for (int row = 0; row < 4; ++row) {
+        float J[7];
+        jac_row(Dm[row], p, J);
+        accum_row(acc, J, r[row], row < 3 ? si_r : si_d, hk);
+      }
+    } else {
+      // project_calib: p' = K p, (u, v) = p'.xy / p'.z
+      const float* K = cp.K;
+      const float q0 = K[0] * p[0] + K[1] * p[1] + K[2] * p[2];
+      const float q1 = K[3] * p[0] + K[4] * p[1] + K[5] * p[2];
+      const float q2 = K[6] * p[0] + K[7] * p[1] + K[8] * p[2];
+      const float u = q0 / q2, v = q1 / q2;
+      const bool vz = p[2] > cp.z_eps;
+      const bool vproj = (u > cp.border) && (u < (float)(cp.w - 1) - cp.border) &&
+                         (v > cp.border) && (v < (float)(cp.h - 1) - cp.border) && vz;
+      const float logz = vz ? logf(p[2]) : 0.0f;
+      // keyframe measurement: pixel grid + log depth, zeroed where invalid
+      const float zk = Xk[i * 3 + 2];
+      const bool vmeas = zk > cp.z_eps;
+      const int64_t pix_v = i / cp.w, pix_u = i - pix_v * cp.w;
+      const float mu = vmeas ? (float)pix_u : 0.f, mv = vmeas ? (float)pix_v : 0.f;
+      const float mz = vmeas ? logf(zk) : 0.f;
+      const float r[3] = {mu - u, mv - v, mz - logz};
+      const float fx = K[0], fy = K[4];
+      const float zi = 1.0f / p[2];
+      const float Dm[3][3] = {{fx * zi, 0.f, -fx * p[0] * zi * zi},
+                              {0.f, fy * zi, -fy * p[1] * zi * zi},
+                              {0.f, 0.f, zi}};
+      const float v2 = (vproj && vmeas) ? 1.0f : 0.0f;
+      const float si_p = v2 * (inv_a * vv * sq), si_z = v2 * (inv_b * vv * sq);
 #pragma unroll
-      for (int c = 0; c < 7; ++c) A[c] = rob * J[c];
-      int q = 0;
-#pragma unroll
-      for (int a = 0; a < 7; ++a)
-#pragma unroll
-        for (int b = a; b < 7; ++b) acc[q++] += A[a] * A[b];
-#pragma unroll
-      for (int a = 0; a < 7; ++a) acc[28 + a] -= A[a] * bb;
-      acc[35] += 0.5f * bb * bb;
+      for (int row = 0; row < 3; ++row) {
+        float J[7];
+        jac_row(Dm[row], p, J);
+        accum_row(acc, J, r[row], row < 2 ? si_p : si_z, hk);
+      }
     }
   }
   // block reduction: wave shuffles, then 4 wave partials through LDS
@@ -189,8 +246,9 @@ extern "C" int s3t_ray_dist_normal_eqs(const float* T, const float* Xf, const fl
   const int nb = blocks_for(n);
   float* partial = static_cast<float*>(workspace);
   // reference: sqrt_info = 1 / sigma * valid * sqrt(Q)  (tracker.py:175-176)
-  k_normal_eqs<<<nb, kThreads, 0, st>>>(nullptr, T, Xf, Xk, Q, valid, n, 1.0f / sigma_ray,
-                                       1.0f / sigma_dist, huber_k, partial);
+  k_normal_eqs<kRayDist><<<nb, kThreads, 0, st>>>(nullptr, T, Xf, Xk, Q, valid, n,
+                                                 1.0f / sigma_ray, 1.0f / sigma_dist, huber_k,
+                                                 CalibP{}, partial);
   S3_LAUNCH_CHECK();
   k_finalize<<<NV, kThreads, 0, st>>>(nullptr, partial, nb, out36);
   S3_LAUNCH_CHECK();
@@ -208,8 +266,73 @@ extern "C" int s3t_gn_iterations(const float* Xf, const float* Xk, const float* 
   const int nb = blocks_for(n);
   float* partial = static_cast<float*>(workspace);
   for (int i = 0; i < iters; ++i) {
-    k_normal_eqs<<<nb, kThreads, 0, st>>>(state, T, Xf, Xk, Q, valid, n, 1.0f / sigma_ray,
-                                         1.0f / sigma_dist, huber_k, partial);
+    k_normal_eqs<kRayDist><<<nb, kThreads, 0, st>>>(state, T, Xf, Xk, Q, valid, n,
+                                                   1.0f / sigma_ray, 1.0f / sigma_dist, huber_k,
+                                                   CalibP{}, partial);
+    S3_LAUNCH_CHECK();
+    k_finalize<<<NV, kThreads, 0, st>>>(state, partial, nb, out36);
+    S3_LAUNCH_CHECK();
+    k_gn_solve<<<1, 64, 0, st>>>(out36, T, state, max_iters, rel_error, delta_norm);
+    S3_LAUNCH_CHECK();
+  }
+  return S3_OK;
+}
+
+namespace {
+
+int make_calib(const float* K, int h, int w, float pixel_border, float depth_eps, CalibP* cp) {
+  S3_REQUIRE(K && h > 0 && w > 0, "s3t calib: K, h > 0, w > 0 required");
+  for (int k = 0; k < 9; ++k) cp->K[k] = K[k];
+  cp->h = h;
+  cp->w = w;
+  cp->border = pixel_border;
+  cp->z_eps = depth_eps;
+  return S3_OK;
+}
+
+}  // namespace
+
+extern "C" int s3t_calib_normal_eqs(const float* T, const float* Xf, const float* Xk,
+                                    const float* Q, const uint8_t* valid, int64_t n,
+                                    const float* K, int h, int w, float pixel_border,
+                                    float depth_eps, float sigma_pixel, float sigma_depth,
+                                    float huber_k, void* workspace, float* out36, void* stream) {
+  S3_REQUIRE(T && n >= 0 && workspace && out36, "s3t_calib_normal_eqs: bad arguments");
+  S3_REQUIRE(n == (int64_t)h * w, "s3t_calib_normal_eqs: n must equal h*w (keyframe pixels)");
+  CalibP cp;
+  if (int e = make_calib(K, h, w, pixel_border, depth_eps, &cp)) return e;
+  hipStream_t st = s3::as_stream(stream);
+  const int nb = blocks_for(n);
+  float* partial = static_cast<float*>(workspace);
+  // sqrt_info = 1 / sigma * valid * sqrt(Q), masked by valid_proj & valid_meas (tracker.py:219-240)
+  k_normal_eqs<kCalib><<<nb, kThreads, 0, st>>>(nullptr, T, Xf, Xk, Q, valid, n,
+                                               1.0f / sigma_pixel, 1.0f / sigma_depth, huber_k,
+                                               cp, partial);
+  S3_LAUNCH_CHECK();
+  k_finalize<<<NV, kThreads, 0, st>>>(nullptr, partial, nb, out36);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+extern "C" int s3t_gn_iterations_calib(const float* Xf, const float* Xk, const float* Q,
+                                       const uint8_t* valid, int64_t n, const float* K, int h,
+                                       int w, float pixel_border, float depth_eps,
+                                       float sigma_pixel, float sigma_depth, float huber_k,
+                                       int iters, int max_iters, float rel_error,
+                                       float delta_norm, float* T, double* state,
+                                       void* workspace, float* out36, void* stream) {
+  S3_REQUIRE(T && state && n >= 0 && workspace && out36 && iters >= 0,
+             "s3t_gn_iterations_calib: bad arguments");
+  S3_REQUIRE(n == (int64_t)h * w, "s3t_gn_iterations_calib: n must equal h*w (keyframe pixels)");
+  CalibP cp;
+  if (int e = make_calib(K, h, w, pixel_border, depth_eps, &cp)) return e;
+  hipStream_t st = s3::as_stream(stream);
+  const int nb = blocks_for(n);
+  float* partial = static_cast<float*>(workspace);
+  for (int i = 0; i < iters; ++i) {
+    k_normal_eqs<kCalib><<<nb, kThreads, 0, st>>>(state, T, Xf, Xk, Q, valid, n,
+                                                 1.0f / sigma_pixel, 1.0f / sigma_depth,
+                                                 huber_k, cp, partial);
     S3_LAUNCH_CHECK();
     k_finalize<<<NV, kThreads, 0, st>>>(state, partial, nb, out36);
     S3_LAUNCH_CHECK();

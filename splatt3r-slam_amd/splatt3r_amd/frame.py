@@ -139,12 +139,23 @@ class Keyframes:
 
     def __init__(self):
         self._kf: list = []
+        self.K: Optional[torch.Tensor] = None
 
     def __len__(self):
         return len(self._kf)
 
     def __getitem__(self, i) -> Frame:
-        return self._kf[i]
+        kf = self._kf[i]
+        if self.K is not None:
+            kf.K = self.K      # frame.py:295 (SharedKeyframes.__getitem__)
+        return kf
+
+    def set_intrinsics(self, K: torch.Tensor):
+        """frame.py:346-349 (use_calib only)."""
+        self.K = K
+
+    def get_intrinsics(self) -> Optional[torch.Tensor]:
+        return self.K
 
     def __setitem__(self, i, frame: Frame):
         self._kf[i] = frame
@@ -156,7 +167,7 @@ class Keyframes:
         self._kf.pop()
 
     def last_keyframe(self) -> Optional[Frame]:
-        return self._kf[-1] if self._kf else None
+        return self[len(self._kf) - 1] if self._kf else None
 
     def get_poses(self) -> lietorch.Sim3:
         return lietorch.Sim3(torch.cat([k.T_WC.data.reshape(1, 8) for k in self._kf]))

@@ -31,6 +31,7 @@ import time
 import torch
 
 import lietorch
+from splatt3r_amd.config import config
 from splatt3r_amd.frame import Frame, Keyframes, Mode, create_frame
 from splatt3r_amd.splatt3r_utils import (gaussians_to_world, splatt3r_inference_mono,
                                          splatt3r_render)
@@ -57,6 +58,10 @@ class Frontend:
         self.device = device
         self.K = K
         self.keyframes = Keyframes()
+        if config["use_calib"]:
+            if K is None:
+                raise ValueError("use_calib needs the camera intrinsics K (main.py:310-318)")
+            self.keyframes.set_intrinsics(K)   # main.py:314-318
         self.tracker = FrameTracker(model, self.keyframes, device)
         self.mode = Mode.INIT
         self.render = render

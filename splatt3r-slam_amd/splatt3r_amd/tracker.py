@@ -3,7 +3,9 @@
 The control flow (match → filter → GN → pointmap fusion → keyframe test)
 stays on the host as in the reference.  Each Gauss-Newton iteration is one
 fused HIP launch (s3t_ray_dist_normal_eqs: act_Sim3 + ray/dist residuals +
-Huber weights + J^T J / J^T r / cost reduction) followed by a 36-float
+Huber weights + J^T J / J^T r / cost reduction; s3t_gn_iterations_calib
+for the calibrated pixel + log-depth residuals of opt_pose_calib_sim3,
+tracker.py:216-270) followed by a 36-float
 download, a 7x7 Cholesky on the host and the Sim3 retraction on the host —
 the reference does ~30 torch launches, a cuBLAS A^T A, a GPU Cholesky and an
 `.item()` sync per iteration (tracker.py:156-214).
@@ -29,6 +31,15 @@ _lib.register({
     "s3t_gn_iterations": (ctypes.c_int, [P_, P_, P_, P_, ctypes.c_int64, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_float, ctypes.c_float, P_, P_, P_, P_, P_]),
+    "s3t_calib_normal_eqs": (ctypes.c_int, [P_, P_, P_, P_, P_, ctypes.c_int64, P_, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                            ctypes.c_float, ctypes.c_float, ctypes.c_float, P_, P_,
+                                            P_]),
+    "s3t_gn_iterations_calib": (ctypes.c_int, [P_, P_, P_, P_, ctypes.c_int64, P_, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                               ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                               ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                               ctypes.c_float, P_, P_, P_, P_, P_]),
 })
 GN_CHUNK = 8   # iterations queued per host check of the device-side GN state
 
@@ -67,20 +78,36 @@ class NormalEquations:
         """Reset the device GN state (the pose slot must already hold T)."""
         self.state.copy_(self.state_init, non_blocking=True)
 
-    def gn_queue(self, Xf, Xk, Q, valid, cfg, iters):
-        """Queue `iters` device-side GN iterations; the state is copied to
-        the pinned host mirror behind them (read after a sync)."""
-        n = Xf.shape[0]
-        _lib.require_cuda(Xf, Xk, Q, valid)
-        _lib.require_contig("s3t_gn_iterations", Xf, Xk, Q, valid)
+    def _workspace(self, name, n, *ts):
+        _lib.require_cuda(*ts)
+        _lib.require_contig(name, *ts)
         need = _lib.lib().s3t_workspace_bytes(n)
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-        _lib.call("s3t_gn_iterations", Xf.data_ptr(), Xk.data_ptr(), Q.data_ptr(),
-                  valid.data_ptr(), n, cfg["sigma_ray"], cfg["sigma_dist"], cfg["huber"],
-                  int(iters), int(cfg["max_iters"]), float(cfg["rel_error"]),
-                  float(cfg["delta_norm"]), self.pose.data_ptr(), self.state.data_ptr(),
-                  self.ws.data_ptr(), self.out.data_ptr(), _lib.stream(self.device))
+
+    def gn_queue(self, Xf, Xk, Q, valid, cfg, iters, calib=None):
+        """Queue `iters` device-side GN iterations; the state is copied to
+        the pinned host mirror behind them (read after a sync).  `calib`
+        = (K host float32[9], (h, w)) selects the calibrated residuals
+        (opt_pose_calib_sim3) instead of the ray/dist ones."""
+        n = Xf.shape[0]
+        if calib is None:
+            self._workspace("s3t_gn_iterations", n, Xf, Xk, Q, valid)
+            _lib.call("s3t_gn_iterations", Xf.data_ptr(), Xk.data_ptr(), Q.data_ptr(),
+                      valid.data_ptr(), n, cfg["sigma_ray"], cfg["sigma_dist"], cfg["huber"],
+                      int(iters), int(cfg["max_iters"]), float(cfg["rel_error"]),
+                      float(cfg["delta_norm"]), self.pose.data_ptr(), self.state.data_ptr(),
+                      self.ws.data_ptr(), self.out.data_ptr(), _lib.stream(self.device))
+        else:
+            K9, (h, w) = calib
+            self._workspace("s3t_gn_iterations_calib", n, Xf, Xk, Q, valid)
+            _lib.call("s3t_gn_iterations_calib", Xf.data_ptr(), Xk.data_ptr(), Q.data_ptr(),
+                      valid.data_ptr(), n, K9.ctypes.data, int(h), int(w),
+                      float(cfg["pixel_border"]), float(cfg["depth_eps"]),
+                      float(cfg["sigma_pixel"]), float(cfg["sigma_depth"]), float(cfg["huber"]),
+                      int(iters), int(cfg["max_iters"]), float(cfg["rel_error"]),
+                      float(cfg["delta_norm"]), self.pose.data_ptr(), self.state.data_ptr(),
+                      self.ws.data_ptr(), self.out.data_ptr(), _lib.stream(self.device))
         self.state_host.copy_(self.state, non_blocking=True)
 
     def set_pose_host(self, T: np.ndarray):
@@ -98,6 +125,17 @@ class NormalEquations:
         _lib.call("s3t_ray_dist_normal_eqs", self.pose.data_ptr(), Xf.data_ptr(), Xk.data_ptr(),
                   Q.data_ptr(), valid.data_ptr(), n, sigma_ray, sigma_dist, huber_k,
                   self.ws.data_ptr(), self.out.data_ptr(), _lib.stream(self.device))
+        self.host.copy_(self.out, non_blocking=True)
+
+    def launch_calib(self, Xf, Xk, Q, valid, K9, img_size, cfg):
+        n = Xf.shape[0]
+        self._workspace("s3t_calib_normal_eqs", n, Xf, Xk, Q, valid)
+        h, w = img_size
+        _lib.call("s3t_calib_normal_eqs", self.pose.data_ptr(), Xf.data_ptr(), Xk.data_ptr(),
+                  Q.data_ptr(), valid.data_ptr(), n, K9.ctypes.data, int(h), int(w),
+                  float(cfg["pixel_border"]), float(cfg["depth_eps"]), float(cfg["sigma_pixel"]),
+                  float(cfg["sigma_depth"]), float(cfg["huber"]), self.ws.data_ptr(),
+                  self.out.data_ptr(), _lib.stream(self.device))
         self.host.copy_(self.out, non_blocking=True)
 
     def fetch(self):
@@ -164,9 +202,13 @@ class FrameTracker:
         Qk = torch.sqrt(Qff[idx_f2k] * Qkf)
         frame.update_pointmap(Xff, Cff)
 
-        if config["use_calib"]:
-            raise NotImplementedError("calibrated tracking (opt_pose_calib_sim3) is §8(f) work")
-        Xf, Xk, T_WCf, T_WCk, Cf, Ck = self.get_points_poses(frame, keyframe, idx_f2k)
+        use_calib = config["use_calib"]
+        img_size = tuple(frame.img.shape[-2:])
+        calib = None
+        if use_calib:
+            calib = (self._host_K(keyframe.K), img_size)
+        Xf, Xk, T_WCf, T_WCk, Cf, Ck = self.get_points_poses(frame, keyframe, idx_f2k, img_size,
+                                                             use_calib, keyframe.K)
 
         valid_Cf = Cf > self.cfg["C_conf"]
         valid_Ck = Ck > self.cfg["C_conf"]
@@ -191,7 +233,7 @@ class FrameTracker:
         ne = self.normal_eqs
         ne.pose.copy_(T_CkCf.data.reshape(8))
         ne.gn_begin(self.cfg)
-        ne.gn_queue(Xf, Xk, Q, valid_c, self.cfg, GN_CHUNK)
+        ne.gn_queue(Xf, Xk, Q, valid_c, self.cfg, GN_CHUNK, calib)
         torch.cuda.current_stream(ne.device).synchronize()
         n_opt, n_kf, n_unique = stats_host.tolist()
 
@@ -199,7 +241,7 @@ class FrameTracker:
             print(f"Skipped frame {frame.frame_id}")
             return False, [], True
         try:
-            T_WCf, T_CkCf = self._gn_finish(Xf, Xk, Q, valid_c, T_WCk)
+            T_WCf, T_CkCf = self._gn_finish(Xf, Xk, Q, valid_c, T_WCk, calib)
         except CholeskyError:
             print(f"Cholesky failed {frame.frame_id}")
             return False, [], True
@@ -217,14 +259,31 @@ class FrameTracker:
         return (new_kf, [keyframe.X_canon, keyframe.get_average_conf(), frame.X_canon,
                          frame.get_average_conf(), Qkf, Qff], False)
 
-    def get_points_poses(self, frame, keyframe, idx_f2k):
-        """tracker.py:129-154 (uncalibrated branch)."""
+    def _host_K(self, K):
+        """K as a host float32[9], cached per tensor (K is constant for a
+        sequence; one device read instead of one per frame)."""
+        key = (K.data_ptr(), K.device)
+        if getattr(self, "_K_key", None) != key:
+            self._K_key = key
+            self._K9 = np.ascontiguousarray(K.detach().float().cpu().numpy().reshape(9))
+        return self._K9
+
+    def get_points_poses(self, frame, keyframe, idx_f2k, img_size=None, use_calib=False, K=None):
+        """tracker.py:129-154.  With use_calib both pointmaps are first
+        constrained to their pixel rays; the calibrated measurements (pixel
+        grid + log keyframe depth, tracker.py:145-151) are formed inside the
+        GN kernel from Xk (include/s3t.h s3t_gn_iterations_calib)."""
+        Xf = frame.X_canon
+        Xk = keyframe.X_canon
+        if use_calib:
+            from splatt3r_amd.geometry import constrain_points_to_ray
+            Xf = constrain_points_to_ray(img_size, Xf[None], K).squeeze(0)
+            Xk = constrain_points_to_ray(img_size, Xk[None], K).squeeze(0)
         Cf = frame.get_average_conf()
         Ck = keyframe.get_average_conf()
-        return (frame.X_canon[idx_f2k], keyframe.X_canon, frame.T_WC, keyframe.T_WC,
-                Cf[idx_f2k], Ck)
+        return Xf[idx_f2k], Xk, frame.T_WC, keyframe.T_WC, Cf[idx_f2k], Ck
 
-    def _gn_finish(self, Xf, Xk, Q, valid, T_WCk):
+    def _gn_finish(self, Xf, Xk, Q, valid, T_WCk, calib=None):
         """Drive the device-side GN loop (first chunk already queued and
         synced) to its flag; returns (T_WCf, T_CkCf)."""
         cfg, ne = self.cfg, self.normal_eqs
@@ -232,7 +291,7 @@ class FrameTracker:
             iters, flag = int(ne.state_host[1]), int(ne.state_host[2])
             if flag != 0 or iters >= cfg["max_iters"]:
                 break
-            ne.gn_queue(Xf, Xk, Q, valid, cfg, min(GN_CHUNK, cfg["max_iters"] - iters))
+            ne.gn_queue(Xf, Xk, Q, valid, cfg, min(GN_CHUNK, cfg["max_iters"] - iters), calib)
             torch.cuda.current_stream(ne.device).synchronize()
         self.last_iters = iters
         if _DEBUG:
@@ -258,6 +317,25 @@ class FrameTracker:
         ne.gn_queue(Xf, Xk, Q, valid, self.cfg, GN_CHUNK)
         torch.cuda.current_stream(ne.device).synchronize()
         return self._gn_finish(Xf, Xk, Q, valid, T_WCk)
+
+    def opt_pose_calib_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size):
+        """tracker.py:216-270 on the device (s3t_gn_iterations_calib).  Xf:
+        ray-constrained frame points gathered by idx_f2k; Xk: ray-constrained
+        keyframe pointmap (its pixel grid and log depth are the measurement,
+        built inside the kernel instead of the reference's meas_k /
+        valid_meas_k tensors)."""
+        ne = self.normal_eqs
+        Xf = Xf.float().contiguous()
+        Xk = Xk.float().contiguous()
+        Q = Qk.float().contiguous()
+        valid = valid.contiguous()
+        calib = (self._host_K(K), tuple(img_size))
+        T_CkCf = T_WCk.inv() * T_WCf
+        ne.pose.copy_(T_CkCf.data.reshape(8))
+        ne.gn_begin(self.cfg)
+        ne.gn_queue(Xf, Xk, Q, valid, self.cfg, GN_CHUNK, calib)
+        torch.cuda.current_stream(ne.device).synchronize()
+        return self._gn_finish(Xf, Xk, Q, valid, T_WCk, calib)
 
     def opt_pose_ray_dist_sim3_host(self, Xf, Xk, T_WCf, T_WCk, Qk, valid):
         """Host-driven variant (one fused normal-equation launch + host

@@ -90,3 +90,31 @@ def test_factor_graph_rays_matches_oracle():
     assert dx is not None and torch.isfinite(dx).all()
     T_dev = torch.cat([kfs[int(k)].T_WC.data.reshape(1, 8) for k in unique]).cpu().numpy()
     np.testing.assert_allclose(T_dev, T_ref, atol=2e-4, rtol=0)
+
+
+@pytest.mark.gpu
+def test_calibrated_frontend_tracks():
+    """config use_calib (config/calib.yaml): intrinsics reach the keyframes
+    (SharedKeyframes.set_intrinsics, main.py:314-318) and frames are tracked
+    with opt_pose_calib_sim3 (tracker.py:78-90) on the device GN loop."""
+    from splatt3r_amd.config import config
+    from splatt3r_amd.slam import Frontend
+    from splatt3r_amd.splatt3r_utils import load_splatt3r
+    from splatt3r_amd.synthetic import tum_like_sequence
+    from splatt3r_amd.weights import FULL
+
+    dev = torch.device("cuda", 0)
+    model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
+    frames = tum_like_sequence(6, 384, 512, seed=3, step_px=2.0, device=dev)
+    K = torch.tensor([[512.0, 0, 256], [0, 512.0, 192], [0, 0, 1]], device=dev)
+    old = config["use_calib"]
+    config["use_calib"] = True
+    try:
+        fe = Frontend(model, device=dev, K=K, spatial_stride=4, render=True)
+        for i in range(6):
+            f = fe.step(i, frames[i])
+            assert torch.isfinite(f.T_WC.data).all()
+        assert fe.keyframes[0].K is K
+        assert fe.stats["tracked"] >= 1 and 1 <= fe.tracker.last_iters <= 50
+    finally:
+        config["use_calib"] = old
