@@ -709,15 +709,30 @@ k_gemm(GemmP p) {
 }
 
 // Split-K combine: sum the partial planes in split order, then the epilogue.
+// V consecutive columns of one row per thread (16-B plane loads when V = 4,
+// host-checked N % 4 == 0); the sum order per element is unchanged.
+template <int V>
 __global__ void __launch_bounds__(kThreads) k_splitk_reduce(GemmP p) {
   const int g = blockIdx.y;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) * V;
   const int64_t MN = (int64_t)p.M * p.N;
   if (i >= MN) return;
   const float* w = p.ws + (int64_t)g * p.split_k * MN + i;
-  float v = w[0];
-  for (int s = 1; s < p.split_k; ++s) v += w[s * MN];
-  epilogue(p, g, (int)(i / p.N), (int)(i % p.N), v);
+  if constexpr (V == 4) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(w);
+    for (int s = 1; s < p.split_k; ++s) {
+      const f32x4 t = *reinterpret_cast<const f32x4*>(w + s * MN);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += t[j];
+    }
+    const int row = (int)(i / p.N), col = (int)(i % p.N);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) epilogue(p, g, row, col + j, v[j]);
+  } else {
+    float v = w[0];
+    for (int s = 1; s < p.split_k; ++s) v += w[s * MN];
+    epilogue(p, g, (int)(i / p.N), (int)(i % p.N), v);
+  }
 }
 
 template <int BM, int BN, int S, int NWM = 2, int NWN = 2, int BK = 64>
@@ -746,8 +761,13 @@ int launch(const GemmP& p, hipStream_t st) {
     k_gemm<BM, BN, NWM, NWN, kConv, S, BK><<<grid, NT, 0, st>>>(q);
   S3_LAUNCH_CHECK();
   if (q.split_k > 1) {
-    dim3 rg((unsigned)s3::cdiv((int64_t)p.M * p.N, kThreads), p.groups);
-    k_splitk_reduce<<<rg, kThreads, 0, st>>>(q);
+    if (p.N % 4 == 0) {
+      dim3 rg((unsigned)s3::cdiv((int64_t)p.M * p.N / 4, kThreads), p.groups);
+      k_splitk_reduce<4><<<rg, kThreads, 0, st>>>(q);
+    } else {
+      dim3 rg((unsigned)s3::cdiv((int64_t)p.M * p.N, kThreads), p.groups);
+      k_splitk_reduce<1><<<rg, kThreads, 0, st>>>(q);
+    }
     S3_LAUNCH_CHECK();
   }
   return S3_OK;
