@@ -65,6 +65,8 @@ def _args():
                          "the timed region then holds steps/enc-batch encoder replays")
     ap.add_argument("--main-priority", type=int, default=None,
                     help="HIP stream priority of the frame's main chain (e.g. -1 = high)")
+    ap.add_argument("--late-prefetch", action="store_true",
+                    help="queue the next frame's encoder after the tracker's GN sync")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="encode each frame inside its own step (no side-stream overlap)")
     return ap.parse_args()
@@ -207,7 +209,7 @@ def main():
         raise SystemExit(f"--steps {a.steps} must be a multiple of --enc-batch {kb}")
     frames = tum_like_sequence(nfr + kb, H, W, seed=rank, step_px=2.0, device=dev)
     fe = Frontend(model, device=dev, spatial_stride=4, render=True, enc_batch=kb,
-                  main_priority=a.main_priority)
+                  main_priority=a.main_priority, late_prefetch=a.late_prefetch)
     nxt = (lambda i: None) if a.no_pipeline else (lambda i: [frames[j] for j in range(i + 1, i + 1 + kb)])
 
     for i in range(a.warmup + 1):          # frame 0 = INIT, then W tracked frames

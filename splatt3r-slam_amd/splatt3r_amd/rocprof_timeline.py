@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--last-ms", type=float, default=50.0)
     ap.add_argument("--skip-last-ms", type=float, default=0.0)
     ap.add_argument("--list", type=int, default=0)
+    ap.add_argument("--gaps", type=int, default=0, help="print the N largest idle gaps")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = list(c.execute("select name, start, end, queue_id from kernels order by start"))
@@ -57,6 +58,27 @@ def main():
     if seg is not None:
         print(f"  seg q{seg[0]} {(seg[1] - t0) / 1e3:9.1f} -> {(seg[2] - t0) / 1e3:9.1f} us"
               f" ({seg[3]} kernels, first {seg[4]})")
+    if a.gaps:
+        # idle gaps of the union timeline with the kernels either side
+        ends, gl = [], []
+        cur_e, prev = None, None
+        for n, s, e, q in win:
+            if cur_e is not None and s > cur_e:
+                gl.append((s - cur_e, (cur_e - t0) / 1e3, prev, n))
+            if cur_e is None or e > cur_e:
+                cur_e, prev = e, n
+        gl.sort(reverse=True)
+        short = lambda n: re.sub(r"\(anonymous namespace\)::", "", n)[:48]
+        tot = {}
+        for g, at, a0, b0 in gl:
+            k = (short(a0), short(b0))
+            tot[k] = tot.get(k, 0) + g
+        print("  largest idle gaps (us, at us, after -> before):")
+        for g, at, a0, b0 in gl[: a.gaps]:
+            print(f"    {g / 1e3:7.1f} @ {at:9.1f}  {short(a0)} -> {short(b0)}")
+        print("  idle time by (after -> before) pair:")
+        for k, g in sorted(tot.items(), key=lambda kv: -kv[1])[: a.gaps]:
+            print(f"    {g / 1e6:7.3f} ms  {k[0]} -> {k[1]}")
     for n, s, e, q in win[: a.list]:
         n = re.sub(r"\(anonymous namespace\)::", "", n)[:70]
         print(f"  q{q} {(s - t0) / 1e3:9.1f} {(e - s) / 1e3:7.1f} us  {n}")

@@ -53,10 +53,11 @@ def should_append_gaussians(add_new_kf, frame_idx, current_T_WC, last_append_T_W
 class Frontend:
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
-                 readback=True, enc_batch=1, main_priority=None):
+                 readback=True, enc_batch=1, main_priority=None, late_prefetch=False):
         self.model = model
         self.device = device
         self.K = K
+        self.late_prefetch = late_prefetch
         self.keyframes = Keyframes()
         if config["use_calib"]:
             if K is None:
@@ -209,7 +210,15 @@ class Frontend:
             # next_img: the next frame's image, or a list of the next frames'
             # images (lookahead); up to enc_batch of them are encoded together
             nxt = list(next_img) if isinstance(next_img, (list, tuple)) else [next_img]
-            self._prefetch(i + 1, nxt[:max(1, self.enc_batch)])
+            pending = (i + 1, nxt[:max(1, self.enc_batch)])
+            # late prefetch: a tracked frame queues the next encoder after
+            # its GN sync, so the encoder fills the device while the host
+            # issues the post-GN launches (pose update, map, render)
+            if not (self.late_prefetch and self.mode == Mode.TRACKING):
+                self._prefetch(*pending)
+                pending = None
+        else:
+            pending = None
         if e0 is not None:
             e0[0] = self._event()
         self.stats["frames"] += 1
@@ -228,6 +237,8 @@ class Frontend:
             return frame
         if self.mode == Mode.TRACKING:
             add_new_kf, _, try_reloc = self.tracker.track(frame)
+            if pending is not None:
+                self._prefetch(*pending)
             self.stats["gn_iters"] += self.tracker.last_iters
             self.stats["tracked"] += 1
             if try_reloc:
