@@ -10,7 +10,7 @@ A step is one frame of the reference's main loop in TRACKING mode
 (main.py:451-506 with --no-viz, rendering on, spatial stride 4):
 encoder on the new frame, fused decoder + both heads against the last
 keyframe, dense matching, Gauss-Newton pose, pointmap fusion, keyframe test,
-gaussians_to_world when the reference would append, and the Gaussian render
+gaussians_to_world on every tracked frame (as the reference under --no-viz), and the Gaussian render
 of the frame's 2*h*w splats read back to the host.  The tracker path does not
 shard (frame i depends on frame i-1), so with N GPUs each rank runs an
 independent replica on its own synthetic sequence: weak scaling, value =

@@ -53,8 +53,14 @@ def should_append_gaussians(add_new_kf, frame_idx, current_T_WC, last_append_T_W
 class Frontend:
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
-                 readback=True, enc_batch=1, main_priority=None, late_prefetch=False):
+                 readback=True, enc_batch=1, main_priority=None, late_prefetch=False,
+                 viz=False):
         self.model = model
+        # viz: the reference's enable_gs_viz (main.py:357, `not --no-viz`).
+        # Only then does it record the last append (main.py:434-435,488-489);
+        # under --no-viz last_gs_append_T_WC stays None, so should_append is
+        # always true and gaussians_to_world runs on every tracked frame.
+        self.viz = viz
         self.device = device
         self.K = K
         self.late_prefetch = late_prefetch
@@ -72,7 +78,7 @@ class Frontend:
                             min_confidence=min_confidence)
         self.last_T_WC = None
         self.last_append_T_WC = None
-        self.last_append_idx = 0
+        self.last_append_idx = -(10 ** 9)                       # main.py:341-342
         self.min_translation, self.min_frame_gap = 0.12, 3   # main.py:339-340
         self.new_kf_frames: list[int] = []
         self.stats = dict(frames=0, tracked=0, reloc=0, keyframes=0, gn_iters=0,
@@ -230,8 +236,8 @@ class Frontend:
             self.new_kf_frames.append(i)
             self.stats["keyframes"] += 1
             self.mode = Mode.TRACKING
-            self._to_world(frame)
-            self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
+            if self._to_world(frame) is not None and self.viz:
+                self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
             self._render(frame, frame, None)
             self.last_T_WC = frame.T_WC
             return frame
@@ -246,7 +252,8 @@ class Frontend:
             if not try_reloc and should_append_gaussians(
                     add_new_kf, i, frame.T_WC, self.last_append_T_WC, self.last_append_idx,
                     self.min_translation, self.min_frame_gap):
-                self._to_world(frame)
+                if self._to_world(frame) is not None and self.viz:
+                    self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
             if not try_reloc:
                 self._render(frame, self.keyframes.last_keyframe(), frame.T_WC)
         elif self.mode == Mode.RELOC:
