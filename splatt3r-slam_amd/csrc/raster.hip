@@ -208,6 +208,10 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
   radii[i] = 0;
   g.tiles[i] = 0;
   g.dup[i] = make_uint4(0u, 0u, 0u, 0u);
+  // depth-sort key/value (fused here instead of a separate pass): culled
+  // Gaussians sort last and emit nothing
+  g.dkey[i] = 0xFFFFFFFFu;
+  g.iota[i] = (uint64_t)i;
   const float mx = means[i * 3 + 0], my = means[i * 3 + 1], mz = means[i * 3 + 2];
   float pv[3];
   xform43(vm, mx, my, mz, pv);
@@ -285,18 +289,12 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
                         (uint32_t)rw | ((uint32_t)(y1 - y0) << 16), (uint32_t)mask,
                         (uint32_t)(mask >> 32));
   g.tiles[i] = n;
+  // stable depth sort key: positive depth bits order like the floats
+  g.dkey[i] = n > 0 ? __float_as_uint(pv[2]) : 0xFFFFFFFFu;
+  g.iota[i] = (uint64_t)i | ((uint64_t)n << 32);
 }
 
 // ------------------------------------------------------------- binning ----
-// Depth keys for the stable depth sort: positive depth bits order like the
-// floats; Gaussians that touch no tile sort last (they emit nothing).
-__global__ void __launch_bounds__(kThreads)
-k_depth_keys(int64_t P, GeomState g) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P) return;
-  g.dkey[i] = g.tiles[i] > 0 ? __float_as_uint(g.depth[i]) : 0xFFFFFFFFu;
-  g.iota[i] = (uint64_t)i | ((uint64_t)g.tiles[i] << 32);
-}
 
 // tiles kept by Gaussian d (its duplication record)
 __device__ __forceinline__ uint32_t dup_count(const uint4 d) {
@@ -954,8 +952,6 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
   S3_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * ntiles, st));
   if (R > 0) {
     const unsigned pb = (unsigned)s3::cdiv(P, kThreads);
-    k_depth_keys<<<pb, kThreads, 0, st>>>(P, g);
-    S3_LAUNCH_CHECK();
     size_t db = g.dsort_bytes;
     S3_HIP(hipcub::DeviceRadixSort::SortPairs(g.dsort_tmp, db, g.dkey, g.dkey_sorted, g.iota,
                                               g.order, (int)P, 0, 32, st));
