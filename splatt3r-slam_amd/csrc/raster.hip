@@ -60,17 +60,24 @@ struct GeomState {
   // tile counts come out of the sort instead of a random gather
   uint64_t* iota;
   uint64_t* order;         // (index | count << 32) per depth rank (stable)
-  uint32_t* tiles_sorted;  // tiles touched per depth rank
   uint32_t* offsets_sorted;
   void* dsort_tmp;
   size_t dsort_bytes;
 };
 
+// tiles touched per depth rank = high word of the depth-sorted value
+struct HighWord {
+  __host__ __device__ uint32_t operator()(uint64_t v) const { return (uint32_t)(v >> 32); }
+};
+typedef hipcub::TransformInputIterator<uint32_t, HighWord, const uint64_t*> TilesIt;
+
 size_t scan_temp_bytes(int64_t P) {
-  size_t bytes = 0;
+  size_t bytes = 0, b2 = 0;
   hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                    (int)P);
-  return bytes;
+  hipcub::DeviceScan::InclusiveSum(nullptr, b2, TilesIt(nullptr, HighWord()),
+                                   (uint32_t*)nullptr, (int)P);
+  return bytes > b2 ? bytes : b2;
 }
 
 size_t key32_sort_temp_bytes(int64_t n) {
@@ -105,7 +112,6 @@ GeomState carve_geom(void* base, int64_t P) {
   g.dkey_sorted = c.take<uint32_t>(P);
   g.iota = c.take<uint64_t>(P);
   g.order = c.take<uint64_t>(P);
-  g.tiles_sorted = c.take<uint32_t>(P);
   g.offsets_sorted = c.take<uint32_t>(P);
   g.dsort_bytes = depth_sort_temp_bytes(P);
   g.dsort_tmp = c.take<char>(g.dsort_bytes);
@@ -302,11 +308,6 @@ __device__ __forceinline__ uint32_t dup_count(const uint4 d) {
   return w * h <= 64u ? (uint32_t)__popcll((uint64_t)d.z | ((uint64_t)d.w << 32)) : w * h;
 }
 
-__global__ void __launch_bounds__(kThreads)
-k_gather_tiles(int64_t P, GeomState g) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < P) g.tiles_sorted[k] = (uint32_t)(g.order[k] >> 32);
-}
 
 // Instances in depth order: the wave's 64 depth ranks k own the contiguous
 // output range [start(k0), end(k0 + 63)).  It is produced in chunks of DCH
@@ -955,10 +956,9 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
     size_t db = g.dsort_bytes;
     S3_HIP(hipcub::DeviceRadixSort::SortPairs(g.dsort_tmp, db, g.dkey, g.dkey_sorted, g.iota,
                                               g.order, (int)P, 0, 32, st));
-    k_gather_tiles<<<pb, kThreads, 0, st>>>(P, g);
-    S3_LAUNCH_CHECK();
     size_t sb = g.scan_bytes;
-    S3_HIP(hipcub::DeviceScan::InclusiveSum(g.scan_tmp, sb, g.tiles_sorted, g.offsets_sorted,
+    S3_HIP(hipcub::DeviceScan::InclusiveSum(g.scan_tmp, sb,
+                                            TilesIt(g.order, HighWord()), g.offsets_sorted,
                                             (int)P, st));
     k_duplicate<<<pb, kThreads, 0, st>>>(P, gx, gy, radii, g, b.keys_unsorted,
                                          b.vals_unsorted);
