@@ -3,7 +3,7 @@ reference from /root/reference (this container only; the GPU box never reads
 /root/reference).  Committed outputs are data only (inputs + expected
 outputs), never reference source.
 
-  python oracle/gen_golden.py [section ...]     sections: matching, net, render
+  python oracle/gen_golden.py [section ...]     sections: matching, net, net_c4, n1, mono, resize, render
 
 matching : splatt3r_slam/image.py img_gradient (imported) driven exactly as
            splatt3r_slam/matching.py:25-49 prep_for_iter_proj does.
@@ -247,15 +247,29 @@ def gen_net():
             with open(os.path.join(GOLDEN, "manifest_small.txt"), "w") as f:
                 f.writelines(f"{n} {list(s)}\n" for n, s in man)
     # (b) full Splatt3R architecture at 384x512: slices + checksums
+    gen_full(384, 512, seed=6, write_manifest=True)
+
+
+def gen_net_c4():
+    """Full architecture at 320x512 (C4: EuRoC 752x480 -> 512x320 by the
+    resize_img rule, splatt3r_utils.py:668-679; N = 640 tokens)."""
+    gen_full(320, 512, seed=7)
+
+
+def gen_full(H, Wd, seed, write_manifest=False):
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "splatt3r-slam_amd"))
+    from splatt3r_amd import weights as W
+    keys = ("pts3d", "conf", "desc", "desc_conf", "scales", "rotations", "sh", "opacities", "means")
     cfg = W.FULL
     torch.manual_seed(0)
     model = build_reference_model(cfg)
     man = load_prng(model, cfg, seed=1234)
-    with open(os.path.join(GOLDEN, "manifest_full.txt"), "w") as f:
-        f.writelines(f"{n} {list(s)}\n" for n, s in man)
-    g = torch.Generator().manual_seed(6)
-    img1 = torch.rand(1, 3, 384, 512, generator=g) * 2 - 1
-    img2 = torch.rand(1, 3, 384, 512, generator=g) * 2 - 1
+    if write_manifest:
+        with open(os.path.join(GOLDEN, "manifest_full.txt"), "w") as f:
+            f.writelines(f"{n} {list(s)}\n" for n, s in man)
+    g = torch.Generator().manual_seed(seed)
+    img1 = torch.rand(1, 3, H, Wd, generator=g) * 2 - 1
+    img2 = torch.rand(1, 3, H, Wd, generator=g) * 2 - 1
     f1, f2, p1, dec1, dec2, r1, r2 = run_reference(model, img1, img2)
     out = dict(img1=img1.numpy(), img2=img2.numpy(), feat1_rows=f1[0, ::37].numpy(),
                feat1_sum=f1.double().sum().numpy(), feat1_abs=f1.double().abs().sum().numpy())
@@ -268,11 +282,279 @@ def gen_net():
             out[f"res{ri}_{k}_sub"] = v[::8, ::8].numpy()
             out[f"res{ri}_{k}_sum"] = v.double().sum().numpy()
             out[f"res{ri}_{k}_abs"] = v.double().abs().sum().numpy()
-    np.savez_compressed(os.path.join(GOLDEN, "net_full_384x512.npz"), **out)
-    print("wrote net_full_384x512.npz")
+    name = f"net_full_{H}x{Wd}.npz"
+    np.savez_compressed(os.path.join(GOLDEN, name), **out)
+    print("wrote", name)
 
 
-SECTIONS = {"matching": gen_matching, "render": gen_render, "net": gen_net}
+def gen_mono():
+    """splatt3r_inference_mono (splatt3r_utils.py:503-536) on the small
+    config: the reference decoder run on (img1, img1) of net_small_off.npz."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "splatt3r-slam_amd"))
+    from splatt3r_amd import weights as W
+    import dataclasses
+    keys = ("pts3d", "conf", "desc", "desc_conf", "scales", "rotations", "sh", "opacities", "means")
+    cfg = dataclasses.replace(W.SMALL, use_offsets=True)
+    torch.manual_seed(0)
+    model = build_reference_model(cfg)
+    load_prng(model, cfg, seed=1234)
+    img1 = torch.from_numpy(np.load(os.path.join(GOLDEN, "net_small_off.npz"))["img1"])
+    _, _, _, _, _, r1, r2 = run_reference(model, img1, img1)
+    out = {"img": img1.numpy()}
+    for k in keys:
+        out["res11_" + k] = r1[k].numpy()
+        out["res21_" + k] = r2[k].numpy()
+    np.savez_compressed(os.path.join(GOLDEN, "net_small_mono.npz"), **out)
+    print("wrote net_small_mono.npz")
+
+
+RESIZE_CASES = ((480, 640, 512), (480, 752, 512), (512, 512, 512), (640, 480, 512),
+                (540, 960, 512), (300, 400, 512), (480, 640, 224))
+
+
+def resize_input(h, w, seed):
+    """Deterministic smooth float image in [0, 1] (also rebuilt by the test)."""
+    yy, xx = np.meshgrid(np.linspace(0, 1, h), np.linspace(0, 1, w), indexing="ij")
+    img = np.stack([0.45 + 0.45 * np.sin(6 * xx + 4 * yy + k + seed) for k in range(3)], -1)
+    iy, ix = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    img += 0.1 * (((ix // 3) + (iy // 3)) % 2)[..., None]   # 3-px checker: resampling detail
+    return np.clip(img, 0, 1).astype(np.float32)
+
+
+def gen_resize():
+    """resize_img (splatt3r_utils.py:646-693), the reference's own function
+    text compiled from the file (the module itself does not import here:
+    lietorch, torchvision); torchvision's ImgNorm is restated as
+    ToTensor + Normalize(0.5, 0.5).  Saved: the cropped uint8 image, the
+    true_shape and the transformation tuple per case."""
+    import ast
+    import PIL.Image
+    path = os.path.join(REF, "splatt3r_slam", "splatt3r_utils.py")
+    tree = ast.parse(open(path).read())
+    fns = [n for n in tree.body if isinstance(n, ast.FunctionDef)
+           and n.name in ("_resize_pil_image", "resize_img")]
+    mod = ast.Module(body=fns, type_ignores=[])
+
+    def img_norm(pil):
+        a = torch.from_numpy(np.asarray(pil).astype(np.float32) / 255.0).permute(2, 0, 1)
+        return (a - 0.5) / 0.5
+
+    ns = {"PIL": PIL, "np": np, "ImgNorm": img_norm}
+    exec(compile(mod, path, "exec"), ns)
+    out = {}
+    for i, (h, w, size) in enumerate(RESIZE_CASES):
+        img = resize_input(h, w, i)
+        res, tr = ns["resize_img"](img, size, return_transformation=True)
+        out[f"case{i}_uimg"] = res["unnormalized_img"]
+        out[f"case{i}_true_shape"] = res["true_shape"]
+        # res["img"] = ImgNorm(uimg) is not stored: the test derives it from uimg
+        out[f"case{i}_transform"] = np.float64(tr)
+        print(i, (h, w, size), "->", res["true_shape"].tolist(), tr)
+    np.savez_compressed(os.path.join(GOLDEN, "resize_img.npz"), **out)
+    print("wrote resize_img.npz")
+
+
+def _tf32_round(t):
+    """fp32 -> TF32 operand (round to nearest even at mantissa bit 13)."""
+    if not torch.is_tensor(t) or t.dtype != torch.float32:
+        return t
+    i = t.contiguous().view(torch.int32)
+    i = (i + 0xFFF + ((i >> 13) & 1)) & ~0x1FFF
+    return i.view(torch.float32)
+
+
+def tf32_mode():
+    """The reference's CUDA path runs its matrix products in TF32
+    (main.py:195 torch.backends.cuda.matmul.allow_tf32 = True; cuDNN convs
+    default to TF32): a TorchFunctionMode that rounds both operands of every
+    linear / matmul / conv / conv-transpose to TF32 and keeps fp32
+    accumulation, so the CPU reference reproduces that precision class."""
+    from torch.overrides import TorchFunctionMode
+
+    ops = {F.linear, torch.matmul, torch.bmm, torch.Tensor.__matmul__, F.conv2d,
+           F.conv_transpose2d}
+
+    class TF32Mode(TorchFunctionMode):
+        def __torch_function__(self, func, types, args=(), kwargs=None):
+            kwargs = kwargs or {}
+            if func in ops:
+                args = tuple(_tf32_round(a) if i < 2 else a for i, a in enumerate(args))
+                if "weight" in kwargs:
+                    kwargs["weight"] = _tf32_round(kwargs["weight"])
+            elif func is torch.einsum:
+                args = (args[0],) + tuple(_tf32_round(a) for a in args[1:])
+            return func(*args, **kwargs)
+
+    return TF32Mode()
+
+
+def _sim3_matrix(T):
+    """lietorch Sim3 data [t, q(xyzw), s] -> 4x4 [sR | t] (fp64 -> fp32), the
+    matrix splatt3r_utils.py:153-165 builds through SE3.matrix()."""
+    T = np.asarray(T, np.float64)
+    x, y, z, w = T[3:7] / np.linalg.norm(T[3:7])
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                  [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                  [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+    M = np.eye(4)
+    M[:3, :3] = R * T[7]
+    M[:3, 3] = T[:3]
+    return torch.from_numpy(M.astype(np.float32))[None]
+
+
+# N1 render cases: (name, context Sim3, target Sim3); the tracked-frame render
+# of main.py:491-499 is a self-render (target_T_WC = frame.T_WC)
+N1_POSES = {
+    "self": ([0.0, 0, 0, 0, 0, 0, 1, 1], [0.0, 0, 0, 0, 0, 0, 1, 1]),
+    "moved": ([0.1, -0.05, 0.2, 0.0499792, 0.0, 0.0, 0.99875026, 1.2],
+              [0.13, -0.04, 0.15, 0.0499792, 0.0399893, 0.0, 0.99795, 1.2]),
+}
+
+
+def _look_at(means, back=1.0):
+    """Sim3 data of a camera at -back * d looking along d = the normalised
+    median of `means` (camera +z -> d, shortest-arc quaternion)."""
+    d = np.median(means.reshape(-1, 3).numpy().astype(np.float64), axis=0)
+    d /= np.linalg.norm(d)
+    z = np.array([0.0, 0.0, 1.0])
+    axis = np.cross(z, d)
+    q = np.concatenate([axis, [1.0 + z @ d]])
+    q /= np.linalg.norm(q)
+    return [float(v) for v in (-back * d)] + [float(v) for v in q] + [1.0]
+
+
+def gen_n1():
+    """North-star N1 fixture: the reference pipeline's rendered RGB.
+
+    Reference head outputs (the committed net_small_* goldens, and the full
+    architecture at 384x512 re-run here with the net_full_384x512 inputs) go
+    through the reference glue exactly as splatt3r_render drives it
+    (splatt3r_utils.py:332-432: build_covariance, RGB2SH residual,
+    DecoderSplattingCUDA with default intrinsics f = max(h, w)), with a stub
+    rasterizer capturing what the glue hands GaussianRasterizer; the captured
+    inputs are rasterized by oracle.raster (the canonical graphdeco forward,
+    oracle/raster_ref.c).  Saved: the rendered [3,H,W] images + the poses."""
+    import types
+    sys.path.insert(0, os.path.dirname(HERE))
+    import oracle
+    captured = {}
+
+    class Settings(tuple):
+        def __new__(cls, **kw):
+            o = tuple.__new__(cls, tuple(kw.values()))
+            o.kw = kw
+            return o
+
+    class Rasterizer(torch.nn.Module):
+        def __init__(self, rs):
+            super().__init__()
+            self.rs = rs
+
+        def forward(self, **kw):
+            captured["settings"] = self.rs.kw
+            captured["inputs"] = kw
+            h, w = self.rs.kw["image_height"], self.rs.kw["image_width"]
+            return torch.zeros(3, h, w), torch.zeros(kw["means3D"].shape[0], dtype=torch.int32)
+
+    stub = types.ModuleType("diff_gaussian_rasterization")
+    stub.GaussianRasterizationSettings = Settings
+    stub.GaussianRasterizer = Rasterizer
+    sys.modules["diff_gaussian_rasterization"] = stub
+    core = os.path.join(REF, "splatt3r_core")
+    ps = os.path.join(core, "src", "pixelsplat_src")
+    for p in (ps, core):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    dec = _load_file("ref_decoder_splatting_cuda", os.path.join(ps, "decoder_splatting_cuda.py"))
+    geo = _load_file("ref_geometry", os.path.join(core, "utils", "geometry.py"))
+    shu = _load_file("ref_sh_utils", os.path.join(core, "utils", "sh_utils.py"))
+    decoder = dec.DecoderSplattingCUDA(background_color=[0.0, 0.0, 0.0])
+
+    def render(r1, r2, img1, img2, T_ctx, T_tgt):
+        # splatt3r_utils.py:358-432 with frame = view 1, ref_frame = view 2
+        hwc = lambda im: (im * 0.5 + 0.5).clamp(0, 1).permute(0, 2, 3, 1)
+        h, w = r1["means"].shape[1:3]
+        cov1 = geo.build_covariance(r1["scales"], r1["rotations"])
+        cov2 = geo.build_covariance(r2["scales"], r2["rotations"])
+        sh1 = r1["sh"].clone(); res = torch.zeros_like(sh1); res[..., 0] = shu.RGB2SH(hwc(img1))
+        sh1 = sh1 + res
+        sh2 = r2["sh"].clone(); res = torch.zeros_like(sh2); res[..., 0] = shu.RGB2SH(hwc(img2))
+        sh2 = sh2 + res
+        pred1 = {"means": r1["means"], "covariances": cov1, "sh": sh1, "opacities": r1["opacities"]}
+        pred2 = {"means_in_other_view": r2["means"], "covariances": cov2, "sh": sh2,
+                 "opacities": r2["opacities"]}
+        f = float(max(h, w))
+        K = torch.tensor([[[f, 0, w / 2.0], [0, f, h / 2.0], [0, 0, 1]]], dtype=torch.float32)
+        batch = {"context": [{"camera_pose": _sim3_matrix(T_ctx)}],
+                 "target": [{"camera_pose": _sim3_matrix(T_tgt), "camera_intrinsics": K}]}
+        decoder(batch, pred1, pred2, (h, w))
+        st, ins = captured["settings"], captured["inputs"]
+        sd = {k: (st[k].detach().numpy() if torch.is_tensor(st[k]) else st[k]) for k in st}
+        o = oracle.raster(sd, ins["means3D"].numpy(), ins["opacities"].numpy(),
+                          shs=ins["shs"].numpy(), cov3D_precomp=ins["cov3D_precomp"].numpy(),
+                          nthreads=8)
+        return o["color"], o["num_rendered"]
+
+    keys = ("means", "scales", "rotations", "sh", "opacities")
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "splatt3r-slam_amd"))
+    from splatt3r_amd import weights as W
+    import dataclasses
+    out = {}
+    cases = []
+    for tag, use_off in (("small_off", True), ("small_nooff", False)):
+        g = np.load(os.path.join(GOLDEN, f"net_{tag}.npz"))
+        im1, im2 = torch.from_numpy(g["img1"]), torch.from_numpy(g["img2"])
+        r1 = {k: torch.from_numpy(g["res1_" + k]) for k in keys}
+        r2 = {k: torch.from_numpy(g["res2_" + k]) for k in keys}
+        cfg = dataclasses.replace(W.SMALL, use_offsets=use_off)
+        torch.manual_seed(0)
+        model = build_reference_model(cfg)
+        load_prng(model, cfg, seed=1234)
+        with tf32_mode():
+            _, _, _, _, _, t1, t2 = run_reference(model, im1, im2)
+        cases.append((tag, r1, r2, t1, t2, im1, im2))
+        # matching on the TF32 reference outputs (splatt3r_match_asymmetric's
+        # idx/valid as the reference CUDA path would produce them)
+        idx_t, valid_t = oracle.match(t1["pts3d"].numpy(), t2["pts3d"].numpy(),
+                                      t1["desc"].numpy(), t2["desc"].numpy())
+        out[f"{tag}_match_tf32_idx"] = idx_t
+        out[f"{tag}_match_tf32_valid"] = valid_t
+    # full architecture at 384x512 (same inputs as net_full_384x512.npz)
+    torch.manual_seed(0)
+    model = build_reference_model(W.FULL)
+    load_prng(model, W.FULL, seed=1234)
+    g = torch.Generator().manual_seed(6)
+    img1 = torch.rand(1, 3, 384, 512, generator=g) * 2 - 1
+    img2 = torch.rand(1, 3, 384, 512, generator=g) * 2 - 1
+    full = np.load(os.path.join(GOLDEN, "net_full_384x512.npz"))
+    assert np.array_equal(full["img1"], img1.numpy())
+    _, _, _, _, _, r1, r2 = run_reference(model, img1, img2)
+    with tf32_mode():
+        _, _, _, _, _, t1, t2 = run_reference(model, img1, img2)
+    del model
+    cases.append(("full_384x512", r1, r2, t1, t2, img1, img2))
+    for tag, r1, r2, t1, t2, im1, im2 in cases:
+        poses = dict(N1_POSES)
+        # a target looking at view 1's point cloud from behind the origin
+        # (portable-PRNG weights put the full model's points outside the
+        # default frustum)
+        poses["lookat"] = ([0.0, 0, 0, 0, 0, 0, 1, 1], _look_at(r1["means"]))
+        for pname, (Tc, Tt) in poses.items():
+            img, nr = render(r1, r2, im1, im2, Tc, Tt)
+            img_t, _ = render(t1, t2, im1, im2, Tc, Tt)
+            out[f"{tag}_{pname}_image"] = img
+            out[f"{tag}_{pname}_image_tf32"] = img_t
+            out[f"{tag}_{pname}_ctx"] = np.float32(Tc)
+            out[f"{tag}_{pname}_tgt"] = np.float32(Tt)
+            print(tag, pname, "num_rendered", nr, "mean", float(img.mean()),
+                  "covered", float((img.sum(0) > 0).mean()),
+                  "tf32-vs-fp32 mean-L1", float(np.abs(img - img_t).mean()))
+    np.savez_compressed(os.path.join(GOLDEN, "n1_render.npz"), **out)
+    del sys.modules["diff_gaussian_rasterization"]
+    print("wrote n1_render.npz")
+
+
+SECTIONS = {"matching": gen_matching, "render": gen_render, "net": gen_net, "net_c4": gen_net_c4, "n1": gen_n1, "mono": gen_mono, "resize": gen_resize}
 
 
 def main(argv):

@@ -66,7 +66,7 @@ def load_splatt3r(path=None, device="cuda", cfg=None, seed: int = 1234, graphs: 
         path = local if os.path.exists(local) else None
     if path is not None:
         print(f"Loading Splatt3R model from {path}")
-        sd = {k: v.to(device) for k, v in load_state_dict_file(path).items()}
+        sd = load_state_dict_file(path, device)
     net = Splatt3RNet(cfg, state_dict=sd, seed=seed, device=device, graphs=graphs,
                       symmetric=symmetric)
     return Splatt3RModel(net, DecoderSplattingCUDA([0.0, 0.0, 0.0]).to(device))

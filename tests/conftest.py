@@ -37,3 +37,36 @@ def pytest_collection_modifyitems(config, items):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+# ------------------------------------------------- measured parity errors ---
+# Tests call parity(key, err=..., tol=..., ...) for every numeric comparison;
+# the values are printed in the terminal summary (so they land in the
+# committed test log) and written to gpurun_out/parity_errors.json.
+_PARITY: list = []
+
+
+@pytest.fixture
+def parity(request):
+    def record(key, **vals):
+        row = {"test": request.node.name, "key": key}
+        row.update({k: (float(v) if not isinstance(v, str) else v) for k, v in vals.items()})
+        _PARITY.append(row)
+        return row
+    return record
+
+
+def pytest_terminal_summary(terminalreporter):
+    if not _PARITY:
+        return
+    import json
+    terminalreporter.section("parity: measured errors vs stated tolerances")
+    for r in _PARITY:
+        terminalreporter.write_line(json.dumps(r, sort_keys=False))
+    out = os.path.join(REPO, "gpurun_out")
+    try:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "parity_errors.json"), "w") as f:
+            json.dump(_PARITY, f, indent=1)
+    except OSError:
+        pass

@@ -4,9 +4,10 @@ Golden files (oracle/gen_golden.py, section `net`) were produced by the
 reference's own torch modules (mast3r.model.AsymmetricMASt3R with the
 Splatt3R arguments) in fp32 on portable-PRNG weights; the GPU path computes
 matrix products with fp16 operands / fp32 accumulation (the reference runs
-TF32, the same 10-bit mantissa class).  Stated tolerances: token tensors
-max-abs error <= 2e-2 * max|ref|, head outputs <= 3e-2 relative (L_inf over
-max), descriptors <= 2e-2 absolute (unit vectors)."""
+TF32, the same 10-bit mantissa class).  Stated tolerances (measured
+values are recorded through the `parity` fixture and printed in the test
+log's summary; tolerances sit at about 2x the measured worst case):
+see TOL below.  Relative errors are L_inf(ours - ref) / L_inf(ref)."""
 import os
 
 import numpy as np
@@ -42,13 +43,47 @@ def test_prng_numpy_is_stable():
     np.testing.assert_allclose(s[13], -2.0)    # opacity split bias
 
 
+# stated tolerances (relative L_inf unless named otherwise), about 2x the
+# worst value measured on MI355X (r02: profiles/r02a_parity_errors.json):
+# tokens 1.06e-3, DPT stages 1.73e-3, head outputs 3.9e-3, desc 0.99e-3 abs,
+# rotations p99.9 4.1e-3, checksums 2.8e-3, Bp=2 vs Bp=1 1.6e-3.  The
+# reference's own CUDA path (TF32) is in the same class: pts3d 1.4e-3, sh
+# 2.5e-3 from its fp32 evaluation (tests/test_n1.py).
+TOL = {
+    "tokens": 2.5e-3,        # encoder features / decoder hook tokens
+    "stage": 4e-3,           # head-1 DPT stage captures
+    "head": 8e-3,            # pts3d, conf, desc_conf, scales, sh, opacities, means
+    "desc_abs": 2.5e-3,      # unit descriptors, absolute
+    "rot_p999": 1e-2,        # rotations: 99.9th percentile (|q| ~ 0 pixels flip)
+    "sum": 6e-3,             # full-size checksums, relative to sum |ref|
+    "batch": 4e-3,           # Bp = 2 pair plan vs Bp = 1 (tile choice only)
+}
+
+
+def _np(a):
+    return a.detach().float().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+
+
 def _err(a, b):
-    a = a.detach().float().cpu().numpy() if torch.is_tensor(a) else a
+    a = _np(a)
     return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12))
 
 
+def _check(parity, key, ours, ref, tol, metric="max_rel"):
+    """Record max-rel / p99.9-rel / mean-abs errors, assert `metric` <= tol."""
+    a = _np(ours).reshape(np.shape(ref)).astype(np.float64)
+    b = np.asarray(ref, np.float64)
+    d = np.abs(a - b)
+    sc = np.abs(b).max() + 1e-12
+    vals = dict(max_rel=d.max() / sc, p999_rel=np.percentile(d, 99.9) / sc,
+                mean_abs=d.mean(), max_abs=d.max())
+    parity(key, **vals, tol=tol, metric=metric)
+    assert vals[metric] <= tol, (key, metric, vals[metric], tol)
+    return vals
+
+
 @pytest.mark.gpu
-def test_small_model_stage_by_stage():
+def test_small_model_stage_by_stage(parity):
     """Per-stage errors of head 1's pts DPT vs the reference captures
     (localises a divergence instead of reporting only the end result)."""
     import torch.nn.functional as F
@@ -59,27 +94,20 @@ def test_small_model_stage_by_stage():
     f1, p1, _ = net._encode_image(torch.from_numpy(g["img1"]).cuda(), None)
     f2, p2, _ = net._encode_image(torch.from_numpy(g["img2"]).cuda(), None)
     r1, r2, pp = net.infer_pair(f1, p1, f2, p2, (48, 64))
-    errs = {}
     for k, ours in pp.stages.items():
         ref = g["stage_" + k]
         if k == "mlp":  # Mlp output [1, S, 6400] -> pixel_shuffle NHWC
             t = torch.from_numpy(ref).transpose(-1, -2).reshape(1, 6400, 3, 4)
             ref = F.pixel_shuffle(t, 16).permute(0, 2, 3, 1).numpy()
-        o = ours.float().cpu().numpy().reshape(ref.shape[0], -1, *ref.shape[2:]) if k != "ref4" else None
         if k == "ref4":  # ours is cropped to layer 3's grid (dpt_head.py:56)
             ref = ref[:, :3, :4]
-            o = ours.float().cpu().numpy()
-        errs[k] = _err(o.reshape(ref.shape), ref)
-    print({k: round(v, 5) for k, v in errs.items()})
-    for hk in (6, 9, 12):
-        pass
-    bad = {k: v for k, v in errs.items() if v > 2e-2}
-    assert not bad, f"stages over 2e-2: {bad} (all: {errs})"
+        o = _np(ours)
+        _check(parity, "stage_" + k, o.reshape(ref.shape), ref, TOL["stage"])
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tag,use_offsets", [("small_off", True), ("small_nooff", False)])
-def test_small_model_vs_reference_golden(tag, use_offsets):
+def test_small_model_vs_reference_golden(tag, use_offsets, parity):
     import dataclasses
     from splatt3r_amd import weights as W
     from splatt3r_amd.net import Splatt3RNet
@@ -90,37 +118,164 @@ def test_small_model_vs_reference_golden(tag, use_offsets):
     img2 = torch.from_numpy(g["img2"]).cuda()
     f1, p1, _ = net._encode_image(img1, None)
     f2, p2, _ = net._encode_image(img2, None)
-    assert _err(f1, g["feat1"]) < 2e-2 and _err(f2, g["feat2"]) < 2e-2
+    _check(parity, "feat1", f1, g["feat1"], TOL["tokens"])
+    _check(parity, "feat2", f2, g["feat2"], TOL["tokens"])
     np.testing.assert_array_equal(p1.cpu().numpy(), g["pos"])
     r1, r2, pp = net.infer_pair(f1, p1, f2, p2, (48, 64))
-    for k in ("pts3d", "conf", "desc_conf", "scales", "rotations", "sh", "opacities", "means"):
-        assert _err(r1[k], g["res1_" + k]) < 3e-2, ("res1", k, _err(r1[k], g["res1_" + k]))
-        assert _err(r2[k], g["res2_" + k]) < 3e-2, ("res2", k, _err(r2[k], g["res2_" + k]))
-    assert np.abs(r1["desc"].cpu().numpy() - g["res1_desc"]).max() < 2e-2
+    for ri, r in (("res1", r1), ("res2", r2)):
+        for k in ("pts3d", "conf", "desc_conf", "scales", "sh", "opacities", "means"):
+            _check(parity, f"{ri}_{k}", r[k], g[f"{ri}_{k}"], TOL["head"])
+        _check(parity, f"{ri}_desc", r["desc"], g[f"{ri}_desc"], TOL["desc_abs"], "max_abs")
+        _check(parity, f"{ri}_rotations", r["rotations"], g[f"{ri}_rotations"], TOL["rot_p999"],
+               "p999_rel")
     # the reference API path (13 token lists + per-head call) agrees with the fused path
     dec1, dec2 = net._decoder(f1, p1, f2, p2)
     dec1, dec2 = list(dec1), list(dec2)
     assert len(dec1) == cfg.dec_depth + 1
     for hk in cfg.hooks[1:]:
-        assert _err(dec1[hk], g[f"dec1_{hk}"]) < 2e-2, hk
-        assert _err(dec2[hk], g[f"dec2_{hk}"]) < 2e-2, hk
+        _check(parity, f"dec1_{hk}", dec1[hk], g[f"dec1_{hk}"], TOL["tokens"])
+        _check(parity, f"dec2_{hk}", dec2[hk], g[f"dec2_{hk}"], TOL["tokens"])
     h1 = net._downstream_head(1, [t.float() for t in dec1], torch.tensor([[48, 64]]))
-    assert _err(h1["pts3d"], g["res1_pts3d"]) < 3e-2
+    _check(parity, "api_head1_pts3d", h1["pts3d"], g["res1_pts3d"], TOL["head"])
 
 
-@pytest.mark.gpu
-def test_full_model_384x512_vs_reference_golden():
+def _full_size(parity, H, W_, name):
     from splatt3r_amd import weights as W
     from splatt3r_amd.net import Splatt3RNet
-    g = np.load(os.path.join(GOLDEN, "net_full_384x512.npz"))
+    g = np.load(os.path.join(GOLDEN, name))
     net = Splatt3RNet(W.FULL, seed=1234, graphs=True)
     f1, p1, _ = net._encode_image(torch.from_numpy(g["img1"]).cuda(), None)
     f2, p2, _ = net._encode_image(torch.from_numpy(g["img2"]).cuda(), None)
-    assert _err(f1[0, ::37], g["feat1_rows"]) < 2e-2
-    r1, r2, pp = net.infer_pair(f1, p1, f2, p2, (384, 512))
+    assert f1.shape[1] == (H // 16) * (W_ // 16)
+    _check(parity, "feat1_rows", f1[0, ::37], g["feat1_rows"], TOL["tokens"])
+    r1, r2, pp = net.infer_pair(f1, p1, f2, p2, (H, W_))
     for ri, r in (("1", r1), ("2", r2)):
-        for k in ("pts3d", "conf", "desc_conf", "scales", "sh", "opacities", "means"):
+        for k in ("pts3d", "conf", "desc", "desc_conf", "scales", "rotations", "sh", "opacities",
+                  "means"):
             sub = r[k][0, ::8, ::8]
-            assert _err(sub, g[f"res{ri}_{k}_sub"]) < 3e-2, (ri, k, _err(sub, g[f"res{ri}_{k}_sub"]))
+            ref = g[f"res{ri}_{k}_sub"]
+            if k == "desc":
+                _check(parity, f"res{ri}_{k}_sub", sub, ref, TOL["desc_abs"], "max_abs")
+            elif k == "rotations":
+                _check(parity, f"res{ri}_{k}_sub", sub, ref, TOL["rot_p999"], "p999_rel")
+            else:
+                _check(parity, f"res{ri}_{k}_sub", sub, ref, TOL["head"])
             s = float(r[k][0].double().sum())
-            assert abs(s - float(g[f"res{ri}_{k}_sum"])) <= 2e-2 * float(g[f"res{ri}_{k}_abs"]) + 1e-6, k
+            rel = abs(s - float(g[f"res{ri}_{k}_sum"])) / float(g[f"res{ri}_{k}_abs"])
+            parity(f"res{ri}_{k}_sum", rel=rel, tol=TOL["sum"])
+            assert rel <= TOL["sum"], (ri, k, rel)
+
+
+@pytest.mark.gpu
+def test_full_model_384x512_vs_reference_golden(parity):
+    """C2/C5 size (768 tokens)."""
+    _full_size(parity, 384, 512, "net_full_384x512.npz")
+
+
+@pytest.mark.gpu
+def test_full_model_320x512_vs_reference_golden(parity):
+    """C4 size: EuRoC 752x480 -> 512x320 (splatt3r_utils.py:668-679), 640 tokens."""
+    _full_size(parity, 320, 512, "net_full_320x512.npz")
+
+
+@pytest.mark.gpu
+def test_pair_batch_bp2_matches_bp1_and_golden(parity):
+    """The DP shard unit: one Bp = 2 grouped pair plan over (1,2) and (2,1)
+    equals two Bp = 1 runs (splatt3r_utils.py:466-499 loops pairs one at a
+    time), and its pair 0 matches the reference golden."""
+    from splatt3r_amd import weights as W
+    from splatt3r_amd.net import Splatt3RNet
+    g = np.load(os.path.join(GOLDEN, "net_small_off.npz"))
+    net = Splatt3RNet(W.SMALL, seed=1234, graphs=False)
+    f1, p1, _ = net._encode_image(torch.from_numpy(g["img1"]).cuda(), None)
+    f2, p2, _ = net._encode_image(torch.from_numpy(g["img2"]).cuda(), None)
+    keys = ("pts3d", "conf", "desc", "desc_conf", "scales", "sh", "opacities", "means")
+    a1, a2, _ = net.infer_pair(f1, p1, f2, p2, (48, 64))
+    a1, a2 = {k: a1[k].clone() for k in keys}, {k: a2[k].clone() for k in keys}
+    b1, b2, _ = net.infer_pair(f2, p2, f1, p1, (48, 64))
+    b1, b2 = {k: b1[k].clone() for k in keys}, {k: b2[k].clone() for k in keys}
+    R1, R2, _ = net.infer_pair(torch.cat([f1, f2]), torch.cat([p1, p2]), torch.cat([f2, f1]),
+                               torch.cat([p2, p1]), (48, 64))
+    for k in keys:
+        _check(parity, f"bp2_pair0_res1_{k}", R1[k][0], _np(a1[k][0]), TOL["batch"])
+        _check(parity, f"bp2_pair0_res2_{k}", R2[k][0], _np(a2[k][0]), TOL["batch"])
+        _check(parity, f"bp2_pair1_res1_{k}", R1[k][1], _np(b1[k][0]), TOL["batch"])
+        _check(parity, f"bp2_pair1_res2_{k}", R2[k][1], _np(b2[k][0]), TOL["batch"])
+    for k in ("pts3d", "conf", "means"):
+        _check(parity, f"bp2_pair0_vs_golden_{k}", R1[k][0], g["res1_" + k][0], TOL["head"])
+
+
+def _small_model(use_offsets=True):
+    import dataclasses
+    from splatt3r_amd import weights as W
+    from splatt3r_amd.net import Splatt3RNet
+    from splatt3r_amd.render import DecoderSplattingCUDA
+    from splatt3r_amd.splatt3r_utils import Splatt3RModel
+    cfg = dataclasses.replace(W.SMALL, use_offsets=use_offsets)
+    net = Splatt3RNet(cfg, seed=1234, graphs=False)
+    return Splatt3RModel(net, DecoderSplattingCUDA([0.0, 0.0, 0.0]).cuda())
+
+
+@pytest.mark.gpu
+def test_match_asymmetric_vs_oracle_chain(parity):
+    """splatt3r_match_asymmetric (splatt3r_utils.py:610-644): outputs vs the
+    reference network golden, idx/valid bit-exact vs oracle.match on the
+    same pointmaps/descriptors, and agreement with the full reference chain
+    (golden head outputs -> oracle matching)."""
+    import oracle
+    from splatt3r_amd.frame import create_frame
+    from splatt3r_amd.splatt3r_utils import (splatt3r_asymmetric_inference,
+                                             splatt3r_match_asymmetric)
+    g = np.load(os.path.join(GOLDEN, "net_small_off.npz"))
+    model = _small_model()
+    fi = create_frame(0, torch.from_numpy(g["img1"]), device="cuda")
+    fj = create_frame(1, torch.from_numpy(g["img2"]), device="cuda")
+    idx, valid, Xii, Cii, Qii, Xji, Cji, Qji = splatt3r_match_asymmetric(model, fi, fj)
+    hw = 48 * 64
+    assert idx.shape == (1, hw) and idx.dtype == torch.int64
+    assert valid.shape == (1, hw, 1) and valid.dtype == torch.bool
+    assert Xii.shape == (hw, 3) and Cii.shape == (hw, 1) and Qji.shape == (hw, 1)
+    _check(parity, "asym_Xii", Xii, g["res1_pts3d"].reshape(hw, 3), TOL["head"])
+    _check(parity, "asym_Xji", Xji, g["res2_pts3d"].reshape(hw, 3), TOL["head"])
+    _check(parity, "asym_Cii", Cii, g["res1_conf"].reshape(hw, 1), TOL["head"])
+    _check(parity, "asym_Qii", Qii, g["res1_desc_conf"].reshape(hw, 1), TOL["head"])
+    _check(parity, "asym_Qji", Qji, g["res2_desc_conf"].reshape(hw, 1), TOL["head"])
+    assert fi.gaussian_pred is not None and fi.gaussian_pred_cross is not None
+    _check(parity, "asym_gauss_means", fi.gaussian_pred["means"], g["res1_means"], TOL["head"])
+    X, C, D, Q, _ = splatt3r_asymmetric_inference(model, fi, fj)
+    idx_o, valid_o = oracle.match(_np(X[:1]), _np(X[1:]), _np(D[:1]), _np(D[1:]))
+    np.testing.assert_array_equal(idx.cpu().numpy(), idx_o)
+    np.testing.assert_array_equal(valid.cpu().numpy(), valid_o)
+    # full reference chain (fp32 golden head outputs -> oracle matching); the
+    # reference CUDA path's own agreement with it (TF32 head outputs,
+    # n1_render.npz) sets the bar: matching is discrete, and with
+    # portable-PRNG weights no pixel passes the occlusion test, so iter_proj
+    # lands far from its start wherever the projections differ slightly
+    idx_r, valid_r = oracle.match(g["res1_pts3d"], g["res2_pts3d"], g["res1_desc"], g["res2_desc"])
+    n1 = np.load(os.path.join(GOLDEN, "n1_render.npz"))
+    ref_agree = float((n1["small_off_match_tf32_idx"] == idx_r).mean())
+    agree = float((idx.cpu().numpy() == idx_r).mean())
+    vagree = float((valid.cpu().numpy() == valid_r).mean())
+    tol = ref_agree - 0.05
+    parity("asym_idx_agreement_vs_reference_chain", frac=agree, valid_agree=vagree,
+           ref_tf32_frac=ref_agree, tol=tol)
+    assert agree >= tol and vagree >= float((n1["small_off_match_tf32_valid"] == valid_r).mean())
+
+
+@pytest.mark.gpu
+def test_inference_mono_vs_reference_golden(parity):
+    """splatt3r_inference_mono (splatt3r_utils.py:503-536) vs the reference
+    decoder run on (img, img) (net_small_mono.npz)."""
+    from splatt3r_amd.frame import create_frame
+    from splatt3r_amd.splatt3r_utils import splatt3r_inference_mono
+    g = np.load(os.path.join(GOLDEN, "net_small_mono.npz"))
+    model = _small_model()
+    f = create_frame(0, torch.from_numpy(g["img"]), device="cuda")
+    Xii, Cii = splatt3r_inference_mono(model, f)
+    hw = 48 * 64
+    assert Xii.shape == (hw, 3) and Cii.shape == (hw, 1)
+    _check(parity, "mono_Xii", Xii, g["res11_pts3d"].reshape(hw, 3), TOL["head"])
+    _check(parity, "mono_Cii", Cii, g["res11_conf"].reshape(hw, 1), TOL["head"])
+    for k in ("means", "opacities", "sh", "scales"):
+        _check(parity, f"mono_pred_{k}", f.gaussian_pred[k], g["res11_" + k], TOL["head"])
+        _check(parity, f"mono_cross_{k}", f.gaussian_pred_cross[k], g["res21_" + k], TOL["head"])
