@@ -46,6 +46,39 @@ int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, float depth_min
                            float depth_max_percentile, float max_scale, float min_confidence,
                            void* workspace, float* out, int64_t* count_dev, void* stream);
 
+/* ---- SharedGaussians map buffer (splatt3r_slam/frame.py:357-463) ----
+ * Structure-of-arrays world map with a device-side count, so appends are
+ * stream-ordered with no host sync.  Replaces SharedGaussians.append /
+ * get_all / clear; the viz full-map render (visualization.py:467-600)
+ * rasterizes means/cov_triu/colors/opacities[:n] with colors_precomp. */
+typedef struct {
+  float* means;       /* [cap, 3] world centres      */
+  float* cov_triu;    /* [cap, 6] xx xy xz yy yz zz  */
+  float* colors;      /* [cap, 3] RGB                */
+  float* opacities;   /* [cap]                       */
+  int32_t* kf_id;     /* [cap] source keyframe       */
+  int64_t* n;         /* device: live Gaussians      */
+  int64_t cap;        /* max_gaussians               */
+} s3w_map;
+
+size_t s3w_map_append_workspace_bytes(int64_t n_max);
+
+/* SharedGaussians.append(means, cov_triu, colors, opacities, kf_idx,
+ * opacity_threshold) on the world records of s3w_gaussians_to_world
+ * (records [n_max, 13], *count_dev valid): keep opacity > threshold in
+ * record order; if the map is full (n == cap) first move the newest half
+ * to the front (FIFO eviction of the oldest half, frame.py:423-437), then
+ * append min(kept, cap - n) records with kf_id = kf_idx. */
+int s3w_map_append(const s3w_map* map, const float* records, const int64_t* count_dev,
+                   int64_t n_max, float opacity_threshold, int32_t kf_idx, void* workspace,
+                   void* stream);
+
+/* Scale-invariant copies for the full-map render (visualization.py:534-585):
+ * means_out = means * s, cov_out = cov_triu * s2 for i < *n_dev (n_max
+ * bounds the launch). */
+int s3w_map_scale(const float* means, const float* cov_triu, const int64_t* n_dev, int64_t n_max,
+                  float s, float s2, float* means_out, float* cov_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,7 @@ reference here (its module needs lietorch/cv2); this restatement is pinned
 by tests/test_gaussians.py's hand-checked cases."""
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 C0 = 0.28209479177387814
@@ -62,3 +63,39 @@ def gaussians_to_world(preds, img, M, spatial_stride=1, depth_min=0.05,
     if not outs:
         return None
     return tuple(torch.cat(x, 0) for x in zip(*outs))
+
+
+class MapRef:
+    """numpy restatement of SharedGaussians (splatt3r_slam/frame.py:357-463):
+    opacity filter, FIFO half-eviction when full, truncating append."""
+
+    def __init__(self, cap):
+        self.cap = cap
+        self.n = 0
+        self.means = np.zeros((cap, 3), np.float32)
+        self.cov = np.zeros((cap, 6), np.float32)
+        self.colors = np.zeros((cap, 3), np.float32)
+        self.opac = np.zeros(cap, np.float32)
+        self.kf = np.zeros(cap, np.int32)
+
+    def append(self, means, cov, colors, opac, kf_idx, thr):
+        m = opac > thr
+        means, cov, colors, opac = means[m], cov[m], colors[m], opac[m]
+        n_new = means.shape[0]
+        if n_new == 0:
+            return
+        n = self.n
+        space = self.cap - n
+        if space <= 0:
+            half = self.cap // 2
+            for a in (self.means, self.cov, self.colors, self.opac, self.kf):
+                a[:half] = a[self.cap - half:].copy()
+            n = half
+            space = self.cap - n
+        k = min(n_new, space)
+        self.means[n:n + k] = means[:k]
+        self.cov[n:n + k] = cov[:k]
+        self.colors[n:n + k] = colors[:k]
+        self.opac[n:n + k] = opac[:k]
+        self.kf[n:n + k] = kf_idx
+        self.n = n + k

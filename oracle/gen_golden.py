@@ -3,7 +3,7 @@ reference from /root/reference (this container only; the GPU box never reads
 /root/reference).  Committed outputs are data only (inputs + expected
 outputs), never reference source.
 
-  python oracle/gen_golden.py [section ...]     sections: matching, net, net_c4, n1, mono, resize, render
+  python oracle/gen_golden.py [section ...]     sections: matching, net, net_c4, n1, mono, resize, viz, render
 
 matching : splatt3r_slam/image.py img_gradient (imported) driven exactly as
            splatt3r_slam/matching.py:25-49 prep_for_iter_proj does.
@@ -388,6 +388,110 @@ def tf32_mode():
     return TF32Mode()
 
 
+def gen_viz():
+    """Full-map render (A14): the reference's own `_render_gs_interactive`
+    (splatt3r_slam/visualization.py:467-600; function text compiled from the
+    file -- the module needs moderngl/imgui/in3d) driven with a synthetic
+    SharedGaussians map and GL camera, a stub rasterizer capturing what it
+    hands GaussianRasterizer, then oracle.raster on the captured inputs.
+    Saved: the map, the camera, the captured settings/inputs and the
+    clamped HWC image the function returns."""
+    import ast
+    import types
+    sys.path.insert(0, os.path.dirname(HERE))
+    import oracle
+    captured = {}
+
+    class Settings(tuple):
+        def __new__(cls, **kw):
+            o = tuple.__new__(cls, tuple(kw.values()))
+            o.kw = kw
+            return o
+
+    class Rasterizer(torch.nn.Module):
+        def __init__(self, rs):
+            super().__init__()
+            self.rs = rs
+
+        def forward(self, **kw):
+            captured["settings"] = self.rs.kw
+            captured["inputs"] = kw
+            h, w = self.rs.kw["image_height"], self.rs.kw["image_width"]
+            return torch.zeros(3, h, w), torch.zeros(kw["means3D"].shape[0], dtype=torch.int32)
+
+    stub = types.ModuleType("diff_gaussian_rasterization")
+    stub.GaussianRasterizationSettings = Settings
+    stub.GaussianRasterizer = Rasterizer
+    sys.modules["diff_gaussian_rasterization"] = stub
+    # import splatt3r_core.src.pixelsplat_src.* without running
+    # splatt3r_core/__init__.py (it imports lightning, absent here)
+    pkg = types.ModuleType("splatt3r_core")
+    pkg.__path__ = [os.path.join(REF, "splatt3r_core")]
+    sys.modules["splatt3r_core"] = pkg
+    sys.path.insert(0, os.path.join(REF, "splatt3r_core", "src", "pixelsplat_src"))
+    path = os.path.join(REF, "splatt3r_slam", "visualization.py")
+    tree = ast.parse(open(path).read())
+    fn = None
+    for node in ast.walk(tree):
+        if isinstance(node, ast.FunctionDef) and node.name == "_render_gs_interactive":
+            fn = node
+    ns = {"torch": torch, "np": np, "math": __import__("math"),
+          "GaussianRasterizationSettings": Settings, "GaussianRasterizer": Rasterizer}
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), path, "exec"), ns)
+    render_fn = ns["_render_gs_interactive"]
+
+    rng = np.random.default_rng(11)
+    n = 30000
+    means = rng.normal(size=(n, 3)).astype(np.float32) * np.float32([0.6, 0.4, 0.5]) \
+        + np.float32([0.1, -0.05, 3.0])
+    sc = np.exp(rng.uniform(np.log(0.01), np.log(0.05), (n, 3)))
+    q = rng.normal(size=(n, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    x, y, z, w = q.T
+    R = np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+                  2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                  2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)], -1)
+    R = R.reshape(n, 3, 3)
+    cov = np.einsum("nik,nk,njk->nij", R, sc * sc, R)
+    iu = np.triu_indices(3)
+    cov6 = cov[:, iu[0], iu[1]].astype(np.float32)
+    colors = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    opac = rng.uniform(0.3, 1.0, n).astype(np.float32)
+    # OpenCV camera-to-world: small yaw and offset; GL world-to-camera from it
+    th = 0.1
+    T_WC_cv = np.eye(4)
+    T_WC_cv[:3, :3] = [[np.cos(th), 0, np.sin(th)], [0, 1, 0], [-np.sin(th), 0, np.cos(th)]]
+    T_WC_cv[:3, 3] = [-0.2, 0.05, -0.3]
+    cv2gl = np.diag([1.0, -1.0, -1.0, 1.0])
+    T_CW_gl = (cv2gl @ np.linalg.inv(T_WC_cv)).astype(np.float32)
+    ns_ = types.SimpleNamespace
+    gm = tuple(torch.from_numpy(a) for a in (means, cov6, colors, opac))
+    self_ = ns_(shared_gaussians=ns_(get_all=lambda: gm),
+                camera=ns_(viewport_size=(640, 480), T_CW=T_CW_gl, proj_mat=ns_(hfov=90.0)),
+                gs_resolution_scale=0.5)
+    render_fn(self_)
+    st, ins = captured["settings"], captured["inputs"]
+    sd = {k: (st[k].detach().numpy() if torch.is_tensor(st[k]) else st[k]) for k in st}
+    o = oracle.raster(sd, ins["means3D"].numpy(), ins["opacities"].numpy(),
+                      colors_precomp=ins["colors_precomp"].numpy(),
+                      cov3D_precomp=ins["cov3D_precomp"].numpy(), nthreads=8)
+    img = np.clip(o["color"], 0, 1).transpose(1, 2, 0)
+    out = dict(means=means, cov6=cov6, colors=colors, opacities=opac, T_CW_gl=T_CW_gl,
+               viewport=np.int32([640, 480]), hfov=np.float32(90.0), res_scale=np.float32(0.5),
+               image_hwc=img, num_rendered=np.int64(o["num_rendered"]))
+    for k in ("tanfovx", "tanfovy", "image_height", "image_width"):
+        out["settings_" + k] = np.asarray(sd[k])
+    for k in ("bg", "viewmatrix", "projmatrix", "campos"):
+        out["settings_" + k] = np.asarray(sd[k], np.float32)
+    out["in_means3D"] = ins["means3D"].numpy()
+    out["in_cov3D_precomp"] = ins["cov3D_precomp"].numpy()
+    np.savez_compressed(os.path.join(GOLDEN, "viz_render.npz"), **out)
+    for m in ("diff_gaussian_rasterization", "splatt3r_core"):
+        del sys.modules[m]
+    print("wrote viz_render.npz", img.shape, "mean", float(img.mean()),
+          "num_rendered", o["num_rendered"])
+
+
 def _sim3_matrix(T):
     """lietorch Sim3 data [t, q(xyzw), s] -> 4x4 [sR | t] (fp64 -> fp32), the
     matrix splatt3r_utils.py:153-165 builds through SE3.matrix()."""
@@ -554,7 +658,7 @@ def gen_n1():
     print("wrote n1_render.npz")
 
 
-SECTIONS = {"matching": gen_matching, "render": gen_render, "net": gen_net, "net_c4": gen_net_c4, "n1": gen_n1, "mono": gen_mono, "resize": gen_resize}
+SECTIONS = {"matching": gen_matching, "render": gen_render, "net": gen_net, "net_c4": gen_net_c4, "n1": gen_n1, "mono": gen_mono, "resize": gen_resize, "viz": gen_viz}
 
 
 def main(argv):

@@ -7,6 +7,13 @@
 // scan      hipcub exclusive sum of the flags (stable compaction order)
 // k_emit    world transform, covariance, colour, opacity -> 13-float records
 // All stream-ordered; the only host-visible result is *count_dev.
+//
+// Map buffer (SharedGaussians, frame.py:357-463):
+// k_map_flags  opacity > threshold over the valid records
+// scan         hipcub exclusive sum (record-order compaction)
+// k_map_evict  if full: newest half -> front (one grid-stride copy), and the
+//              post-eviction count for the append
+// k_map_emit   scatter kept records into the SoA map, update the count
 #include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
@@ -206,6 +213,144 @@ extern "C" int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, floa
   size_t sb = w.scan_bytes;
   S3_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, sb, w.flags, w.offsets, (int)n, st));
   k_emit<<<blocks, kThreads, 0, st>>>(n, g, *v, T_WC, w.flags, w.offsets, out, count_dev);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+// ------------------------------------------------------------ map buffer --
+namespace {
+
+struct MapWs {
+  uint32_t* flags;
+  uint32_t* offsets;
+  int64_t* n0;  // count after eviction (read by k_map_emit)
+  void* scan_tmp;
+  size_t scan_bytes;
+};
+
+MapWs carve_map(void* base, int64_t n, size_t* total = nullptr) {
+  char* p = static_cast<char*>(base);
+  char* p0 = p;
+  MapWs w;
+  w.flags = (uint32_t*)p; p += align256(sizeof(uint32_t) * n);
+  w.offsets = (uint32_t*)p; p += align256(sizeof(uint32_t) * n);
+  w.n0 = (int64_t*)p; p += 256;
+  w.scan_bytes = scan_bytes(n);
+  w.scan_tmp = p; p += align256(w.scan_bytes);
+  if (total) *total = (size_t)(p - p0);
+  return w;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_map_flags(int64_t n_max, const float* __restrict__ rec, const int64_t* __restrict__ count,
+            float thr, uint32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n_max) return;
+  flags[i] = (i < *count && rec[i * 13 + 12] > thr) ? 1u : 0u;
+}
+
+// grid-stride: every block copies a slice of the newest half when full
+__global__ void __launch_bounds__(kThreads)
+k_map_evict(s3w_map m, int64_t* __restrict__ n0) {
+  const int64_t n = *m.n;
+  const int64_t half = m.cap / 2;
+  const bool full = n >= m.cap;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n0 = full ? half : n;
+  if (!full) return;
+  const int64_t src = m.cap - half;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < half;
+       i += (int64_t)gridDim.x * kThreads) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) m.means[i * 3 + k] = m.means[(src + i) * 3 + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) m.cov_triu[i * 6 + k] = m.cov_triu[(src + i) * 6 + k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) m.colors[i * 3 + k] = m.colors[(src + i) * 3 + k];
+    m.opacities[i] = m.opacities[src + i];
+    m.kf_id[i] = m.kf_id[src + i];
+  }
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_map_emit(int64_t n_max, s3w_map m, const float* __restrict__ rec,
+           const uint32_t* __restrict__ flags, const uint32_t* __restrict__ offsets,
+           const int64_t* __restrict__ n0p, int32_t kf) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n_max) return;
+  const int64_t n0 = *n0p;
+  const int64_t space = m.cap - n0;
+  if (i == n_max - 1) {
+    const int64_t kept = (int64_t)offsets[i] + flags[i];
+    *m.n = n0 + (kept < space ? kept : space);
+  }
+  if (!flags[i] || (int64_t)offsets[i] >= space) return;
+  const int64_t j = n0 + offsets[i];
+  const float* r = rec + i * 13;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) m.means[j * 3 + k] = r[k];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) m.cov_triu[j * 6 + k] = r[3 + k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) m.colors[j * 3 + k] = r[9 + k];
+  m.opacities[j] = r[12];
+  m.kf_id[j] = kf;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_map_scale(const float* __restrict__ means, const float* __restrict__ cov,
+            const int64_t* __restrict__ n_dev, int64_t n_max, float s, float s2,
+            float* __restrict__ mo, float* __restrict__ co) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n_max || i >= *n_dev) return;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) mo[i * 3 + k] = means[i * 3 + k] * s;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) co[i * 6 + k] = cov[i * 6 + k] * s2;
+}
+
+}  // namespace
+
+extern "C" size_t s3w_map_append_workspace_bytes(int64_t n_max) {
+  size_t n = 0;
+  carve_map(nullptr, n_max > 0 ? n_max : 1, &n);
+  return n;
+}
+
+extern "C" int s3w_map_append(const s3w_map* map, const float* records, const int64_t* count_dev,
+                              int64_t n_max, float opacity_threshold, int32_t kf_idx,
+                              void* workspace, void* stream) {
+  S3_REQUIRE(map && map->means && map->cov_triu && map->colors && map->opacities && map->kf_id &&
+                 map->n && map->cap > 0,
+             "s3w_map_append: bad map");
+  S3_REQUIRE(n_max >= 0 && n_max < ((int64_t)1 << 31), "s3w_map_append: bad n_max");
+  if (n_max == 0) return S3_OK;
+  S3_REQUIRE(records && count_dev && workspace, "s3w_map_append: null argument");
+  hipStream_t st = s3::as_stream(stream);
+  MapWs w = carve_map(workspace, n_max);
+  const int blocks = (int)s3::cdiv(n_max, kThreads);
+  k_map_flags<<<blocks, kThreads, 0, st>>>(n_max, records, count_dev, opacity_threshold,
+                                           w.flags);
+  S3_LAUNCH_CHECK();
+  size_t sb = w.scan_bytes;
+  S3_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, sb, w.flags, w.offsets, (int)n_max, st));
+  const int64_t half = map->cap / 2;
+  const int eb = (int)std::max<int64_t>(1, std::min<int64_t>(s3::cdiv(half, kThreads), 2048));
+  k_map_evict<<<eb, kThreads, 0, st>>>(*map, w.n0);
+  S3_LAUNCH_CHECK();
+  k_map_emit<<<blocks, kThreads, 0, st>>>(n_max, *map, records, w.flags, w.offsets, w.n0,
+                                          kf_idx);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+extern "C" int s3w_map_scale(const float* means, const float* cov_triu, const int64_t* n_dev,
+                             int64_t n_max, float s, float s2, float* means_out, float* cov_out,
+                             void* stream) {
+  S3_REQUIRE(n_max >= 0, "s3w_map_scale: n_max < 0");
+  if (n_max == 0) return S3_OK;
+  S3_REQUIRE(means && cov_triu && n_dev && means_out && cov_out, "s3w_map_scale: null argument");
+  k_map_scale<<<(int)s3::cdiv(n_max, kThreads), kThreads, 0, s3::as_stream(stream)>>>(
+      means, cov_triu, n_dev, n_max, s, s2, means_out, cov_out);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

@@ -50,7 +50,7 @@ struct GeomState {
   // z/w = kept-tile mask (bit (y - y0) * w + (x - x0)) for rects of 2..64
   // tiles; one 16-B gather serves the depth-ordered passes
   uint4* dup;
-  uint32_t* offsets;
+  uint64_t* total;         // instances over all Gaussians (64-bit: no wrap)
   void* scan_tmp;
   size_t scan_bytes;
   // depth-ordered duplication (gsr_render)
@@ -71,10 +71,16 @@ struct HighWord {
 };
 typedef hipcub::TransformInputIterator<uint32_t, HighWord, const uint64_t*> TilesIt;
 
+// tiles touched per Gaussian, widened so the total cannot wrap
+struct Widen {
+  __host__ __device__ uint64_t operator()(uint32_t v) const { return (uint64_t)v; }
+};
+typedef hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t*> Tiles64It;
+
 size_t scan_temp_bytes(int64_t P) {
   size_t bytes = 0, b2 = 0;
-  hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                   (int)P);
+  hipcub::DeviceReduce::Sum(nullptr, bytes, Tiles64It(nullptr, Widen()), (uint64_t*)nullptr,
+                            (int)P);
   hipcub::DeviceScan::InclusiveSum(nullptr, b2, TilesIt(nullptr, HighWord()),
                                    (uint32_t*)nullptr, (int)P);
   return bytes > b2 ? bytes : b2;
@@ -94,7 +100,8 @@ size_t depth_sort_temp_bytes(int64_t n) {
   return bytes;
 }
 
-GeomState carve_geom(void* base, int64_t P) {
+// One layout routine serves both sizing (base == nullptr) and carving.
+GeomState carve_geom(void* base, int64_t P, size_t* total = nullptr) {
   Carver c{static_cast<char*>(base)};
   GeomState g;
   g.depth = c.take<float>(P);
@@ -105,7 +112,7 @@ GeomState carve_geom(void* base, int64_t P) {
   g.clamped = c.take<uint8_t>(P * 3);
   g.tiles = c.take<uint32_t>(P);
   g.dup = c.take<uint4>(P);
-  g.offsets = c.take<uint32_t>(P);
+  g.total = c.take<uint64_t>(1);
   g.scan_bytes = scan_temp_bytes(P);
   g.scan_tmp = c.take<char>(g.scan_bytes);
   g.dkey = c.take<uint32_t>(P);
@@ -115,18 +122,13 @@ GeomState carve_geom(void* base, int64_t P) {
   g.offsets_sorted = c.take<uint32_t>(P);
   g.dsort_bytes = depth_sort_temp_bytes(P);
   g.dsort_tmp = c.take<char>(g.dsort_bytes);
+  if (total) *total = c.off;
   return g;
 }
 size_t geom_bytes(int64_t P) {
-  Carver c{nullptr};
-  c.take<float>(P); c.take<float4>(P); c.take<float4>(P); c.take<float>(P * 3);
-  c.take<float>(P * 6); c.take<uint8_t>(P * 3); c.take<uint32_t>(P); c.take<uint4>(P);
-  c.take<uint32_t>(P);
-  c.take<char>(scan_temp_bytes(P));
-  c.take<uint32_t>(P); c.take<uint32_t>(P); c.take<uint64_t>(P); c.take<uint64_t>(P);
-  c.take<uint32_t>(P); c.take<uint32_t>(P);
-  c.take<char>(depth_sort_temp_bytes(P));
-  return c.off;
+  size_t n = 0;
+  carve_geom(nullptr, P, &n);
+  return n;
 }
 
 struct BinningState {
@@ -140,7 +142,7 @@ struct BinningState {
 
 size_t sort_temp_bytes(int64_t R) { return key32_sort_temp_bytes(R); }
 
-BinningState carve_binning(void* base, int64_t R) {
+BinningState carve_binning(void* base, int64_t R, size_t* total = nullptr) {
   Carver c{static_cast<char*>(base)};
   BinningState b;
   b.keys_unsorted = c.take<uint32_t>(R);
@@ -149,13 +151,13 @@ BinningState carve_binning(void* base, int64_t R) {
   b.vals = c.take<uint32_t>(R);
   b.sort_bytes = sort_temp_bytes(R);
   b.sort_tmp = c.take<char>(b.sort_bytes);
+  if (total) *total = c.off;
   return b;
 }
 size_t binning_bytes(int64_t R) {
-  Carver c{nullptr};
-  c.take<uint32_t>(R); c.take<uint32_t>(R); c.take<uint32_t>(R); c.take<uint32_t>(R);
-  c.take<char>(sort_temp_bytes(R));
-  return c.off;
+  size_t n = 0;
+  carve_binning(nullptr, R, &n);
+  return n;
 }
 
 struct ImageState {
@@ -163,20 +165,20 @@ struct ImageState {
   uint32_t* n_contrib; // [H*W]
   float* final_T;      // [H*W]
 };
-ImageState carve_image(void* base, int H, int W) {
+ImageState carve_image(void* base, int H, int W, size_t* total = nullptr) {
   Carver c{static_cast<char*>(base)};
   int tiles = ((W + BX - 1) / BX) * ((H + BY - 1) / BY);
   ImageState s;
   s.ranges = c.take<uint2>(tiles);
   s.n_contrib = c.take<uint32_t>((size_t)H * W);
   s.final_T = c.take<float>((size_t)H * W);
+  if (total) *total = c.off;
   return s;
 }
 size_t image_bytes(int H, int W) {
-  Carver c{nullptr};
-  int tiles = ((W + BX - 1) / BX) * ((H + BY - 1) / BY);
-  c.take<uint2>(tiles); c.take<uint32_t>((size_t)H * W); c.take<float>((size_t)H * W);
-  return c.off;
+  size_t n = 0;
+  carve_image(nullptr, H, W, &n);
+  return n;
 }
 
 int tile_bits(int tiles) {
@@ -926,12 +928,16 @@ int gsr_preprocess(const gsr_settings* s, int64_t P, int M, const float* means3D
   S3_LAUNCH_CHECK();
   tmark(1, st);
   size_t tb = g.scan_bytes;
-  S3_HIP(hipcub::DeviceScan::InclusiveSum(g.scan_tmp, tb, g.tiles, g.offsets, (int)P, st));
+  S3_HIP(hipcub::DeviceReduce::Sum(g.scan_tmp, tb, Tiles64It(g.tiles, Widen()), g.total, (int)P,
+                                   st));
   tmark(2, st);
-  uint32_t last = 0;
-  S3_HIP(hipMemcpyAsync(&last, g.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  uint64_t total = 0;
+  S3_HIP(hipMemcpyAsync(&total, g.total, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   S3_HIP(hipStreamSynchronize(st));
-  *num_rendered = last;
+  // the binning pass indexes instances with 32-bit offsets
+  S3_REQUIRE(total < ((uint64_t)1 << 32), "gsr_preprocess: %llu tile instances exceed 2^32",
+             (unsigned long long)total);
+  *num_rendered = (int64_t)total;
   return S3_OK;
 }
 

@@ -33,34 +33,29 @@ import torch
 import lietorch
 from splatt3r_amd.config import config
 from splatt3r_amd.frame import Frame, Keyframes, Mode, create_frame
-from splatt3r_amd.splatt3r_utils import (gaussians_to_world, splatt3r_inference_mono,
-                                         splatt3r_render)
+from splatt3r_amd.gaussian_map import SharedGaussians, should_append_gaussians
+from splatt3r_amd.splatt3r_utils import (_sim3_to_4x4, gaussians_to_world, splatt3r_inference_mono,
+                                         splatt3r_render, world_records)
 from splatt3r_amd.tracker import FrameTracker
 
-
-def should_append_gaussians(add_new_kf, frame_idx, current_T_WC, last_append_T_WC,
-                            last_append_frame_idx, min_translation, min_frame_gap) -> bool:
-    """main.py:54-73."""
-    if add_new_kf or last_append_T_WC is None:
-        return True
-    if frame_idx - last_append_frame_idx < min_frame_gap:
-        return False
-    t_cur = current_T_WC.matrix()[0, :3, 3]
-    t_last = last_append_T_WC.matrix()[0, :3, 3]
-    return float(torch.linalg.norm(t_cur - t_last)) >= min_translation
+__all__ = ["Frontend", "should_append_gaussians"]
 
 
 class Frontend:
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
                  readback=True, enc_batch=1, main_priority=None, late_prefetch=False,
-                 viz=False):
+                 viz=False, max_gaussians=4 * 1024 * 1024):
         self.model = model
         # viz: the reference's enable_gs_viz (main.py:357, `not --no-viz`).
         # Only then does it record the last append (main.py:434-435,488-489);
         # under --no-viz last_gs_append_T_WC stays None, so should_append is
         # always true and gaussians_to_world runs on every tracked frame.
         self.viz = viz
+        # the world map the viz process renders (frame.py:357-463); appended
+        # to with opacity > 0.3 (main.py:426-433, 480-487)
+        self.gmap = SharedGaussians(max_gaussians=max_gaussians, device=device) if viz else None
+        self.map_opacity_threshold = 0.3
         self.device = device
         self.K = K
         self.late_prefetch = late_prefetch
@@ -168,7 +163,21 @@ class Frontend:
             self._rb_events[k] = ev
             self._last_render, self._rb_event = host, ev
 
-    def _to_world(self, frame):
+    def _to_world(self, frame, kf_idx):
+        if self.gmap is not None:
+            # viz on: the world records of gaussians_to_world go straight
+            # into the device map (stream-ordered, no host sync)
+            a = self.gs_args
+            T = _sim3_to_4x4(frame.T_WC)[0].to(frame.img.device)
+            pred = frame.gaussian_pred
+            for b in range(pred["means"].shape[0]):
+                view = {k: v[b] for k, v in pred.items()}
+                rec, cnt = world_records(view, frame.img[min(b, frame.img.shape[0] - 1)], T,
+                                         max(1, int(a["spatial_stride"])), 0.05,
+                                         a["depth_max_percentile"], a["max_scale"],
+                                         a["min_confidence"])
+                self.gmap.append_records(rec, cnt, kf_idx, self.map_opacity_threshold)
+            return True
         gs = gaussians_to_world(frame, **self.gs_args)
         if gs is not None:
             self.stats["gaussians_world"] += int(gs[0].shape[0])
@@ -236,7 +245,7 @@ class Frontend:
             self.new_kf_frames.append(i)
             self.stats["keyframes"] += 1
             self.mode = Mode.TRACKING
-            if self._to_world(frame) is not None and self.viz:
+            if self._to_world(frame, len(self.keyframes) - 1) is not None and self.viz:
                 self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
             self._render(frame, frame, None)
             self.last_T_WC = frame.T_WC
@@ -252,7 +261,7 @@ class Frontend:
             if not try_reloc and should_append_gaussians(
                     add_new_kf, i, frame.T_WC, self.last_append_T_WC, self.last_append_idx,
                     self.min_translation, self.min_frame_gap):
-                if self._to_world(frame) is not None and self.viz:
+                if self._to_world(frame, len(self.keyframes)) is not None and self.viz:
                     self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
             if not try_reloc:
                 self._render(frame, self.keyframes.last_keyframe(), frame.T_WC)

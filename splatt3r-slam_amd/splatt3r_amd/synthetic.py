@@ -16,6 +16,7 @@ import torch
 
 C3_K = np.array([[776.0, 0.0, 480.0], [0.0, 776.0, 270.0], [0.0, 0.0, 1.0]], np.float32)
 C3_HW = (540, 960)
+C3_P = 4_194_304
 
 
 def quat_xyzw_to_rot(q: np.ndarray) -> np.ndarray:

@@ -42,7 +42,7 @@ def test_every_declared_symbol_has_a_ctypes_signature():
     import importlib
     for mod in ("splatt3r_amd.net", "splatt3r_amd.tracker", "diff_gaussian_rasterization",
                 "splatt3r_amd.render", "splatt3r_amd.splatt3r_utils", "mast3r_slam_backends",
-                "splatt3r_amd.retrieval_database"):
+                "splatt3r_amd.retrieval_database", "splatt3r_amd.gaussian_map"):
         try:
             importlib.import_module(mod)  # registers its signatures
         except ModuleNotFoundError:
@@ -73,7 +73,7 @@ def test_ctypes_signatures_match_header_arity():
     import importlib
     for mod in ("splatt3r_amd.net", "splatt3r_amd.tracker", "diff_gaussian_rasterization",
                 "splatt3r_amd.render", "splatt3r_amd.splatt3r_utils", "mast3r_slam_backends",
-                "splatt3r_amd.retrieval_database"):
+                "splatt3r_amd.retrieval_database", "splatt3r_amd.gaussian_map"):
         try:
             importlib.import_module(mod)
         except ModuleNotFoundError:

@@ -1,0 +1,136 @@
+"""World-space Gaussian map (SharedGaussians, frame.py:357-463) and the
+full-map render (visualization.py:467-600).
+
+Append: HIP (include/s3w.h s3w_map_append) vs the numpy restatement
+oracle/gaussians_ref.MapRef -- bit-exact (pure copies and selection).
+Full-map render: tests/golden/viz_render.npz holds the reference's own
+_render_gs_interactive driven on a synthetic map with a stub rasterizer
+(settings + inputs captured) and oracle.raster's image; our camera math,
+scale-invariant copies and HIP raster must reproduce them (settings 1e-6,
+inputs and image bit-exact).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle.gaussians_ref import MapRef
+
+
+def _batch(rng, n):
+    return (rng.normal(size=(n, 3)).astype(np.float32), rng.normal(size=(n, 6)).astype(np.float32),
+            rng.uniform(0, 1, (n, 3)).astype(np.float32), rng.uniform(0, 1, n).astype(np.float32))
+
+
+def test_oracle_map_eviction_and_truncation():
+    m = MapRef(10)
+    rng = np.random.default_rng(0)
+    a = _batch(rng, 8)
+    m.append(*a, kf_idx=0, thr=-1.0)
+    assert m.n == 8
+    b = _batch(rng, 5)
+    m.append(*b, kf_idx=1, thr=-1.0)         # space 2 -> truncated to 2, no eviction
+    assert m.n == 10 and list(m.kf) == [0] * 8 + [1] * 2
+    np.testing.assert_array_equal(m.means[8:10], b[0][:2])
+    c = _batch(rng, 3)
+    m.append(*c, kf_idx=2, thr=-1.0)         # full: newest half to the front, then append
+    assert m.n == 8
+    np.testing.assert_array_equal(m.means[:3], a[0][5:8])
+    np.testing.assert_array_equal(m.means[3:5], b[0][:2])
+    np.testing.assert_array_equal(m.means[5:8], c[0])
+    m.append(*_batch(rng, 4), kf_idx=3, thr=2.0)   # everything filtered: no-op
+    assert m.n == 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [1000, 1001])
+def test_hip_map_append_matches_oracle(cap):
+    from splatt3r_amd.gaussian_map import SharedGaussians
+    rng = np.random.default_rng(cap)
+    gm = SharedGaussians(max_gaussians=cap, device="cuda")
+    ref = MapRef(cap)
+    for step, n in enumerate([300, 0, 450, 700, 120, 999, 1, 640, 333, 0, 800]):
+        b = _batch(rng, n)
+        thr = 0.3 if step % 3 else 0.05
+        ref.append(*b, kf_idx=step, thr=thr)
+        if n:
+            gm.append(*(torch.from_numpy(x).cuda() for x in b), kf_idx=step,
+                      opacity_threshold=thr)
+        assert gm.n_gaussians == ref.n, step
+        k = ref.n
+        np.testing.assert_array_equal(gm.means[:k].cpu().numpy(), ref.means[:k])
+        np.testing.assert_array_equal(gm.cov_triu[:k].cpu().numpy(), ref.cov[:k])
+        np.testing.assert_array_equal(gm.colors[:k].cpu().numpy(), ref.colors[:k])
+        np.testing.assert_array_equal(gm.opacities[:k].cpu().numpy(), ref.opac[:k])
+        np.testing.assert_array_equal(gm.kf_id[:k].cpu().numpy(), ref.kf[:k])
+    gm.clear()
+    assert gm.get_all() is None
+
+
+@pytest.mark.gpu
+def test_hip_map_append_from_world_records_respects_device_count():
+    """append_records reads the valid row count from the device (the output
+    of s3w_gaussians_to_world): rows past it are ignored."""
+    from splatt3r_amd.gaussian_map import SharedGaussians
+    rng = np.random.default_rng(5)
+    rec = rng.uniform(0, 1, (500, 13)).astype(np.float32)
+    gm = SharedGaussians(max_gaussians=4096, device="cuda")
+    cnt = torch.tensor([321], dtype=torch.int64, device="cuda")
+    gm.append_records(torch.from_numpy(rec).cuda(), cnt, kf_idx=7, opacity_threshold=0.3)
+    ref = MapRef(4096)
+    r = rec[:321]
+    ref.append(r[:, :3], r[:, 3:9], r[:, 9:12], r[:, 12], 7, 0.3)
+    assert gm.n_gaussians == ref.n
+    np.testing.assert_array_equal(gm.means[:ref.n].cpu().numpy(), ref.means[:ref.n])
+    np.testing.assert_array_equal(gm.opacities[:ref.n].cpu().numpy(), ref.opac[:ref.n])
+
+
+def test_viz_camera_matches_reference_capture():
+    """Camera math of _render_gs_interactive (CPU): settings vs the capture."""
+    from splatt3r_amd.gaussian_map import gl_to_cv_T_WC, viz_camera
+    g = np.load(os.path.join(GOLDEN, "viz_render.npz"))
+    vw, vh = (int(v) for v in g["viewport"])
+    s = float(g["res_scale"])
+    rw, rh = max(64, int(vw * s)), max(64, int(vh * s))
+    assert (rh, rw) == (int(g["settings_image_height"]), int(g["settings_image_width"]))
+    tx, ty, view_t, proj, campos, sc, sc2 = viz_camera(gl_to_cv_T_WC(g["T_CW_gl"]), rw, rh,
+                                                      float(g["hfov"]) / 2.0)
+    assert abs(tx - float(g["settings_tanfovx"])) <= 1e-7
+    assert abs(ty - float(g["settings_tanfovy"])) <= 1e-7
+    np.testing.assert_allclose(view_t.numpy(), g["settings_viewmatrix"], atol=1e-6)
+    np.testing.assert_allclose(proj.numpy(), g["settings_projmatrix"], atol=1e-5)
+    np.testing.assert_allclose(campos.numpy(), g["settings_campos"], atol=1e-6)
+    np.testing.assert_array_equal(g["means"] * np.float32(sc), g["in_means3D"])
+
+
+@pytest.mark.gpu
+def test_hip_full_map_render_matches_reference_viz(parity):
+    """Bit-exact with the captured camera; with this host's own camera math
+    (torch CPU ops: tanfovy / matrices can differ in the last bit from the
+    capturing host) within 1e-6 mean-L1."""
+    from splatt3r_amd.gaussian_map import SharedGaussians, gl_to_cv_T_WC, render_map
+    g = np.load(os.path.join(GOLDEN, "viz_render.npz"))
+    n = g["means"].shape[0]
+    gm = SharedGaussians(max_gaussians=1 << 16, device="cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    gm.append(t(g["means"]), t(g["cov6"]), t(g["colors"]), t(g["opacities"]), kf_idx=0,
+              opacity_threshold=0.0)
+    assert gm.n_gaussians == n
+    vw, vh = (int(v) for v in g["viewport"])
+    s = float(g["res_scale"])
+    rw, rh = max(64, int(vw * s)), max(64, int(vh * s))
+    T = gl_to_cv_T_WC(g["T_CW_gl"])
+    cam = (float(g["settings_tanfovx"]), float(g["settings_tanfovy"]),
+           torch.from_numpy(g["settings_viewmatrix"]), torch.from_numpy(g["settings_projmatrix"]),
+           torch.from_numpy(g["settings_campos"]), 20.0, 400.0)
+    ours = render_map(gm, T, rw, rh, float(g["hfov"]) / 2.0, camera=cam).permute(1, 2, 0)
+    ours = ours.cpu().numpy()
+    d = np.abs(ours.astype(np.float64) - g["image_hwc"])
+    parity("viz_full_map_render_captured_camera", max_abs=d.max(), mean_l1=d.mean(), tol=0.0)
+    np.testing.assert_array_equal(ours, g["image_hwc"])
+    own = render_map(gm, T, rw, rh, float(g["hfov"]) / 2.0).permute(1, 2, 0).cpu().numpy()
+    d = np.abs(own.astype(np.float64) - g["image_hwc"])
+    parity("viz_full_map_render_own_camera", max_abs=d.max(), mean_l1=d.mean(), tol=1e-6)
+    assert d.mean() <= 1e-6

@@ -118,3 +118,48 @@ def test_calibrated_frontend_tracks():
         assert fe.stats["tracked"] >= 1 and 1 <= fe.tracker.last_iters <= 50
     finally:
         config["use_calib"] = old
+
+
+@pytest.mark.gpu
+def test_viz_frontend_appends_world_map_like_the_reference():
+    """viz on (enable_gs_viz, main.py:413-435 / 468-489): every appended
+    frame's world records (gaussians_to_world) enter the device map with
+    opacity > 0.3 and the keyframe index; the map matches the numpy
+    restatement fed the same records, and the full-map render runs."""
+    import numpy as np
+    from oracle.gaussians_ref import MapRef
+    from splatt3r_amd.gaussian_map import render_map
+    from splatt3r_amd.slam import Frontend
+    from splatt3r_amd.splatt3r_utils import _sim3_to_4x4, load_splatt3r, world_records
+    from splatt3r_amd.synthetic import tum_like_sequence
+    from splatt3r_amd.weights import FULL
+
+    dev = torch.device("cuda", 0)
+    model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
+    frames = tum_like_sequence(6, 384, 512, seed=3, step_px=2.0, device=dev)
+    fe = Frontend(model, device=dev, spatial_stride=4, render=False, viz=True,
+                  max_gaussians=20000)
+    # portable-PRNG opacities are ~0.12 (sigmoid(-2) bias): below the
+    # reference's 0.3, so this test appends with 0.1 to exercise the path
+    fe.map_opacity_threshold = 0.1
+    ref = MapRef(20000)
+    appended = 0
+    for i in range(6):
+        last = fe.last_append_idx
+        n_kf = len(fe.keyframes)
+        f = fe.step(i, frames[i])
+        if fe.last_append_idx == i and last != i:
+            appended += 1
+            kf_idx = n_kf if i > 0 else 0
+            T = _sim3_to_4x4(f.T_WC)[0].to(dev)
+            view = {k: v[0] for k, v in f.gaussian_pred.items()}
+            rec, cnt = world_records(view, f.img[0], T, 4, 0.05, 0.98, 1.0, 1.5)
+            r = rec[:int(cnt)].cpu().numpy()
+            ref.append(r[:, :3], r[:, 3:9], r[:, 9:12], r[:, 12], kf_idx, 0.1)
+    assert appended >= 2
+    gm = fe.gmap
+    assert gm.n_gaussians == ref.n > 0
+    np.testing.assert_array_equal(gm.means[:ref.n].cpu().numpy(), ref.means[:ref.n])
+    np.testing.assert_array_equal(gm.kf_id[:ref.n].cpu().numpy(), ref.kf[:ref.n])
+    img = render_map(gm, np.eye(4, dtype=np.float32), 256, 192, 60.0)
+    assert img.shape == (3, 192, 256) and torch.isfinite(img).all()
