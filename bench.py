@@ -16,7 +16,14 @@ shard (frame i depends on frame i-1), so with N GPUs each rank runs an
 independent replica on its own synthetic sequence: weak scaling, value =
 frames of all ranks / max-over-ranks wall time.  The keyframe-pair batch
 (the unit that does shard) is reported beside it by
-splatt3r_amd/pairs.py.
+splatt3r_amd/pairs.py through the sharded FactorGraph.add_factors path.
+
+Further legs on rank 0 (N = 1): `backend` -- the same frontend with the
+reference's backend running concurrently on a worker thread / HIP stream
+(base.yaml single_thread: False: retrieval + add_factors + GN per
+keyframe), reported as a second frames/s; `map_c5` -- the full-map render
+of an 8,388,608-Gaussian world map (C5) at 960x540; `raster_c3` (C3),
+`retrieval`, and the CPU baseline.
 
 Weights are portable-PRNG (no checkpoint offline) with the two decoder
 branches and the two heads tied (weights.tie_symmetric: same architecture,
@@ -50,13 +57,17 @@ PEAK_HBM_GBPS = 8000.0
 def _args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=120)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-frames", type=int, default=2,
                     help="frames of the CPU restatement timed for cpu_baseline (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the 4.19M-splat raster microbench")
     ap.add_argument("--no-pairs", action="store_true", help="skip the keyframe-pair batch leg")
+    ap.add_argument("--no-backend", action="store_true",
+                    help="skip the frontend + concurrent backend leg")
+    ap.add_argument("--backend-steps", type=int, default=60)
+    ap.add_argument("--no-map", action="store_true", help="skip the C5 full-map render leg")
     ap.add_argument("--pairs-per-rank", type=int, default=4)
     ap.add_argument("--no-kprof", action="store_true",
                     help="skip the per-launch network profile (roofline object)")
@@ -189,6 +200,94 @@ def _cpu_render(oracle, r1, r2, img, kimg, threads):
                   nthreads=threads)
 
 
+def bench_backend(model, dev, steps, rank):
+    """The frontend with the reference backend running concurrently
+    (single_thread: False, main.py:122-190): keyframe tasks (retrieval
+    update, add_factors over consecutive + retrieved keyframes, GN) on a
+    worker thread and its own HIP stream.  Timed from the first tracked
+    frame until the backend has drained the queue."""
+    from splatt3r_amd.backend import Backend
+    from splatt3r_amd.frame import Keyframes
+    from splatt3r_amd.slam import Frontend
+    from splatt3r_amd.synthetic import tum_like_sequence
+    frames = tum_like_sequence(steps + 4, H, W, seed=100 + rank, step_px=2.0, device=dev)
+    for b in range(1, 5):                   # backend pair plans, built before timing
+        model.encoder.pair_plan(b, H, W, tag="backend")
+    be = Backend(model, Keyframes(), device=dev)
+    be.start_worker()
+    fe = Frontend(model, device=dev, spatial_stride=4, render=True, backend=be)
+    nxt = lambda i: [frames[i + 1]]
+    try:
+        for i in range(3):
+            fe.step(i, frames[i], next_img=nxt(i))
+        be.wait()
+        torch.cuda.synchronize()
+        s0, b0 = dict(fe.stats), dict(be.stats)
+        t0 = time.perf_counter()
+        for i in range(3, 3 + steps):
+            fe.step(i, frames[i], next_img=nxt(i))
+        torch.cuda.synchronize()
+        t_front = time.perf_counter() - t0
+        be.wait()
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+    finally:
+        be.stop()
+    st = {k: fe.stats[k] - s0[k] for k in fe.stats}
+    bs = {k: be.stats[k] - b0.get(k, 0) for k in be.stats}
+    return {"frames_per_s": steps / t, "frames_per_s_frontend_only_window": steps / t_front,
+            "steps": steps, "keyframes": st["keyframes"],
+            "keyframe_rate": st["keyframes"] / steps, "backend_tasks": bs["optimized"],
+            "factor_graph_edges": be.stats["edges"],
+            "retrieval_candidates": bs["retrieval_candidates"],
+            "mode": "single_thread: False (worker thread + HIP stream, same GPU)"}
+
+
+def bench_map(dev, n=8_388_608, iters=5, warmup=2, seed=0):
+    """C5 full-map render: an n-Gaussian world map (SharedGaussians, filled
+    through s3w_map_append in 1M-record batches) rasterized with
+    colors_precomp at 960x540 (half of a 1920x1080 viewport), vfov 45,
+    near 0.05 / far 100 (visualization.py:467-600).  Synthetic Gaussians in
+    a 4 m x 2.5 m x 4 m room in front of the camera."""
+    from splatt3r_amd.gaussian_map import SharedGaussians, render_map
+    g = torch.Generator(device=dev).manual_seed(seed)
+    gm = SharedGaussians(max_gaussians=n, device=dev)
+    chunk = 1 << 20
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        u = lambda *sh: torch.rand(*sh, generator=g, device=dev)
+        means = (u(m, 3) - 0.5) * torch.tensor([4.0, 2.5, 4.0], device=dev) + \
+            torch.tensor([0.0, 0.0, 4.0], device=dev)
+        sc = torch.exp(torch.log(torch.tensor(0.004, device=dev)) + u(m, 3) * 2.0)
+        q = torch.nn.functional.normalize(torch.randn(m, 4, generator=g, device=dev), dim=1)
+        x, y, z, w = q.unbind(1)
+        R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+                         2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                         2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)],
+                        1).reshape(m, 3, 3)
+        cov = torch.einsum("nik,nk,njk->nij", R, sc * sc, R)
+        iu = torch.triu_indices(3, 3, device=dev)
+        gm.append(means, cov[:, iu[0], iu[1]], u(m, 3), 0.35 + 0.65 * u(m), kf_idx=s // chunk,
+                  opacity_threshold=0.3)
+    out = {"map_gaussians": gm.n_gaussians, "image": "960x540", "vfov_deg": 45.0}
+    T = np.eye(4, dtype=np.float32)
+    import diff_gaussian_rasterization as dgr
+    for label, cnt in (("4.19M", n // 2), ("8.39M", n)):
+        for _ in range(warmup):
+            render_map(gm, T, 960, 540, 45.0, n=cnt)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            render_map(gm, T, 960, 540, 45.0, n=cnt)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        out[label] = {"ms": ms, "msplats_per_s": cnt / (ms * 1e-3) / 1e6,
+                      "instances": int(dgr.last_num_rendered)}
+    return out
+
+
 def main():
     a = _args()
     ws, rank, local = _dist()
@@ -250,7 +349,9 @@ def main():
         "frame_breakdown": {"network_ms": net_ms,
                             "rest_ms": t_max / a.steps * 1e3 - net_ms,
                             "gn_iters_avg": st["gn_iters"] / max(1, st["tracked"]),
-                            "keyframes": st["keyframes"], "reloc": st["reloc"],
+                            "keyframes": st["keyframes"],
+                            "keyframe_rate": st["keyframes"] / max(1, a.steps),
+                            "reloc": st["reloc"],
                             "rendered": st["rendered"], "tracked": st["tracked"]},
     }
     if rank == 0 and not a.no_kprof:
@@ -279,8 +380,12 @@ def main():
     if not a.no_pairs:
         from splatt3r_amd.pairs import bench_pairs
         result["pairs"] = bench_pairs(model, frames, ws, rank, dev, a.pairs_per_rank)
+    if rank == 0 and ws == 1 and not a.no_backend:
+        result["backend"] = bench_backend(model, dev, a.backend_steps, rank)
+    if rank == 0 and not a.no_map:
+        result["map_c5"] = bench_map(dev)
     if rank == 0 and not a.no_c3:
-        from splatt3r_amd.bench_raster import run as raster_run
+        from tools.bench_raster import run as raster_run
         r = raster_run(4_194_304, iters=5, warmup=2, backward=True, device=dev)
         result["raster_c3"] = {k: r[k] for k in ("P", "fwd_ms", "msplats_per_s", "fwd_GBps",
                                                  "phases_ms", "bwd_ms", "bwd_GBps",

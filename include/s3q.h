@@ -11,9 +11,16 @@
  *   RetrievalDatabase.quantize_custom retrieval_database.py:95-104
  *     |q|^2 + |c|^2 - 2 q c^T, topk(k, largest=False)
  *
- * The ASMK inverted file (aggregate / search, third-party `asmk`, CPU) is
- * not part of this ABI.  All pointers are device pointers; calls are async
- * on `stream`.
+ *   ASMK inverted file (RetrievalDatabase.update / query / add_to_ivf_custom,
+ *   retrieval_database.py:43-134; the third-party `asmk` package, absent
+ *   here, restated from its published algorithm: Tolias et al., ICCV'13,
+ *   binary ASMK*, with Retriever's asmk_params, processor.py:84-89):
+ *     aggregate  per visual word: sum of residuals (x - c_w) over the
+ *                descriptors assigned to w, binarised to sign bits
+ *     search     score(image) = sum over shared words of
+ *                max(0, 1 - 2 hamming / D)^alpha   (alpha = 3, threshold 0)
+ *
+ * All pointers are device pointers; calls are async on `stream`.
  */
 #ifndef S3Q_H
 #define S3Q_H
@@ -51,6 +58,29 @@ int s3q_row_sqnorm(const float* x, int R, int D, float* out, void* stream);
 size_t s3q_l2_topk_workspace_bytes(int M, int C, int k);
 int s3q_l2_topk(const float* q, const float* c, const float* c_sqnorm, int M, int C, int D, int k,
                 int64_t* idx_out, float* dist_out, void* workspace, void* stream);
+
+/* ASMK aggregate_image, binary: feats [n, D] f32, words [n, k] i64 (the
+ * quantize_custom indices; a descriptor is in word w's set when any of its
+ * k assignments is w).  Unique words ascending -> out_words [n*k] i32
+ * (first *out_count valid), out_codes [n*k, D/32] u32 with bit (d % 32) of
+ * word d / 32 = (sum_x (x_d - c_wd) > 0), the sum of fp32 differences
+ * accumulated in fp64.  n * k <= 4096, D % 32 == 0, D <= 4096. */
+size_t s3q_asmk_aggregate_workspace_bytes(int n, int k);
+int s3q_asmk_aggregate(const float* feats, const int64_t* words, const float* centroids, int n,
+                       int k, int D, int32_t* out_words, uint32_t* out_codes, int32_t* out_count,
+                       void* workspace, void* stream);
+
+/* ASMK search over a flat inverted file of n_db entries (word, image, code):
+ * for every entry whose word is among the query's *q_count aggregated words,
+ * s = D - 2 hamming(code, q_code); when s / D >= sim_threshold, s^alpha is
+ * added to scores[image] (int64, exact and order-independent; the score is
+ * scores / D^alpha).  word_slot: [n_words] i32 scratch, all -1 on entry and
+ * on return.  alpha in 1..3, q_max bounds *q_count. */
+int s3q_asmk_search(const int32_t* q_words, const uint32_t* q_codes, const int32_t* q_count,
+                    int q_max, const int32_t* db_words, const int32_t* db_images,
+                    const uint32_t* db_codes, int64_t n_db, int D, int alpha,
+                    float sim_threshold, int32_t* word_slot, int n_words,
+                    unsigned long long* scores, void* stream);
 
 #ifdef __cplusplus
 }

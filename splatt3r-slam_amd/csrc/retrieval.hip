@@ -16,6 +16,8 @@
 //    keep the lower centroid index.
 #include <cfloat>
 
+#include <hipcub/hipcub.hpp>
+
 #include "common.hpp"
 #include "s3q.h"
 
@@ -386,6 +388,199 @@ extern "C" int s3q_l2_topk(const float* q, const float* c, const float* c_sqnorm
   k_l2_merge<<<(unsigned)s3::cdiv(M, kThreads / 64), kThreads, 0, st>>>(cand_d, cand_i, M,
                                                                         (int)nc, k, idx_out,
                                                                         dist_out);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+// ------------------------------------------------------------------ ASMK --
+// aggregate: one workgroup sorts the n*k (word, descriptor) pairs in LDS
+// (bitonic; keys word << 16 | descriptor are unique) and writes the
+// unique-word list + segment starts; then one workgroup per unique word sums
+// the residuals over its descriptors (fp64) and packs the sign bits with
+// wave ballots.  search: one lane per inverted-file entry, XOR + popcount
+// against the query code of the same word (found through a word -> slot
+// table), exact int64 score accumulation.
+namespace {
+
+constexpr int kAggMax = 4096;
+constexpr int kAggThreads = 1024;
+constexpr int kAggItems = kAggMax / kAggThreads;
+
+struct AggWs {
+  int32_t* seg_start;   // [m + 1]
+  int32_t* seg_desc;    // [m] descriptor index per sorted pair
+};
+
+AggWs carve_agg(void* base, int m, size_t* total = nullptr) {
+  char* p = static_cast<char*>(base);
+  char* p0 = p;
+  AggWs w;
+  w.seg_start = (int32_t*)p; p += align256(sizeof(int32_t) * (m + 1));
+  w.seg_desc = (int32_t*)p; p += align256(sizeof(int32_t) * m);
+  if (total) *total = (size_t)(p - p0);
+  return w;
+}
+
+__global__ void __launch_bounds__(kAggThreads)
+k_asmk_sort(const int64_t* __restrict__ words, int m, int k, int32_t* __restrict__ out_words,
+            int32_t* __restrict__ out_count, AggWs w) {
+  typedef hipcub::BlockScan<int, kAggThreads> Scan;
+  __shared__ uint64_t key[kAggMax];
+  __shared__ typename Scan::TempStorage scan_tmp;
+  int L = 1;
+  while (L < m) L <<= 1;
+  for (int i = threadIdx.x; i < L; i += kAggThreads)
+    key[i] = i < m ? ((uint64_t)words[i] << 16) | (uint64_t)(i / k) : ~0ull;
+  __syncthreads();
+  for (int size = 2; size <= L; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < L; i += kAggThreads) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const uint64_t a = key[i], b = key[j];
+          if ((a > b) == up) { key[i] = b; key[j] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // segment heads -> unique index by a block exclusive scan (blocked items)
+  int hd[kAggItems];
+  const int base = threadIdx.x * kAggItems;
+#pragma unroll
+  for (int t = 0; t < kAggItems; ++t) {
+    const int i = base + t;
+    hd[t] = (i < m && (i == 0 || (key[i] >> 16) != (key[i - 1] >> 16))) ? 1 : 0;
+  }
+  int total = 0;
+  Scan(scan_tmp).ExclusiveSum(hd, hd, total);
+#pragma unroll
+  for (int t = 0; t < kAggItems; ++t) {
+    const int i = base + t;
+    if (i >= m) break;
+    w.seg_desc[i] = (int32_t)(key[i] & 0xFFFF);
+    const bool head = i == 0 || (key[i] >> 16) != (key[i - 1] >> 16);
+    if (head) {
+      out_words[hd[t]] = (int32_t)(key[i] >> 16);
+      w.seg_start[hd[t]] = i;
+    }
+  }
+  if (threadIdx.x == 0) {
+    w.seg_start[total] = m;
+    *out_count = total;
+  }
+}
+
+// one workgroup (256 lanes) per unique word; lanes stride the D dimensions
+__global__ void __launch_bounds__(kThreads)
+k_asmk_codes(const float* __restrict__ feats, const float* __restrict__ cen, int D,
+             const int32_t* __restrict__ uwords, const int32_t* __restrict__ count, AggWs w,
+             uint32_t* __restrict__ codes) {
+  const int u = blockIdx.x;
+  if (u >= *count) return;
+  const int word = uwords[u];
+  const int s0 = w.seg_start[u], s1 = w.seg_start[u + 1];
+  const float* c = cen + (int64_t)word * D;
+  const int lane = threadIdx.x & 63;
+  for (int d0 = 0; d0 < D; d0 += kThreads) {
+    const int d = d0 + threadIdx.x;
+    double acc = 0.0;
+    if (d < D) {
+      const float cd = c[d];
+      for (int s = s0; s < s1; ++s) acc += (double)(feats[(int64_t)w.seg_desc[s] * D + d] - cd);
+    }
+    const uint64_t bits = __ballot(d < D && acc > 0.0);
+    if (lane == 0 && d < D) {
+      uint32_t* o = codes + (int64_t)u * (D / 32) + d / 32;
+      o[0] = (uint32_t)bits;
+      if (d + 32 < D) o[1] = (uint32_t)(bits >> 32);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_slot_set(const int32_t* __restrict__ qw, const int32_t* __restrict__ q_count, int q_max,
+           int32_t* __restrict__ slot, int set) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= q_max || i >= *q_count) return;
+  slot[qw[i]] = set ? i : -1;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_asmk_search(const uint32_t* __restrict__ q_codes, const int32_t* __restrict__ db_words,
+              const int32_t* __restrict__ db_images, const uint32_t* __restrict__ db_codes,
+              int64_t n_db, int D, int alpha, int s_min, const int32_t* __restrict__ slot,
+              unsigned long long* __restrict__ scores) {
+  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (e >= n_db) return;
+  const int q = slot[db_words[e]];
+  if (q < 0) return;
+  const int nw = D / 32;
+  const uint32_t* a = db_codes + e * nw;
+  const uint32_t* b = q_codes + (int64_t)q * nw;
+  int ham = 0;
+  for (int i = 0; i < nw; ++i) ham += __popc(a[i] ^ b[i]);
+  const int s = D - 2 * ham;
+  if (s < s_min) return;
+  long long v = s;
+  if (alpha >= 2) v *= s;
+  if (alpha >= 3) v *= s;
+  atomicAdd(&scores[db_images[e]], (unsigned long long)v);
+}
+
+}  // namespace
+
+extern "C" size_t s3q_asmk_aggregate_workspace_bytes(int n, int k) {
+  size_t t = 0;
+  carve_agg(nullptr, n * k > 0 ? n * k : 1, &t);
+  return t;
+}
+
+extern "C" int s3q_asmk_aggregate(const float* feats, const int64_t* words, const float* centroids,
+                                  int n, int k, int D, int32_t* out_words, uint32_t* out_codes,
+                                  int32_t* out_count, void* workspace, void* stream) {
+  S3_REQUIRE(n >= 0 && k >= 1 && n * k <= kAggMax && n < 65536,
+             "s3q_asmk_aggregate: n*k=%d exceeds %d", n * k, kAggMax);
+  S3_REQUIRE(D > 0 && D % 32 == 0 && D <= 4096, "s3q_asmk_aggregate: D=%d (multiple of 32)", D);
+  hipStream_t st = s3::as_stream(stream);
+  if (n == 0) {
+    S3_HIP(hipMemsetAsync(out_count, 0, sizeof(int32_t), st));
+    return S3_OK;
+  }
+  S3_REQUIRE(feats && words && centroids && out_words && out_codes && out_count && workspace,
+             "s3q_asmk_aggregate: null argument");
+  const int m = n * k;
+  AggWs w = carve_agg(workspace, m);
+  k_asmk_sort<<<1, kAggThreads, 0, st>>>(words, m, k, out_words, out_count, w);
+  S3_LAUNCH_CHECK();
+  k_asmk_codes<<<m, kThreads, 0, st>>>(feats, centroids, D, out_words, out_count, w, out_codes);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+extern "C" int s3q_asmk_search(const int32_t* q_words, const uint32_t* q_codes,
+                               const int32_t* q_count, int q_max, const int32_t* db_words,
+                               const int32_t* db_images, const uint32_t* db_codes, int64_t n_db,
+                               int D, int alpha, float sim_threshold, int32_t* word_slot,
+                               int n_words, unsigned long long* scores, void* stream) {
+  S3_REQUIRE(alpha >= 1 && alpha <= 3, "s3q_asmk_search: alpha=%d (1..3)", alpha);
+  S3_REQUIRE(D > 0 && D % 32 == 0, "s3q_asmk_search: D=%d", D);
+  S3_REQUIRE(q_max >= 0 && n_db >= 0 && n_words > 0, "s3q_asmk_search: bad sizes");
+  if (q_max == 0 || n_db == 0) return S3_OK;
+  S3_REQUIRE(q_words && q_codes && q_count && db_words && db_images && db_codes && word_slot &&
+                 scores,
+             "s3q_asmk_search: null argument");
+  hipStream_t st = s3::as_stream(stream);
+  // s / D >= threshold  <=>  s >= ceil(threshold * D)
+  const int s_min = (int)ceil((double)sim_threshold * D);
+  const int qb = (int)s3::cdiv(q_max, kThreads);
+  k_slot_set<<<qb, kThreads, 0, st>>>(q_words, q_count, q_max, word_slot, 1);
+  S3_LAUNCH_CHECK();
+  k_asmk_search<<<(unsigned)s3::cdiv(n_db, kThreads), kThreads, 0, st>>>(
+      q_codes, db_words, db_images, db_codes, n_db, D, alpha, s_min, word_slot, scores);
+  S3_LAUNCH_CHECK();
+  k_slot_set<<<qb, kThreads, 0, st>>>(q_words, q_count, q_max, word_slot, 0);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

@@ -1,0 +1,161 @@
+"""The SLAM backend's task bodies (main.py:76-190), in-process.
+
+  Backend.global_optimization(idx)  run_backend's loop body (main.py:142-190):
+      consecutive keyframe + retrieval candidates (RetrievalDatabase.update,
+      k = 3, min_thresh 5e-3) -> FactorGraph.add_factors -> solve_GN_rays /
+      solve_GN_calib
+  Backend.relocalization(frame)     relocalization (main.py:76-119): retrieval
+      query without adding -> tentative keyframe -> strict add_factors ->
+      on success add to the database, copy the pose of the best match and
+      solve; on failure pop the keyframe
+
+The reference runs these in a second process sharing the GPU
+(config base.yaml single_thread: False) and polls a task queue.  Here the
+frontend calls them directly (single_thread) or hands keyframe tasks to a
+worker thread that issues them on its own HIP stream (`start_worker`), so
+backend kernels run concurrently with the tracker's on the same device.
+With a pairs.PairShard over W ranks, keyframe features are broadcast at
+keyframe creation and add_factors' pair batches run across the ranks.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+
+import torch
+
+import lietorch
+from splatt3r_amd.config import config
+from splatt3r_amd.global_opt import FactorGraph
+
+
+class Backend:
+    def __init__(self, model, keyframes, K=None, device="cuda", retrieval=None, shard=None):
+        from splatt3r_amd.retrieval_database import (RetrievalDatabase,
+                                                     synthetic_retrieval_weights)
+        self.model = model
+        self.keyframes = keyframes
+        self.device = torch.device(device)
+        self.shard = shard
+        self.factor_graph = FactorGraph(model, keyframes, K, device, shard=shard)
+        # the retrieval checkpoint is not available offline: synthetic
+        # weights of its shapes unless a database is passed in
+        self.retrieval = retrieval if retrieval is not None else RetrievalDatabase(
+            synthetic_retrieval_weights(self.device), self.device)
+        self.stats = dict(optimized=0, edges=0, reloc_attempts=0, reloc_success=0,
+                          retrieval_candidates=0)
+        self._q = None
+        self._thread = None
+        self._stream = None
+        self._err = None
+
+    # ------------------------------------------------------ keyframes ----
+    def on_keyframe(self, idx: int, frame):
+        """A keyframe was appended on the frontend: broadcast its features to
+        the pair-shard ranks (the reference shares them through
+        SharedKeyframes' shared memory)."""
+        if self.shard is not None and self.shard.ws > 1:
+            self.shard.broadcast_keyframe(idx, frame)
+
+    def _solve(self):
+        if config["use_calib"]:
+            return self.factor_graph.solve_GN_calib()
+        return self.factor_graph.solve_GN_rays()
+
+    def global_optimization(self, idx: int):
+        """main.py:142-190 for the queued keyframe idx."""
+        kf_idx = [idx - 1 - j for j in range(min(1, idx))]
+        frame = self.keyframes[idx]
+        retrieval_inds = self.retrieval.update(frame, add_after_query=True,
+                                               k=config["retrieval"]["k"],
+                                               min_thresh=config["retrieval"]["min_thresh"])
+        self.stats["retrieval_candidates"] += len(retrieval_inds)
+        kf_idx += retrieval_inds
+        kf_idx = set(kf_idx)
+        kf_idx.discard(idx)
+        kf_idx = list(kf_idx)
+        frame_idx = [idx] * len(kf_idx)
+        if kf_idx:
+            self.factor_graph.add_factors(kf_idx, frame_idx, config["local_opt"]["min_match_frac"])
+        self.stats["edges"] = int(self.factor_graph.ii.numel())
+        self._solve()
+        self.stats["optimized"] += 1
+
+    def relocalization(self, frame) -> bool:
+        """main.py:76-119."""
+        self.stats["reloc_attempts"] += 1
+        kf_idx = list(self.retrieval.update(frame, add_after_query=False,
+                                            k=config["retrieval"]["k"],
+                                            min_thresh=config["retrieval"]["min_thresh"]))
+        success = False
+        if kf_idx:
+            self.keyframes.append(frame)
+            n_kf = len(self.keyframes)
+            self.on_keyframe(n_kf - 1, frame)
+            frame_idx = [n_kf - 1] * len(kf_idx)
+            if self.factor_graph.add_factors(frame_idx, kf_idx, config["reloc"]["min_match_frac"],
+                                             is_reloc=config["reloc"]["strict"]):
+                self.retrieval.update(frame, add_after_query=True, k=config["retrieval"]["k"],
+                                      min_thresh=config["retrieval"]["min_thresh"])
+                success = True
+                self.keyframes[n_kf - 1].T_WC = lietorch.Sim3(
+                    self.keyframes[kf_idx[0]].T_WC.data.clone())
+            else:
+                self.keyframes.pop_last()
+        if success:
+            self.stats["reloc_success"] += 1
+            self._solve()
+        return success
+
+    # --------------------------------------------------------- worker ----
+    def start_worker(self):
+        """single_thread: False -- keyframe tasks run on a worker thread and
+        its own HIP stream, concurrently with the frontend."""
+        self._q = queue.Queue()
+        self._stream = torch.cuda.Stream(device=self.device)
+        self._thread = threading.Thread(target=self._loop, daemon=True)
+        self._thread.start()
+
+    def _loop(self):
+        torch.cuda.set_device(self.device)
+        while True:
+            item = self._q.get()
+            if item is None:
+                self._q.task_done()
+                return
+            idx, ready = item
+            try:
+                with torch.cuda.stream(self._stream), torch.inference_mode():
+                    self._stream.wait_event(ready)
+                    self.global_optimization(idx)
+            except Exception as e:   # surfaced by wait()/stop()
+                self._err = e
+            self._q.task_done()
+
+    def queue_global_optimization(self, idx: int):
+        """states.queue_global_optimization (main.py:409, 526): run now
+        (single thread) or hand to the worker."""
+        if self._q is None:
+            self.global_optimization(idx)
+            return
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.device))
+        self._q.put((idx, ready))
+
+    def wait(self):
+        if self._q is not None:
+            self._q.join()
+            torch.cuda.current_stream(self.device).wait_stream(self._stream)
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise e
+
+    def stop(self):
+        if self._q is not None:
+            self._q.put(None)
+            self._q.join()
+            self._thread.join()
+            self._q = None
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise e

@@ -8,6 +8,11 @@ Same attribute names, edge bookkeeping and acceptance rule as the
 reference; solve_GN_calib (config use_calib) runs the calibrated device
 solve (mast3r_slam_backends.gauss_newton_calib) on points constrained to
 their pixel rays.
+
+Multi-GPU: with a `shard` (pairs.PairShard over W > 1
+ranks) add_factors sends the pair list to every rank, pair p is decoded and
+matched on rank p mod W, and rank 0 receives idx / valid / Q for all pairs
+in order; edges and the GN solve are then exactly the single-rank ones.
 """
 from __future__ import annotations
 
@@ -16,12 +21,16 @@ import torch
 import lietorch
 import mast3r_slam_backends
 from splatt3r_amd.config import config
+from splatt3r_amd.pairs import q_weighted
 from splatt3r_amd.splatt3r_utils import splatt3r_match_symmetric
 
 
 class FactorGraph:
-    def __init__(self, model, frames, K=None, device="cuda"):
+    def __init__(self, model, frames, K=None, device="cuda", shard=None, match_fn=None):
         self.model = model
+        self.shard = shard
+        # splatt3r_match_symmetric(model, ...) unless injected (protocol tests)
+        self.match_fn = match_fn or (lambda *a: splatt3r_match_symmetric(model, *a))
         self.frames = frames
         self.device = device
         self.cfg = config["local_opt"]
@@ -35,20 +44,21 @@ class FactorGraph:
 
     def add_factors(self, ii, jj, min_match_frac, is_reloc=False):
         """global_opt.py:30-99."""
-        kf_ii = [self.frames[i] for i in ii]
-        kf_jj = [self.frames[j] for j in jj]
-        feat_i = torch.cat([k.feat for k in kf_ii])
-        feat_j = torch.cat([k.feat for k in kf_jj])
-        pos_i = torch.cat([k.pos for k in kf_ii])
-        pos_j = torch.cat([k.pos for k in kf_jj])
-        shape_i = [k.img_true_shape for k in kf_ii]
-        shape_j = [k.img_true_shape for k in kf_jj]
-        (idx_i2j, idx_j2i, valid_match_j, valid_match_i, Qii, Qjj, Qji, Qij) = \
-            splatt3r_match_symmetric(self.model, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j)
-        b = torch.arange(idx_i2j.shape[0], device=idx_i2j.device)[:, None].repeat(
-            1, idx_i2j.shape[1])
-        Qj = torch.sqrt(Qii[b, idx_i2j] * Qji)
-        Qi = torch.sqrt(Qjj[b, idx_j2i] * Qij)
+        if self.shard is not None and self.shard.ws > 1:
+            idx_i2j, idx_j2i, valid_match_j, valid_match_i, Qj, Qi = \
+                self.shard.match_pairs(ii, jj)
+        else:
+            kf_ii = [self.frames[i] for i in ii]
+            kf_jj = [self.frames[j] for j in jj]
+            feat_i = torch.cat([k.feat for k in kf_ii])
+            feat_j = torch.cat([k.feat for k in kf_jj])
+            pos_i = torch.cat([k.pos for k in kf_ii])
+            pos_j = torch.cat([k.pos for k in kf_jj])
+            shape_i = [k.img_true_shape for k in kf_ii]
+            shape_j = [k.img_true_shape for k in kf_jj]
+            m = self.match_fn(feat_i, pos_i, feat_j, pos_j, shape_i, shape_j)
+            idx_i2j, idx_j2i, valid_match_j, valid_match_i, Qj, Qi = q_weighted(
+                m, self.cfg["Q_conf"])
         valid_j = valid_match_j & (Qj > self.cfg["Q_conf"])
         valid_i = valid_match_i & (Qi > self.cfg["Q_conf"])
         match_frac_j = valid_j.sum(dim=(1, 2)) / (valid_j.shape[1] * valid_j.shape[2])

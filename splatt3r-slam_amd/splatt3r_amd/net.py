@@ -524,8 +524,10 @@ class Splatt3RNet:
             self._enc[key] = ep
         return self._enc[key]
 
-    def pair_plan(self, Bp, H, W, keep_tokens=False) -> PairPlan:
-        key = (Bp, H, W, keep_tokens)
+    def pair_plan(self, Bp, H, W, keep_tokens=False, tag=None) -> PairPlan:
+        """`tag` separates plan buffers of concurrent users of one network
+        (the frontend tracker and the backend worker thread)."""
+        key = (Bp, H, W, keep_tokens, tag)
         if key not in self._pair:
             with torch.inference_mode(False):
                 pp = PairPlan(self, Bp, H, W, keep_tokens)
@@ -545,13 +547,13 @@ class Splatt3RNet:
         feat, pos = self._timed("encoder", ep, image.to(device=self.device, dtype=F32))
         return feat.clone(), pos.clone(), None
 
-    def infer_pair(self, feat1, pos1, feat2, pos2, hw):
+    def infer_pair(self, feat1, pos1, feat2, pos2, hw, tag=None):
         """Fused decoder + both heads for Bp pairs: returns (res1, res2)
         dicts of [Bp, H, W, ...] tensors (views into static buffers: copy
         before the next call if they must persist) and the plan."""
         Bp, N, E = feat1.shape
         H, W = hw
-        pp = self.pair_plan(Bp, H, W)
+        pp = self.pair_plan(Bp, H, W, tag=tag)
         self._load_pair_inputs(pp, feat1, pos1, feat2, pos2)
         self._timed("pair", pp.run)
         return pp.res[0], pp.res[1], pp

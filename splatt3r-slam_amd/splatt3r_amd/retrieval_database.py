@@ -9,9 +9,15 @@ come from the MASt3R retrieval checkpoint (`Retriever`, mast3r/retrieval/
 processor.py:62-96: prewhiten / projector / postwhiten, nfeat, and the ASMK
 codebook centroids); `RetrievalWeights` holds them as device tensors.
 
-The ASMK inverted file (`asmk` package: aggregate_image, ivf.search; CPU)
-is third-party and absent here, so `update` / `query` / `add_to_database`
-raise NotImplementedError; the GEMM + top-k that feeds them is here.
+The ASMK inverted file (the third-party `asmk` package the reference drives
+through `update` / `query` / `add_to_ivf_custom`, :43-134; absent here and
+unpinned) is restated from its published algorithm (binary ASMK*, Tolias et
+al. ICCV'13) with Retriever's asmk_params (processor.py:84-89) as two HIP
+passes (include/s3q.h): `s3q_asmk_aggregate` (per visual word, sign bits of
+the summed residuals) and `s3q_asmk_search` (a flat device-resident inverted
+file scanned with XOR + popcount, exact int64 scores).  The database lives
+on the device and grows geometrically; one host read of the per-image
+scores per query (the reference's torch.topk on the CPU).
 """
 from __future__ import annotations
 
@@ -33,11 +39,21 @@ _lib.register({
     "s3q_l2_topk_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int] * 3),
     "s3q_l2_topk": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 +
                     [ctypes.c_void_p] * 4),
+    "s3q_asmk_aggregate_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
+    "s3q_asmk_aggregate": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 +
+                           [ctypes.c_void_p] * 5),
+    "s3q_asmk_search": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int] +
+                        [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_float, ctypes.c_void_p, ctypes.c_int,
+                                                 ctypes.c_void_p, ctypes.c_void_p]),
 })
 
 # asmk_params of Retriever (processor.py:84-89)
-ASMK_PARAMS = {"build_ivf": {"quantize": {"multiple_assignment": 1}},
-               "query_ivf": {"quantize": {"multiple_assignment": 5}}}
+ASMK_PARAMS = {"build_ivf": {"kernel": {"binary": True}, "ivf": {"use_idf": False},
+                             "quantize": {"multiple_assignment": 1}, "aggregate": {}},
+               "query_ivf": {"quantize": {"multiple_assignment": 5}, "aggregate": {},
+                             "search": {"topk": None},
+                             "similarity": {"similarity_threshold": 0.0, "alpha": 3.0}}}
 
 
 @dataclasses.dataclass
@@ -126,8 +142,67 @@ def l2_topk(q, centroids, c_sqnorm, k):
     return idx, dist
 
 
+def asmk_aggregate(feats, words, centroids):
+    """aggregate_image (binary): feats [n, D] f32, words [n, k] i64 ->
+    (unique words [u] i32, codes [u, D/32] u32, device count [1] i32); the
+    arrays are sized n*k, the first `count` rows valid."""
+    feats = _chk(feats, torch.float32, "asmk_aggregate")
+    words = words.to(torch.int64).contiguous()
+    n, D = feats.shape
+    k = words.shape[1]
+    dev = feats.device
+    out_w = torch.empty(n * k, dtype=torch.int32, device=dev)
+    out_c = torch.empty(n * k, D // 32, dtype=torch.int32, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    ws = torch.empty(int(_lib.lib().s3q_asmk_aggregate_workspace_bytes(n, k)), dtype=torch.uint8,
+                     device=dev)
+    _lib.call("s3q_asmk_aggregate", feats.data_ptr(), words.data_ptr(), centroids.data_ptr(), n, k,
+              D, out_w.data_ptr(), out_c.data_ptr(), cnt.data_ptr(), ws.data_ptr(),
+              _lib.stream(dev))
+    return out_w, out_c, cnt
+
+
+class InvertedFile:
+    """Flat device inverted file: one (word, image, code) entry per
+    aggregated word of every database image (asmk ivf.add)."""
+
+    def __init__(self, n_words: int, D: int, device):
+        self.n_words, self.D, self.device = n_words, D, device
+        self.n = 0
+        self.n_images = 0
+        self.words = torch.empty(0, dtype=torch.int32, device=device)
+        self.images = torch.empty(0, dtype=torch.int32, device=device)
+        self.codes = torch.empty(0, D // 32, dtype=torch.int32, device=device)
+        self.slot = torch.full((n_words,), -1, dtype=torch.int32, device=device)
+
+    def add(self, words, codes, count: int, image: int):
+        need = self.n + count
+        if need > self.words.shape[0]:
+            cap = max(need, 2 * self.words.shape[0], 4096)
+            grow = lambda t, *s: torch.cat([t[:self.n], torch.empty(cap - self.n, *s, dtype=t.dtype,
+                                                                     device=self.device)])
+            self.words = grow(self.words)
+            self.images = grow(self.images)
+            self.codes = grow(self.codes, self.D // 32)
+        self.words[self.n:need] = words[:count]
+        self.images[self.n:need] = image
+        self.codes[self.n:need] = codes[:count]
+        self.n = need
+        self.n_images = max(self.n_images, image + 1)
+
+    def search(self, q_words, q_codes, q_count, alpha=3, threshold=0.0):
+        """-> float64 host scores [n_images] (exact: sum of s^alpha / D^alpha)."""
+        sc = torch.zeros(max(1, self.n_images), dtype=torch.int64, device=self.device)
+        _lib.call("s3q_asmk_search", q_words.data_ptr(), q_codes.data_ptr(), q_count.data_ptr(),
+                  q_words.shape[0], self.words.data_ptr(), self.images.data_ptr(),
+                  self.codes.data_ptr(), self.n, self.D, int(alpha), float(threshold),
+                  self.slot.data_ptr(), self.n_words, sc.data_ptr(), _lib.stream(self.device))
+        return sc[:self.n_images].cpu().double() / float(self.D) ** alpha
+
+
 class RetrievalDatabase:
-    """retrieval_database.py:9-22 minus the ASMK IVF builder."""
+    """retrieval_database.py:9-134: prep_features / quantize_custom on the
+    device kernels above, the ASMK inverted file restated on the device."""
 
     def __init__(self, weights: RetrievalWeights, device="cuda"):
         self.w = weights
@@ -137,6 +212,10 @@ class RetrievalDatabase:
         self.query_device = device
         self.centroids = weights.centroids.to(device=device, dtype=torch.float32).contiguous()
         self._c_sq = row_sqnorm(self.centroids)
+        self.ivf = InvertedFile(self.centroids.shape[0], self.centroids.shape[1], device)
+        prm = ASMK_PARAMS["query_ivf"]["similarity"]
+        self.alpha = int(prm["alpha"])
+        self.sim_threshold = float(prm["similarity_threshold"])
 
     def prep_features(self, backbone_feat):
         """retrieval_database.py:24-41 -> topk_features [B, nfeat, dim]."""
@@ -156,8 +235,51 @@ class RetrievalDatabase:
         return idx
 
     def update(self, frame, add_after_query, k, min_thresh=0.0):
-        raise NotImplementedError("RetrievalDatabase.update needs the ASMK inverted file "
-                                  "(third-party `asmk`, CPU), which is not available")
+        """retrieval_database.py:43-72: query (if the database is not empty)
+        -> keyframe indices of the top-k scores above min_thresh; then add
+        the frame when add_after_query."""
+        feat = self.prep_features(frame.feat)[0]   # one frame at a time
+        topk_inds = []
+        topk_codes = None
+        if self.kf_counter > 0:
+            scores, topk_codes = self.query(feat)
+            top = torch.topk(scores.float(), min(k, self.ivf.n_images))
+            topk_inds = top.indices[top.values > min_thresh].tolist()
+        if add_after_query:
+            self.add_to_database(feat, topk_codes)
+        return topk_inds
+
+    def query(self, feat):
+        """retrieval_database.py:74-87 + accumulate_scores (:106-134):
+        quantise (5 words), aggregate, search -> (scores [n_images] f64 host,
+        topk_codes [n, 5] device)."""
+        codes = self.quantize_custom(feat, ASMK_PARAMS["query_ivf"])
+        qw, qc, qn = asmk_aggregate(feat, codes, self.centroids)
+        return self.ivf.search(qw, qc, qn, self.alpha, self.sim_threshold), codes
+
+    def add_to_database(self, feat, topk_codes=None):
+        """add_to_ivf_custom (:136-166) + bookkeeping (:89-93): reuse the
+        query's first assignment when present (build multiple_assignment 1)."""
+        k1 = ASMK_PARAMS["build_ivf"]["quantize"]["multiple_assignment"]
+        codes = (self.quantize_custom(feat, ASMK_PARAMS["build_ivf"]) if topk_codes is None
+                 else topk_codes[:, :k1].contiguous())
+        w, c, n = asmk_aggregate(feat, codes, self.centroids)
+        self.ivf.add(w, c, int(n.item()), self.kf_counter)
+        self.kf_ids.append(self.kf_counter)
+        self.kf_counter += 1
+
+
+def synthetic_retrieval_weights(device, dim=1024, n_clusters=65536, nfeat=300, seed=0):
+    """Weights of the retrieval checkpoint's shapes (the checkpoint and its
+    ASMK codebook are not available offline): portable generator, unit
+    centroids."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    W = (torch.randn(dim, 1024, generator=g) / 32.0).to(device)
+    b = torch.zeros(dim, device=device)
+    cen = torch.nn.functional.normalize(torch.randn(n_clusters, dim, generator=g), dim=1).to(device)
+    P = (torch.randn(1024, 1024, generator=g, dtype=torch.float64) / 32.0).to(device)
+    m = torch.zeros(1, 1024, dtype=torch.float64, device=device)
+    return RetrievalWeights(W, b, cen, (m, P), (m, P), nfeat=nfeat)
 
 
 def bench(device, iters=20, C=65536, dim=1024, nfeat=300, k=5):

@@ -1,8 +1,10 @@
 """The frontend of the SLAM loop: main.py:395-535 (one call of `step` = one
-frame of the reference's `while True` body) without the viz/backend
-processes, which are out of scope (the tracker path is a
-replica per GPU; the pair batches of the backend shard across GPUs in
-splatt3r_amd/pairs.py).
+frame of the reference's `while True` body).  The backend (main.py:76-190)
+is optional (`backend=backend.Backend(...)`): keyframe tasks run inline or
+on a worker thread/stream, RELOC frames go through its retrieval-based
+relocalization; its pair batches shard across GPUs (splatt3r_amd/pairs.py).
+With `viz=True` the world map the viz process renders is kept on the device
+(gaussian_map.SharedGaussians); the GUI itself is out of scope.
 
 Per tracked frame this runs, as the reference does with --no-viz and
 rendering on (the default):
@@ -45,7 +47,7 @@ class Frontend:
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
                  readback=True, enc_batch=1, main_priority=None, late_prefetch=False,
-                 viz=False, max_gaussians=4 * 1024 * 1024):
+                 viz=False, max_gaussians=4 * 1024 * 1024, backend=None):
         self.model = model
         # viz: the reference's enable_gs_viz (main.py:357, `not --no-viz`).
         # Only then does it record the last append (main.py:434-435,488-489);
@@ -65,6 +67,12 @@ class Frontend:
                 raise ValueError("use_calib needs the camera intrinsics K (main.py:310-318)")
             self.keyframes.set_intrinsics(K)   # main.py:314-318
         self.tracker = FrameTracker(model, self.keyframes, device)
+        # backend.Backend (main.py:76-190) or None (frontend only, as the
+        # headline bench); its factor graph shares this keyframe list
+        self.backend = backend
+        if backend is not None:
+            backend.keyframes = self.keyframes
+            backend.factor_graph.frames = self.keyframes
         self.mode = Mode.INIT
         self.render = render
         self.readback = readback
@@ -183,6 +191,13 @@ class Frontend:
             self.stats["gaussians_world"] += int(gs[0].shape[0])
         return gs
 
+    def _kf_added(self, frame):
+        """states.queue_global_optimization (main.py:409, 525-526)."""
+        if self.backend is not None:
+            idx = len(self.keyframes) - 1
+            self.backend.on_keyframe(idx, frame)
+            self.backend.queue_global_optimization(idx)
+
     def _event(self):
         if self.spans is None:
             return None
@@ -244,6 +259,7 @@ class Frontend:
             self.keyframes.append(frame)
             self.new_kf_frames.append(i)
             self.stats["keyframes"] += 1
+            self._kf_added(frame)
             self.mode = Mode.TRACKING
             if self._to_world(frame, len(self.keyframes) - 1) is not None and self.viz:
                 self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
@@ -266,18 +282,26 @@ class Frontend:
             if not try_reloc:
                 self._render(frame, self.keyframes.last_keyframe(), frame.T_WC)
         elif self.mode == Mode.RELOC:
-            # Relocalisation against the retrieval database runs in the
-            # backend (main.py:76-127), which is out of scope; the frame is
-            # re-initialised as a keyframe at the last pose instead.
+            # main.py:508-517 + relocalization (main.py:76-119): with a
+            # backend the frame is matched against the retrieval database and
+            # becomes a keyframe only if strict add_factors accepts it;
+            # without one the frontend stays in RELOC (no keyframe is made
+            # from an unverified pose)
             X, C = splatt3r_inference_mono(self.model, frame)
             frame.update_pointmap(X, C)
             self.stats["reloc"] += 1
-            add_new_kf = True
-            self.mode = Mode.TRACKING
+            if self.backend is not None:
+                self.backend.wait()
+                if self.backend.relocalization(frame):
+                    self.stats["keyframes"] += 1
+                    self.new_kf_frames.append(i)
+                    self.tracker.reset_idx_f2k()
+                    self.mode = Mode.TRACKING
         if add_new_kf:
             self.keyframes.append(frame)
             self.new_kf_frames.append(i)
             self.stats["keyframes"] += 1
             self.tracker.reset_idx_f2k()
+            self._kf_added(frame)
         self.last_T_WC = frame.T_WC
         return frame

@@ -164,17 +164,20 @@ def splatt3r_match_asymmetric(model, frame_i, frame_j, idx_i2j_init=None):
 
 
 @torch.inference_mode()
-def splatt3r_decode_symmetric_batch(model, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
+def splatt3r_decode_symmetric_batch(model, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j,
+                                    tag="backend"):
     """splatt3r_utils.py:466-499, batched: one fused pair plan over the b
-    pairs in each order (the reference loops pairs one at a time)."""
+    pairs in each order (the reference loops pairs one at a time).  The
+    backend's plans (tag) are separate from the tracker's, so a backend
+    worker thread can decode while the frontend tracks."""
     b = feat_i.shape[0]
     H, W = _hw(shape_i)
-    r11, r21, _ = model.encoder.infer_pair(feat_i, pos_i, feat_j, pos_j, (H, W))
+    r11, r21, _ = model.encoder.infer_pair(feat_i, pos_i, feat_j, pos_j, (H, W), tag=tag)
     Xa = [r11["pts3d"].clone(), r21["pts3d"].clone()]
     Ca = [r11["conf"].clone(), r21["conf"].clone()]
     Da = [r11["desc"].clone(), r21["desc"].clone()]
     Qa = [r11["desc_conf"].clone(), r21["desc_conf"].clone()]
-    r22, r12, _ = model.encoder.infer_pair(feat_j, pos_j, feat_i, pos_i, (H, W))
+    r22, r12, _ = model.encoder.infer_pair(feat_j, pos_j, feat_i, pos_i, (H, W), tag=tag)
     Xa += [r22["pts3d"], r12["pts3d"]]
     Ca += [r22["conf"], r12["conf"]]
     Da += [r22["desc"], r12["desc"]]
@@ -184,10 +187,11 @@ def splatt3r_decode_symmetric_batch(model, feat_i, pos_i, feat_j, pos_j, shape_i
     return downsample(X, C, D, Q)
 
 
-def splatt3r_match_symmetric(model, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
+def splatt3r_match_symmetric(model, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j,
+                             tag="backend"):
     """splatt3r_utils.py:539-576."""
     X, C, D, Q = splatt3r_decode_symmetric_batch(model, feat_i, pos_i, feat_j, pos_j,
-                                                 shape_i, shape_j)
+                                                 shape_i, shape_j, tag)
     b = X.shape[1]
     Xii, Xji, Xjj, Xij = X
     Dii, Dji, Djj, Dij = D

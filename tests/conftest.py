@@ -70,3 +70,16 @@ def pytest_terminal_summary(terminalreporter):
             json.dump(_PARITY, f, indent=1)
     except OSError:
         pass
+
+
+@pytest.fixture(autouse=True)
+def _progress_marker(request):
+    """Append the running test's name to gpurun_out/progress.log (long GPU
+    tests otherwise write nothing until they finish)."""
+    try:
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(REPO, "gpurun_out", "progress.log"), "a") as f:
+            f.write(f"start {request.node.nodeid}\n")
+    except OSError:
+        pass
+    yield

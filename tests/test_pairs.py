@@ -56,6 +56,96 @@ def test_gather_map_world_size_2_gloo():
         np.testing.assert_array_equal(res[r], want)
 
 
+def fake_match(feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
+    """Deterministic stand-in for splatt3r_match_symmetric (no network on the
+    CPU): the 8-tuple's shapes and dtypes, values derived from the keyframe
+    features so every pair differs."""
+    b = feat_i.shape[0]
+    H, W = (int(v) for v in shape_i[0].reshape(-1)[:2])
+    hw = H * W
+    ki = feat_i[:, 0, 0].round().long()
+    kj = feat_j[:, 0, 0].round().long()
+    ar = torch.arange(hw)
+    idx_i2j = (ar[None] * (ki[:, None] + 1) + kj[:, None] * 7) % hw
+    idx_j2i = (ar[None] * (kj[:, None] + 1) + ki[:, None] * 5) % hw
+    valid_j = ((ar[None] + ki[:, None]) % 3 != 0)[..., None]
+    valid_i = ((ar[None] + kj[:, None]) % 4 != 0)[..., None]
+    q = lambda s: (1.0 + ((ar[None] * (s[:, None] + 2)) % 11).float() * (s[:, None] + 1).float()
+                   / 5.0)[..., None]
+    return idx_i2j, idx_j2i, valid_j, valid_i, q(ki), q(kj), q(ki + kj), q(ki * 2 + kj)
+
+
+def _kf_frames(n, H=32, W=48):
+    from splatt3r_amd.frame import Frame
+    from splatt3r_amd.net import positions
+    frames = []
+    for k in range(n):
+        f = Frame(k, torch.zeros(1, 3, H, W), torch.tensor([[H, W]]), torch.tensor([[H, W]]),
+                  T_WC=object())
+        f.feat = torch.full((1, (H // 16) * (W // 16), 8), float(k))
+        f.pos = positions(1, H // 16, W // 16, "cpu")
+        frames.append(f)
+    return frames
+
+
+PAIRS = [[(0, 1), (1, 2), (0, 2), (2, 3), (1, 3), (0, 3), (3, 4)], [(4, 5), (2, 5), (1, 5)]]
+
+
+def _edges(fg):
+    return {k: getattr(fg, k).clone() for k in ("ii", "jj", "idx_ii2jj", "idx_jj2ii",
+                                                "valid_match_j", "valid_match_i", "Q_ii2jj",
+                                                "Q_jj2ii")}
+
+
+def _shard_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from splatt3r_amd.global_opt import FactorGraph
+    from splatt3r_amd.pairs import PairShard
+    sh = PairShard(None, "cpu", match_fn=fake_match)
+    if rank == 0:
+        frames = _kf_frames(6)
+        for k, f in enumerate(frames):
+            sh.broadcast_keyframe(k, f)
+        fg = FactorGraph(None, frames, device="cpu", shard=sh)
+        accepted = [fg.add_factors([p[0] for p in ps], [p[1] for p in ps], 0.5) for ps in PAIRS]
+        sh.stop()
+        q.put((rank, (accepted, {k: v.numpy() for k, v in _edges(fg).items()}, sh.stats)))
+    else:
+        sh.serve()
+        q.put((rank, sh.stats))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_sharded_add_factors_matches_single_rank_gloo(ws):
+    """FactorGraph.add_factors with the pair shard over ws gloo ranks (pair p
+    on rank p mod ws, keyframe features broadcast at creation, idx/valid/Q
+    gathered to rank 0) builds exactly the single-rank edges."""
+    from splatt3r_amd.global_opt import FactorGraph
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    accepted, edges, st0 = res[0]
+    fg = FactorGraph(None, _kf_frames(6), device="cpu", match_fn=fake_match)
+    want_acc = [fg.add_factors([p[0] for p in ps], [p[1] for p in ps], 0.5) for ps in PAIRS]
+    assert accepted == want_acc
+    for k, v in _edges(fg).items():
+        np.testing.assert_array_equal(edges[k], v.numpy(), err_msg=k)
+    assert len(edges["ii"]) > 0
+    # every rank received every keyframe and ran its share of the pairs
+    n_pairs = sum(len(ps) for ps in PAIRS)
+    assert sum(res[r]["pairs"] if r else st0["pairs"] for r in range(ws)) == n_pairs
+    assert all((res[r] if r else st0)["keyframes"] == 6 for r in range(ws))
+
+
 @pytest.mark.gpu
 def test_world_gaussians_matches_numpy():
     from splatt3r_amd.pairs import world_gaussians
@@ -90,3 +180,98 @@ def test_world_gaussians_matches_numpy():
     sh0 = res["sh"].numpy().reshape(-1, 3) + (rgb - 0.5) / C0
     np.testing.assert_allclose(out[:, 9:12], np.clip(sh0 * C0 + 0.5, 0, 1), rtol=1e-5, atol=1e-6)
     np.testing.assert_array_equal(out[:, 12], res["opacities"].numpy().reshape(-1))
+
+
+def _beat(rank, msg):
+    import time
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(path, exist_ok=True)
+    with open(os.path.join(path, "progress.log"), "a") as f:
+        f.write(f"{time.time():.1f} rank {rank}: {msg}\n")
+
+
+def _gpu_shard_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import datetime
+    _beat(rank, "init")
+    dist.init_process_group("gloo", rank=rank, world_size=ws,
+                            timeout=datetime.timedelta(seconds=240))
+    _beat(rank, "process group up")
+    try:
+        from splatt3r_amd.frame import Keyframes, create_frame
+        from splatt3r_amd.pairs import PairShard, q_weighted, shard
+        from splatt3r_amd.splatt3r_utils import load_splatt3r, splatt3r_match_symmetric
+        from splatt3r_amd.synthetic import tum_like_sequence
+        from splatt3r_amd.weights import FULL
+        dev = torch.device("cuda", 0)
+        model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
+        _beat(rank, "model loaded")
+        sh = PairShard(model, dev)
+        pairs = [(0, 1), (1, 2), (0, 2), (2, 3), (1, 3)]
+        if rank == 0:
+            imgs = tum_like_sequence(4, 384, 512, seed=5, step_px=3.0, device=dev)
+            kfs = Keyframes()
+            for k in range(4):
+                f = create_frame(k, imgs[k], device=dev)
+                f.feat, f.pos, _ = model.encoder._encode_image(f.img, f.img_true_shape)
+                kfs.append(f)
+                sh.broadcast_keyframe(k, f)
+            _beat(rank, "keyframes broadcast")
+            got = sh.match_pairs([p[0] for p in pairs], [p[1] for p in pairs])
+            _beat(rank, "pairs gathered")
+            sh.stop()
+            # the same per-rank batches decoded locally, reassembled in order
+            want = [None] * len(pairs)
+            for r in range(ws):
+                mine = shard(pairs, ws, r)
+                cat = lambda ks, a: torch.cat([getattr(kfs[k], a) for k in ks])
+                m = splatt3r_match_symmetric(model, cat([p[0] for p in mine], "feat"),
+                                             cat([p[0] for p in mine], "pos"),
+                                             cat([p[1] for p in mine], "feat"),
+                                             cat([p[1] for p in mine], "pos"),
+                                             [kfs[0].img_true_shape] * len(mine),
+                                             [kfs[0].img_true_shape] * len(mine))
+                res = q_weighted(m, sh.Q_conf)
+                for s_, p in enumerate(range(r, len(pairs), ws)):
+                    want[p] = [t[s_] for t in res]
+            ok = all(torch.equal(got[k][p], want[p][k]) for p in range(len(pairs))
+                     for k in range(6))
+            q.put((rank, ok))
+        else:
+            sh.serve()
+            _beat(rank, "served")
+            q.put((rank, sh.stats["pairs"]))
+    except Exception as e:           # report instead of leaving the peer blocked
+        q.put((rank, f"error: {e!r}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_pairs_two_ranks_on_gpu_match_local_decode():
+    """Two ranks on the GPU (gloo transport staged through the host): keyframe
+    features broadcast from rank 0, pairs decoded on rank p mod 2 with the
+    real network, idx/valid/Q gathered back in pair order -- identical to
+    decoding the same per-rank batches locally."""
+    ws, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gpu_shard_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        while len(res) < ws:
+            r, v = q.get(timeout=300)
+            res[r] = v
+            assert not (isinstance(v, str) and v.startswith("error")), (r, v)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    assert res[0] is True
+    assert res[1] == 2          # pairs 1 and 3 ran on rank 1

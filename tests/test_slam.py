@@ -163,3 +163,84 @@ def test_viz_frontend_appends_world_map_like_the_reference():
     np.testing.assert_array_equal(gm.kf_id[:ref.n].cpu().numpy(), ref.kf[:ref.n])
     img = render_map(gm, np.eye(4, dtype=np.float32), 256, 192, 60.0)
     assert img.shape == (3, 192, 256) and torch.isfinite(img).all()
+
+
+def _model_and_frames(n, seed=3, step_px=2.0):
+    from splatt3r_amd.splatt3r_utils import load_splatt3r
+    from splatt3r_amd.synthetic import tum_like_sequence
+    from splatt3r_amd.weights import FULL
+    dev = torch.device("cuda", 0)
+    model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
+    return dev, model, tum_like_sequence(n, 384, 512, seed=seed, step_px=step_px, device=dev)
+
+
+@pytest.mark.gpu
+def test_frontend_with_backend_single_thread():
+    """main.py with single_thread: every keyframe is queued to the backend
+    (retrieval update + add_factors + GN), the factor graph grows, keyframe
+    poses stay finite, the retrieval database holds every keyframe."""
+    from splatt3r_amd.backend import Backend
+    from splatt3r_amd.frame import Keyframes
+    from splatt3r_amd.slam import Frontend
+    dev, model, frames = _model_and_frames(10, step_px=4.0)
+    be = Backend(model, Keyframes(), device=dev)
+    fe = Frontend(model, device=dev, spatial_stride=4, render=False, backend=be)
+    for i in range(10):
+        fe.step(i, frames[i])
+    n_kf = len(fe.keyframes)
+    assert n_kf >= 3
+    assert be.stats["optimized"] == n_kf
+    assert be.retrieval.kf_counter == n_kf
+    assert be.factor_graph.ii.numel() >= 1
+    for k in range(n_kf):
+        assert torch.isfinite(fe.keyframes[k].T_WC.data).all()
+
+
+@pytest.mark.gpu
+def test_frontend_with_backend_worker_thread():
+    """single_thread: False -- keyframe tasks run on the backend worker's
+    own HIP stream while the frontend keeps tracking."""
+    from splatt3r_amd.backend import Backend
+    from splatt3r_amd.frame import Keyframes
+    from splatt3r_amd.slam import Frontend
+    dev, model, frames = _model_and_frames(10, step_px=4.0)
+    be = Backend(model, Keyframes(), device=dev)
+    be.start_worker()
+    fe = Frontend(model, device=dev, spatial_stride=4, render=True, backend=be)
+    try:
+        for i in range(10):
+            fe.step(i, frames[i])
+        be.wait()
+    finally:
+        be.stop()
+    assert be.stats["optimized"] == len(fe.keyframes) >= 3
+    assert fe.stats["tracked"] == 9
+    for k in range(len(fe.keyframes)):
+        assert torch.isfinite(fe.keyframes[k].T_WC.data).all()
+
+
+@pytest.mark.gpu
+def test_relocalization_with_and_without_backend():
+    """A RELOC frame showing keyframe 0's view again: the backend's
+    relocalization (main.py:76-119) retrieves keyframe 0, accepts the strict
+    edges and returns the frontend to TRACKING with the new keyframe at the
+    matched pose; without a backend the frontend stays in RELOC and makes no
+    keyframe."""
+    from splatt3r_amd.backend import Backend
+    from splatt3r_amd.frame import Keyframes, Mode
+    from splatt3r_amd.slam import Frontend
+    dev, model, frames = _model_and_frames(6, step_px=4.0)
+    for with_backend in (True, False):
+        be = Backend(model, Keyframes(), device=dev) if with_backend else None
+        fe = Frontend(model, device=dev, spatial_stride=4, render=False, backend=be)
+        for i in range(5):
+            fe.step(i, frames[i])
+        n_kf = len(fe.keyframes)
+        fe.mode = Mode.RELOC
+        fe.step(5, frames[0])
+        assert fe.stats["reloc"] == 1
+        if with_backend:
+            assert be.stats["reloc_success"] == 1, be.stats
+            assert fe.mode == Mode.TRACKING and len(fe.keyframes) == n_kf + 1
+        else:
+            assert fe.mode == Mode.RELOC and len(fe.keyframes) == n_kf

@@ -1,11 +1,11 @@
 """Attention kernel variants on the network's shapes (graph-replay timing;
-tuning harness).  python -m splatt3r_amd.bench_attn"""
+tuning harness).  python -m tools.bench_attn"""
 from __future__ import annotations
 
 import torch
 
 from splatt3r_amd import _lib, ops
-from splatt3r_amd.bench_gemm import timeit
+from tools.bench_gemm import timeit
 
 
 def main():

@@ -1,6 +1,6 @@
 """Encoder plan replay time vs image batch (tuning harness).
 
-  python -m splatt3r_amd.bench_encb
+  python -m tools.bench_encb
 """
 from __future__ import annotations
 

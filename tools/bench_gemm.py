@@ -2,7 +2,7 @@
 one process, next to torch.matmul (hipBLASLt) on the same fp16 operands as
 a calibration of what the box reaches on that shape.
 
-  python -m splatt3r_amd.bench_gemm
+  python -m tools.bench_gemm
 """
 from __future__ import annotations
 

@@ -6,7 +6,7 @@ with their B operand cold.  This times one launch after evicting the caches
 (a 512 MiB write), after a streaming read of B only (an L2/MALL prefetch),
 and back to back (warm), for each tile/stage choice.
 
-  python -m splatt3r_amd.bench_gemm_cold
+  python -m tools.bench_gemm_cold
 """
 from __future__ import annotations
 

@@ -3,7 +3,7 @@ long K) for each staging depth, plus a 4096^3 throughput point."""
 import torch
 
 from splatt3r_amd import _lib, ops
-from splatt3r_amd.bench_gemm import timeit
+from tools.bench_gemm import timeit
 
 
 def main():

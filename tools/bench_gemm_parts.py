@@ -2,14 +2,14 @@
 the MFMAs skipped (operand DMA + barriers + LDS reads) and with the DMA
 skipped (LDS reads + MFMAs on stale LDS), HIP-graph replays (tuning only).
 
-  python -m splatt3r_amd.bench_gemm_parts
+  python -m tools.bench_gemm_parts
 """
 from __future__ import annotations
 
 import torch
 
 from splatt3r_amd import _lib, ops
-from splatt3r_amd.bench_gemm import timeit
+from tools.bench_gemm import timeit
 
 import argparse
 

@@ -1,12 +1,12 @@
 """Dense matching kernels at C2 size (tuning harness): per-kernel HIP-graph
 timing of prep / iter_proj / occlusion / refine_matches on a smooth synthetic
-pointmap pair.  python -m splatt3r_amd.bench_match"""
+pointmap pair.  python -m tools.bench_match"""
 from __future__ import annotations
 
 import torch
 
 from splatt3r_amd import matching
-from splatt3r_amd.bench_gemm import timeit
+from tools.bench_gemm import timeit
 
 
 def main():

@@ -5,7 +5,7 @@ Algorithmic bytes: forward 56 P + 12 H W, backward
 120 P + 12 H W.  Timed with HIP events on torch's current stream (the one the
 rasterizer launches on).
 
-  python -m splatt3r_amd.bench_raster --P 4194304 --iters 10
+  python -m tools.bench_raster --P 4194304 --iters 10
 """
 from __future__ import annotations
 

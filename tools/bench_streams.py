@@ -2,7 +2,7 @@
 then on two streams at once, as HIP-graph replays and as eager launches, with
 and without a host synchronisation of the first stream in between (tuning).
 
-  python -m splatt3r_amd.bench_streams
+  python -m tools.bench_streams
 """
 from __future__ import annotations
 

@@ -1,6 +1,6 @@
 """Run one s3n_gemm configuration a few times (for rocprofv3 --pmc passes).
 
-  python -m splatt3r_amd.gemm_one M N K tile [split_k] [debug]
+  python -m tools.gemm_one M N K tile [split_k] [debug]
 """
 from __future__ import annotations
 

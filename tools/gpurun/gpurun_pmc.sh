@@ -3,9 +3,8 @@
 set -o pipefail
 mkdir -p gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-cd splatt3r-slam_amd
 i=0
 for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_VALU GRBM_GUI_ACTIVE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $grp -d ../gpurun_out/pmc/p$i -o run --output-format csv -- python3 -m splatt3r_amd.gemm_one $ARGS > ../gpurun_out/pmc/log$i.txt 2>&1 || exit $?
+  timeout -s KILL 90 rocprofv3 --pmc $grp -d gpurun_out/pmc/p$i -o run --output-format csv -- python3 -m tools.gemm_one $ARGS > gpurun_out/pmc/log$i.txt 2>&1 || exit $?
 done

@@ -10,4 +10,4 @@ tail -1 gpurun_out/smoke.log
 timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
 tail -c 3000 gpurun_out/bench.log
 [ -n "$NO_PROF" ] && exit 0
-bash gpurun_prof.sh
+bash tools/gpurun/gpurun_prof.sh

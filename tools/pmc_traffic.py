@@ -3,10 +3,10 @@
 Two steps (gpurun_traffic.sh runs both):
 
   rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d D1 -- \\
-      python3 -m splatt3r_amd.pmc_traffic run
+      python3 -m tools.pmc_traffic run
   rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d D2 -- \\
-      python3 -m splatt3r_amd.pmc_traffic run
-  python -m splatt3r_amd.pmc_traffic summarize D1 D2 --out traffic.json
+      python3 -m tools.pmc_traffic run
+  python -m tools.pmc_traffic summarize D1 D2 --out traffic.json
 
 `run` builds the full-size network plans (512x384, the bench's model),
 warms them, then replays one frame's network (encoder plan + pair plan)

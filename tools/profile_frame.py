@@ -1,7 +1,7 @@
 """Host-side profile of the per-frame SLAM step (cProfile over bench.py's
 frame loop) — where the frame's wall time goes outside GPU kernels.
 
-  python -m splatt3r_amd.profile_frame [--steps 10]
+  python -m tools.profile_frame [--steps 10]
 """
 from __future__ import annotations
 

@@ -1,6 +1,6 @@
 """Per-launch HIP-event profile of the network plans (tuning harness).
 
-  python -m splatt3r_amd.profile_net [--H 384 --W 512 --Bp 1 --reps 5]
+  python -m tools.profile_net [--H 384 --W 512 --Bp 1 --reps 5]
 
 Prints one line per distinct launch shape: count, mean us, TFLOP/s, and the
 share of the frame's network time."""

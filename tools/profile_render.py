@@ -2,7 +2,7 @@
 frontend frames, then times the render glue stage by stage (host wall with a
 device sync after each stage) and the whole call unsynced.
 
-  python -m splatt3r_amd.profile_render
+  python -m tools.profile_render
 """
 from __future__ import annotations
 

@@ -4,7 +4,7 @@ matching, tracking, render) on the current stream, and how much of the
 frame period they overlap.  HIP events only, no profiler attached, so the
 overlap is the one bench.py gets.
 
-  python -m splatt3r_amd.profile_spans [--steps 20]
+  python -m tools.profile_spans [--steps 20]
 """
 from __future__ import annotations
 

@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 --kernel-trace --stats run into the table kept under
 profiles/ (per kernel: calls, total ms, average us, share).
 
-  python -m splatt3r_amd.rocprof_summary <results.db | kernel_stats.csv> [--top N]
+  python -m tools.rocprof_summary <results.db | kernel_stats.csv> [--top N]
 
 Reads either the rocpd SQLite database rocprofv3 writes by default or the
 `*_kernel_stats.csv` of `--output-format csv`.

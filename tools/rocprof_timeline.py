@@ -2,7 +2,7 @@
 busy time, the union of all queues (GPU busy), idle gaps, and the kernels
 of a time window in start order.
 
-  python -m splatt3r_amd.rocprof_timeline <results.db> [--last-ms 50] [--list 0]
+  python -m tools.rocprof_timeline <results.db> [--last-ms 50] [--list 0]
 """
 from __future__ import annotations
 
