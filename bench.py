@@ -234,7 +234,7 @@ def bench_backend(model, dev, steps, rank):
     finally:
         be.stop()
     st = {k: fe.stats[k] - s0[k] for k in fe.stats}
-    bs = {k: be.stats[k] - b0.get(k, 0) for k in be.stats}
+    bs = {k: be.stats[k] - b0.get(k, 0) for k in be.stats if isinstance(be.stats[k], int)}
     return {"frames_per_s": steps / t, "frames_per_s_frontend_only_window": steps / t_front,
             "steps": steps, "keyframes": st["keyframes"],
             "keyframe_rate": st["keyframes"] / steps, "backend_tasks": bs["optimized"],

@@ -184,6 +184,13 @@ int s3n_prng_fill(float* out, int64_t n, uint64_t seed, float a, float c, void* 
 int s3n_cast_f16(const float* in, int64_t ld_in, void* out, int64_t ld_out, int64_t rows,
                  int cols, void* stream);
 
+/* fp16 range guard: every fp16 activation the GEMM epilogues and LayerNorm
+ * write saturates at +-65504 (NaN passes through) instead of overflowing
+ * to inf, and sets a device flag.  Returns how many of the two flags (GEMM,
+ * LayerNorm) are set (0 = no activation left the fp16 range since the last
+ * reset), -1 on a HIP error; reset != 0 clears them.  Synchronous. */
+int s3n_f16_saturations(int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,7 +3,7 @@ reference from /root/reference (this container only; the GPU box never reads
 /root/reference).  Committed outputs are data only (inputs + expected
 outputs), never reference source.
 
-  python oracle/gen_golden.py [section ...]     sections: matching, net, net_c4, n1, mono, resize, viz, render
+  python oracle/gen_golden.py [section ...]     sections: matching, net, net_c4, n1, mono, resize, viz, portrait, render
 
 matching : splatt3r_slam/image.py img_gradient (imported) driven exactly as
            splatt3r_slam/matching.py:25-49 prep_for_iter_proj does.
@@ -492,6 +492,39 @@ def gen_viz():
           "num_rendered", o["num_rendered"])
 
 
+def gen_portrait():
+    """Portrait inputs through the reference model API: a landscape-shaped
+    image tensor with a portrait true_shape (ManyAR_PatchEmbed transposes it,
+    patch_embed.py:42-70; _LandscapeWrapperYes runs the heads on the
+    transposed grid and transposes back, utils/misc.py:80-116).  Small
+    config, use_offsets."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "splatt3r-slam_amd"))
+    from splatt3r_amd import weights as W
+    import dataclasses
+    keys = ("pts3d", "conf", "desc", "desc_conf", "scales", "rotations", "sh", "opacities", "means")
+    cfg = dataclasses.replace(W.SMALL, use_offsets=True)
+    torch.manual_seed(0)
+    model = build_reference_model(cfg)
+    load_prng(model, cfg, seed=1234)
+    g = torch.Generator().manual_seed(9)
+    img1 = torch.rand(1, 3, 48, 64, generator=g) * 2 - 1
+    img2 = torch.rand(1, 3, 48, 64, generator=g) * 2 - 1
+    shape = torch.tensor([[64, 48]], dtype=torch.int32)      # portrait true shape
+    f1, p1, _ = model._encode_image(img1, shape)
+    f2, p2, _ = model._encode_image(img2, shape)
+    dec1, dec2 = model._decoder(f1, p1, f2, p2)
+    dec1, dec2 = list(dec1), list(dec2)
+    r1 = model._downstream_head(1, [t.float() for t in dec1], shape)
+    r2 = model._downstream_head(2, [t.float() for t in dec2], shape)
+    out = dict(img1=img1.numpy(), img2=img2.numpy(), true_shape=shape.numpy(), feat1=f1.numpy(),
+               pos1=p1.numpy())
+    for k in keys:
+        out["res1_" + k] = r1[k].numpy()
+        out["res2_" + k] = r2[k].numpy()
+    np.savez_compressed(os.path.join(GOLDEN, "net_small_portrait.npz"), **out)
+    print("wrote net_small_portrait.npz", r1["pts3d"].shape)
+
+
 def _sim3_matrix(T):
     """lietorch Sim3 data [t, q(xyzw), s] -> 4x4 [sR | t] (fp64 -> fp32), the
     matrix splatt3r_utils.py:153-165 builds through SE3.matrix()."""
@@ -658,7 +691,7 @@ def gen_n1():
     print("wrote n1_render.npz")
 
 
-SECTIONS = {"matching": gen_matching, "render": gen_render, "net": gen_net, "net_c4": gen_net_c4, "n1": gen_n1, "mono": gen_mono, "resize": gen_resize, "viz": gen_viz}
+SECTIONS = {"matching": gen_matching, "render": gen_render, "net": gen_net, "net_c4": gen_net_c4, "n1": gen_n1, "mono": gen_mono, "resize": gen_resize, "viz": gen_viz, "portrait": gen_portrait}
 
 
 def main(argv):

@@ -222,11 +222,65 @@ __device__ __forceinline__ double a_elem(const double* A, int a, int b) {
   return A[r * 7 - r * (r - 1) / 2 + (c - r)];
 }
 
+// Edges incident to every unfixed pose (CSR, edge ids ascending): one
+// workgroup counts, scans, fills with atomic cursors and sorts each list, so
+// the assembly below visits only a pose's own edges, in edge order.
+constexpr int kCsrThreads = 1024;
+
+__global__ void __launch_bounds__(kCsrThreads)
+k_edge_csr(const int32_t* __restrict__ ii, const int32_t* __restrict__ jj, int E, int num_fix,
+           int np, int32_t* __restrict__ off, int32_t* __restrict__ list) {
+  __shared__ int cnt[4097];
+  const int tid = threadIdx.x;
+  for (int i = tid; i <= np; i += kCsrThreads) cnt[i] = 0;
+  __syncthreads();
+  for (int e = tid; e < E; e += kCsrThreads) {
+    const int io = ii[e] - num_fix, jo = jj[e] - num_fix;
+    if (io >= 0) atomicAdd(&cnt[io], 1);
+    if (jo >= 0) atomicAdd(&cnt[jo], 1);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int i = 0; i < np; ++i) {
+      const int c = cnt[i];
+      off[i] = acc;
+      cnt[i] = acc;       // becomes the fill cursor
+      acc += c;
+    }
+    off[np] = acc;
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += kCsrThreads) {
+    const int io = ii[e] - num_fix, jo = jj[e] - num_fix;
+    if (io >= 0) list[atomicAdd(&cnt[io], 1)] = e;
+    if (jo >= 0) list[atomicAdd(&cnt[jo], 1)] = e;
+  }
+  __syncthreads();
+  // ascending edge ids per pose (insertion sort; lists are short)
+  for (int pz = tid; pz < np; pz += kCsrThreads) {
+    const int a = off[pz], z = off[pz + 1];
+    for (int i = a + 1; i < z; ++i) {
+      const int v = list[i];
+      int j = i - 1;
+      while (j >= a && list[j] > v) {
+        list[j + 1] = list[j];
+        --j;
+      }
+      list[j + 1] = v;
+    }
+  }
+}
+
 // Dense H [n x n], b [n] over the unfixed poses: edge blocks (io,io)+A,
 // (io,jo)-A, (jo,io)-A, (jo,jo)+A and b(io) -u, b(jo) +u (SparseBlock
-// update_lhs/update_rhs with Hs = {A, -A, -A, A}, gs = {-u, u}).
+// update_lhs/update_rhs with Hs = {A, -A, -A, A}, gs = {-u, u}).  Element
+// (r, c) of block (pr, pc) sums over pr's incident edges in edge order: the
+// same terms in the same order as a sweep over all edges (the others add
+// nothing), at O(degree) instead of O(E) per element.
 __global__ void k_assemble(const double* __restrict__ esum, const int32_t* __restrict__ ii,
-                           const int32_t* __restrict__ jj, int E, int num_fix, int n,
+                           const int32_t* __restrict__ jj, const int32_t* __restrict__ off,
+                           const int32_t* __restrict__ list, int num_fix, int n,
                            double* __restrict__ H, double* __restrict__ b, const double* state) {
   if (state && state[0] != 0.0) return;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -235,7 +289,8 @@ __global__ void k_assemble(const double* __restrict__ esum, const int32_t* __res
     const int r = (int)(t / n), c = (int)(t % n);
     const int pr = r / 7, a = r % 7, pc = c / 7, bb = c % 7;
     double h = 0.0;
-    for (int e = 0; e < E; ++e) {
+    for (int q = off[pr]; q < off[pr + 1]; ++q) {
+      const int e = list[q];
       const int io = ii[e] - num_fix, jo = jj[e] - num_fix;
       const double* A = esum + (int64_t)e * NA;
       double sgn = 0.0;
@@ -250,7 +305,8 @@ __global__ void k_assemble(const double* __restrict__ esum, const int32_t* __res
     const int r = (int)(t - (int64_t)n * n);
     const int pr = r / 7, a = r % 7;
     double v = 0.0;
-    for (int e = 0; e < E; ++e) {
+    for (int q = off[pr]; q < off[pr + 1]; ++q) {
+      const int e = list[q];
       const int io = ii[e] - num_fix, jo = jj[e] - num_fix;
       const double u = esum[(int64_t)e * NA + 28 + a];
       if (pr == io) v -= u;
@@ -258,6 +314,156 @@ __global__ void k_assemble(const double* __restrict__ esum, const int32_t* __res
     }
     b[r] = v;
   }
+}
+
+// ---- blocked right-looking Cholesky (multi-workgroup) ------------------
+// H = L L^T in place (lower), 64-wide panels, three launches per panel:
+// the diagonal block in one workgroup (LDS), the panel below it (one
+// workgroup per 64 rows, triangular solve against the LDS diagonal block),
+// and the trailing lower triangle (one workgroup per 64x64 block,
+// H_ij -= L_i L_j^T with the two panel slices in LDS).  Replaces the
+// O(n^3)-in-one-workgroup factorisation for long keyframe sequences.  A
+// non-positive pivot sets ctl[0]; later launches then skip and the solve
+// writes dx = 0 (SimplicialLLT failure in the reference).
+constexpr int kNB = 64;
+// systems up to this size keep the single-workgroup factorisation (the
+// small pose graphs of the first keyframes: one launch instead of 3 per panel)
+constexpr int kSmallChol = 7 * 24;
+
+__global__ void __launch_bounds__(kThreads)
+k_potrf_diag(double* __restrict__ H, int n, int k0, int* __restrict__ ctl, const double* state) {
+  if ((state && state[0] != 0.0) || ctl[0]) return;
+  __shared__ double A[kNB][kNB + 1];
+  __shared__ int fail;
+  const int nb = min(kNB, n - k0), tid = threadIdx.x;
+  for (int t = tid; t < nb * nb; t += kThreads) {
+    const int i = t / nb, j = t % nb;
+    A[i][j] = H[(int64_t)(k0 + i) * n + k0 + j];
+  }
+  if (tid == 0) fail = 0;
+  __syncthreads();
+  for (int k = 0; k < nb; ++k) {
+    if (tid == 0) {
+      const double d = A[k][k];
+      if (!(d > 0.0)) fail = 1;
+      A[k][k] = fail ? 1.0 : sqrt(d);
+    }
+    __syncthreads();
+    if (fail) break;
+    for (int i = k + 1 + tid; i < nb; i += kThreads) A[i][k] /= A[k][k];
+    __syncthreads();
+    const int m = nb - k - 1;
+    for (int t = tid; t < m * m; t += kThreads) {
+      const int i = k + 1 + t / m, j = k + 1 + t % m;
+      if (j <= i) A[i][j] -= A[i][k] * A[j][k];
+    }
+    __syncthreads();
+  }
+  if (fail) {
+    if (tid == 0) ctl[0] = 1;
+    return;
+  }
+  for (int t = tid; t < nb * nb; t += kThreads) {
+    const int i = t / nb, j = t % nb;
+    if (j <= i) H[(int64_t)(k0 + i) * n + k0 + j] = A[i][j];
+  }
+}
+
+// L21 = A21 L11^-T: one thread per row of the panel, columns in order.
+__global__ void __launch_bounds__(kThreads)
+k_trsm_panel(double* __restrict__ H, int n, int k0, const int* __restrict__ ctl,
+             const double* state) {
+  if ((state && state[0] != 0.0) || ctl[0]) return;
+  __shared__ double L[kNB][kNB + 1];
+  const int nb = min(kNB, n - k0), tid = threadIdx.x;
+  for (int t = tid; t < nb * nb; t += kThreads) {
+    const int i = t / nb, j = t % nb;
+    L[i][j] = j <= i ? H[(int64_t)(k0 + i) * n + k0 + j] : 0.0;
+  }
+  __syncthreads();
+  const int r = k0 + nb + blockIdx.x * kThreads + tid;
+  if (r >= n) return;
+  // in place along the row (the solved prefix stays in the row, L1-resident)
+  double* row = H + (int64_t)r * n + k0;
+  for (int c = 0; c < nb; ++c) {
+    double v = row[c];
+    for (int j = 0; j < c; ++j) v -= row[j] * L[c][j];
+    row[c] = v / L[c][c];
+  }
+}
+
+// Trailing update of the lower triangle: block (bi, bj), bi >= bj, of the
+// rows/cols after the panel: H_ij -= L_i L_j^T (L_* = panel columns).
+__global__ void __launch_bounds__(kThreads)
+k_syrk_trailing(double* __restrict__ H, int n, int k0, const int* __restrict__ ctl,
+                const double* state) {
+  if ((state && state[0] != 0.0) || ctl[0]) return;
+  const int nb = min(kNB, n - k0);
+  const int base = k0 + nb;
+  // linear block index -> (bi, bj), bj <= bi
+  const int t = blockIdx.x;
+  int bi = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+  while (bi * (bi + 1) / 2 > t) --bi;
+  const int bj = t - bi * (bi + 1) / 2;
+  const int r0 = base + bi * kNB, c0 = base + bj * kNB;
+  if (r0 >= n || c0 >= n) return;
+  __shared__ double Li[kNB][kNB + 1];
+  __shared__ double Lj[kNB][kNB + 1];
+  const int tid = threadIdx.x;
+  for (int q = tid; q < kNB * nb; q += kThreads) {
+    const int i = q / nb, k = q % nb;
+    Li[i][k] = r0 + i < n ? H[(int64_t)(r0 + i) * n + k0 + k] : 0.0;
+    Lj[i][k] = c0 + i < n ? H[(int64_t)(c0 + i) * n + k0 + k] : 0.0;
+  }
+  __syncthreads();
+  // 256 threads x 16 outputs: thread (ty, tx) owns rows ty*4..+4, cols tx*4..+4
+  const int ty = tid / 16, tx = tid % 16;
+  double acc[4][4] = {};
+  for (int k = 0; k < nb; ++k) {
+    double a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { a[u] = Li[ty * 4 + u][k]; b[u] = Lj[tx * 4 + u][k]; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[u][v] += a[u] * b[v];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int i = r0 + ty * 4 + u, j = c0 + tx * 4 + v;
+      if (i < n && j < n && j <= i) H[(int64_t)i * n + j] -= acc[u][v];
+    }
+}
+
+// L L^T x = b after the blocked factorisation (one workgroup), dx = -x;
+// a failed factorisation (ctl[0]) gives dx = 0.
+__global__ void __launch_bounds__(kThreads)
+k_chol_subst(const double* __restrict__ H, double* __restrict__ b, int n,
+             float* __restrict__ dx, const int* __restrict__ ctl, const double* state) {
+  if (state && state[0] != 0.0) return;
+  const int tid = threadIdx.x;
+  if (ctl[0]) {
+    for (int i = tid; i < n; i += kThreads) dx[i] = 0.f;
+    return;
+  }
+  for (int k = 0; k < n; ++k) {
+    if (tid == 0) b[k] /= H[(int64_t)k * n + k];
+    __syncthreads();
+    const double yk = b[k];
+    for (int i = k + 1 + tid; i < n; i += kThreads) b[i] -= H[(int64_t)i * n + k] * yk;
+    __syncthreads();
+  }
+  for (int k = n - 1; k >= 0; --k) {
+    if (tid == 0) b[k] /= H[(int64_t)k * n + k];
+    __syncthreads();
+    const double xk = b[k];
+    for (int i = tid; i < k; i += kThreads) b[i] -= H[(int64_t)k * n + i] * xk;
+    __syncthreads();
+  }
+  for (int i = tid; i < n; i += kThreads) dx[i] = (float)(-b[i]);
 }
 
 // One workgroup: in-place fp64 Cholesky H = L L^T (lower), then L L^T x = b,
@@ -352,6 +558,9 @@ struct Ws {
   double* H;
   double* b;
   double* state;
+  int32_t* off;    // [free poses + 1] CSR offsets of the incident edges
+  int32_t* list;   // [2 E] incident edge ids
+  int* ctl;        // [0]: blocked Cholesky failed (non-positive pivot)
   int S;
 };
 
@@ -378,6 +587,12 @@ Ws carve(void* ws, int n_poses, int n_edges, int64_t n_points, int num_fix) {
   w.b = reinterpret_cast<double*>(p);
   p += align256(sizeof(double) * (size_t)n);
   w.state = reinterpret_cast<double*>(p);
+  p += align256(sizeof(double) * 4);
+  w.off = reinterpret_cast<int32_t*>(p);
+  p += align256(sizeof(int32_t) * (size_t)(n / 7 + 1));
+  w.list = reinterpret_cast<int32_t*>(p);
+  p += align256(sizeof(int32_t) * 2 * (size_t)n_edges);
+  w.ctl = reinterpret_cast<int*>(p);
   return w;
 }
 
@@ -414,7 +629,15 @@ int queue_system(const float* Twc, const float* Xs, const float* Cs, int64_t n_p
     S3_LAUNCH_CHECK();
   }
   k_assemble<<<(unsigned)s3::cdiv((int64_t)n * n + n, kThreads), kThreads, 0, st>>>(
-      w.esum, ii, jj, n_edges, num_fix, n, w.H, w.b, state);
+      w.esum, ii, jj, w.off, w.list, num_fix, n, w.H, w.b, state);
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}
+
+// The incident-edge CSR of the (constant) edge set, once per solve.
+int queue_csr(const int32_t* ii, const int32_t* jj, int n_edges, int num_fix, int n, const Ws& w,
+              hipStream_t st) {
+  k_edge_csr<<<1, kCsrThreads, 0, st>>>(ii, jj, n_edges, num_fix, n / 7, w.off, w.list);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }
@@ -426,7 +649,9 @@ extern "C" size_t s3g_workspace_bytes(int n_poses, int n_edges, int64_t n_points
   const size_t n = 7 * (size_t)(n_poses > num_fix ? n_poses - num_fix : 0);
   return align256(sizeof(float) * (size_t)n_edges * S * NA) +
          align256(sizeof(double) * (size_t)n_edges * NA) + align256(sizeof(double) * n * n) +
-         align256(sizeof(double) * n) + align256(sizeof(double) * 4);
+         align256(sizeof(double) * n) + align256(sizeof(double) * 4) +
+         align256(sizeof(int32_t) * (n / 7 + 1)) + align256(sizeof(int32_t) * 2 * (size_t)n_edges) +
+         align256(sizeof(int) * 4);
 }
 
 extern "C" int s3g_ray_system(const float* Twc, int n_poses, const float* Xs, const float* Cs,
@@ -442,6 +667,7 @@ extern "C" int s3g_ray_system(const float* Twc, int n_poses, const float* Xs, co
   w.H = H;
   w.b = b;
   const int n = 7 * (n_poses - num_fix);
+  if (int r = queue_csr(ii, jj, n_edges, num_fix, n, w, st)) return r;
   return queue_system(Twc, Xs, Cs, n_points, ii, jj, n_edges, idx_ii2jj, valid_match, Q,
                       sigma_ray, sigma_dist, C_thresh, Q_thresh, num_fix, n, w, nullptr, st);
 }
@@ -456,13 +682,34 @@ int solve(float* Twc, int n_poses, const float* Xs, const float* Cs, int64_t n_p
   const int n = 7 * (n_poses - num_fix);
   S3_HIP(hipMemsetAsync(w.state, 0, sizeof(double) * 4, st));
   S3_HIP(hipMemsetAsync(dx, 0, sizeof(float) * n, st));
+  if (int r = queue_csr(ii, jj, n_edges, num_fix, n, w, st)) return r;
   for (int it = 0; it < max_iter; ++it) {
     if (int r = queue_system(Twc, Xs, Cs, n_points, ii, jj, n_edges, idx_ii2jj, valid_match, Q,
                              sigma_a, sigma_b, C_thresh, Q_thresh, num_fix, n, w, w.state, st,
                              cal))
       return r;
-    k_chol_solve<<<1, kThreads, 0, st>>>(w.H, w.b, n, dx, w.state);
-    S3_LAUNCH_CHECK();
+    if (n <= kSmallChol) {
+      k_chol_solve<<<1, kThreads, 0, st>>>(w.H, w.b, n, dx, w.state);
+      S3_LAUNCH_CHECK();
+    } else {
+      S3_HIP(hipMemsetAsync(w.ctl, 0, sizeof(int), st));
+      for (int k0 = 0; k0 < n; k0 += kNB) {
+        k_potrf_diag<<<1, kThreads, 0, st>>>(w.H, n, k0, w.ctl, w.state);
+        S3_LAUNCH_CHECK();
+        const int rest = n - k0 - kNB;
+        if (rest > 0) {
+          k_trsm_panel<<<(unsigned)s3::cdiv(rest, kThreads), kThreads, 0, st>>>(w.H, n, k0, w.ctl,
+                                                                               w.state);
+          S3_LAUNCH_CHECK();
+          const int T = (int)s3::cdiv(rest, kNB);
+          k_syrk_trailing<<<(unsigned)(T * (T + 1) / 2), kThreads, 0, st>>>(w.H, n, k0, w.ctl,
+                                                                            w.state);
+          S3_LAUNCH_CHECK();
+        }
+      }
+      k_chol_subst<<<1, kThreads, 0, st>>>(w.H, w.b, n, dx, w.ctl, w.state);
+      S3_LAUNCH_CHECK();
+    }
     k_retr<<<1, kThreads, 0, st>>>(Twc, n_poses, num_fix, dx, delta_thresh, w.state);
     S3_LAUNCH_CHECK();
   }
@@ -520,6 +767,7 @@ extern "C" int s3g_calib_system(const float* Twc, int n_poses, const float* Xs, 
   CalibArgs cal;
   cal.K = K; cal.height = height; cal.width = width; cal.pixel_border = pixel_border;
   cal.z_eps = z_eps;
+  if (int r = queue_csr(ii, jj, n_edges, num_fix, n, w, st)) return r;
   return queue_system(Twc, Xs, Cs, n_points, ii, jj, n_edges, idx_ii2jj, valid_match, Q,
                       sigma_pixel, sigma_depth, C_thresh, Q_thresh, num_fix, n, w, nullptr, st,
                       cal);

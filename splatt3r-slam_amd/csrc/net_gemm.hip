@@ -9,6 +9,15 @@
 // every ds_read_b128 lane group of the A/B fragment reads hits 16 distinct
 // 16-B slots of the 256-B bank row (conflict-free, guide §2/T2).  The tile
 // grid is remapped so that each XCD gets a contiguous run of tiles.
+//
+// In-workgroup split-K (KG > 1): a workgroup holds KG groups of NWM x NWN
+// waves on the same output tile; group kg consumes the K tiles
+// kt = kg, kg + KG, ... through its own LDS ring, all groups step together
+// (one barrier per K step), and the KG partial tiles are summed through LDS
+// in group order before one epilogue.  At M = 768 (one image) the tile grid
+// alone leaves one 4-wave workgroup per CU waiting on its DMA; KG groups give
+// each SIMD KG waves to overlap load latency with MFMA without the fp32
+// workspace round trip of a split-K launch.
 #include "common.hpp"
 #include "s3n.h"
 
@@ -65,6 +74,20 @@ template <int BK>
 __device__ __forceinline__ int swz(int row, int kc) {
   if constexpr (BK == 64) return kc ^ ((row >> 1) & 7);   // 2 rows per 256-B bank row
   else return kc ^ (row & 15);                            // 1 row per 256-B bank row
+}
+
+// fp16 range guard: activations stored as fp16 saturate at +-65504 instead
+// of becoming inf (real checkpoints may produce larger activations than the
+// portable-PRNG weights), and the event is recorded for the host
+// (s3n_f16_saturations).  The flag store carries a lane-dependent value.
+__device__ uint32_t g_f16_sat;
+
+__device__ __forceinline__ f16 sat_f16(float v) {
+  if (!(fabsf(v) <= 65504.0f)) {
+    g_f16_sat = 1u + (threadIdx.x & 63);
+    if (!isnan(v)) v = copysignf(65504.0f, v);
+  }
+  return (f16)v;
 }
 
 __device__ __forceinline__ float gelu(float x) {
@@ -145,9 +168,9 @@ __device__ __forceinline__ void store_out(const GemmP& p, int g, int row, int co
   void* C = p.C[g];
   f16* C2 = p.C2[g];
   const int64_t off = out_offset(p, row, col);
-  if (p.c_f16) reinterpret_cast<f16*>(C)[off] = (f16)v;
+  if (p.c_f16) reinterpret_cast<f16*>(C)[off] = sat_f16(v);
   else reinterpret_cast<float*>(C)[off] = v;
-  if (C2) C2[(int64_t)row * p.ldc2 + col] = (f16)v;
+  if (C2) C2[(int64_t)row * p.ldc2 + col] = sat_f16(v);
 }
 
 __device__ __forceinline__ float act_fn(const GemmP& p, float v) {
@@ -222,9 +245,9 @@ __device__ __forceinline__ void epilogue_block(const GemmP& p, int g, int row0, 
     for (int r = 0; r < 16; ++r) {
       if (acc_row(r) > rmax) continue;
       const int64_t e = o + (int64_t)acc_row(r) * p.ldc;
-      if (p.c_f16) reinterpret_cast<f16*>(p.C[g])[e] = (f16)x[r];
+      if (p.c_f16) reinterpret_cast<f16*>(p.C[g])[e] = sat_f16(x[r]);
       else reinterpret_cast<float*>(p.C[g])[e] = x[r];
-      if (C2) C2[o2 + (int64_t)acc_row(r) * p.ldc2] = (f16)x[r];
+      if (C2) C2[o2 + (int64_t)acc_row(r) * p.ldc2] = sat_f16(x[r]);
     }
   } else {
     for (int r = 0; r < 16; ++r)
@@ -262,7 +285,7 @@ __device__ __forceinline__ void store8_f32(float* q, const float (&v)[8]) {
 __device__ __forceinline__ void store8_f16(f16* q, const float (&v)[8]) {
   f16x8 h;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) h[e] = (f16)v[e];
+  for (int e = 0; e < 8; ++e) h[e] = sat_f16(v[e]);
   *reinterpret_cast<f16x8*>(q) = h;
 }
 
@@ -272,18 +295,19 @@ __device__ __forceinline__ void store8_f16(f16* q, const float (&v)[8]) {
 // vector accesses along rows (fully coalesced) instead of one 2-4 B access
 // per accumulator register.  The host enables it when every row stride and
 // base is 16-B aligned and 8-column chunks stay contiguous in the output.
-template <int BM, int BN, int NWM, int NWN, int FM, int FN, int LDT, int RING_BYTES>
+template <int BM, int BN, int NWM, int NWN, int FM, int FN, int LDT, int RING_BYTES, int KG = 1>
 __device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int n0,
                                              f32x16 (&acc)[FM][FN], float* stage) {
-  constexpr int WM = BM / NWM, WN = BN / NWN, NT = 64 * NWM * NWN;
+  constexpr int WM = BM / NWM, WN = BN / NWN, NT = 64 * NWM * NWN * KG;
   constexpr int CPR = BN / 8;                 // 8-column chunks per tile row
-  constexpr int NCH = BM * CPR / NT;          // chunks per thread
-  static_assert(NCH * NT == BM * CPR, "chunks must split over the threads");
+  constexpr int NCH = (BM * CPR + NT - 1) / NT;   // chunks per thread
+  constexpr int SLICE = BM * LDT;             // one K-group's partial tile (floats)
   // small tiles: the chunk operands (bias, fp32 residual, RoPE position) are
   // loaded before the LDS staging so their latency overlaps it
   constexpr bool kPre = NCH <= 4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / NWN, wn = wave % NWN;
+  const int kg = wave / (NWM * NWN), wq = wave % (NWM * NWN);
+  const int wm = wq / NWN, wn = wq % NWN;
   const float* __restrict__ bias = p.bias[g];
   const void* R1 = p.R1[g];
   const void* R2 = p.R2[g];
@@ -296,7 +320,7 @@ __device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int 
   if constexpr (kPre) {
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
-      const int c = tid + k * NT, rl = c / CPR, cl = (c % CPR) * 8;
+      const int c = min(tid + k * NT, BM * CPR - 1), rl = c / CPR, cl = (c % CPR) * 8;
       const int row = min(m0 + rl, p.M - 1), col = min(n0 + cl, p.N - 8);
       if (bias && !split) load8(bias + col, pb[k]);
       if (R1 && !split) load8_res(R1, p.r1_f16, (int64_t)row * p.ldr1 + col, pr[k]);
@@ -304,18 +328,38 @@ __device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int 
     }
   }
   __syncthreads();   // every wave is done with the K loop's LDS reads
+  // each K-group stages its partial tile in its own slice
+  float* mine = stage + kg * SLICE;
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        stage[(wm * WM + fm * 32 + acc_row(r) + 4 * (lane >> 5)) * LDT + wn * WN + fn * 32 +
-              (lane & 31)] = acc[fm][fn][r];
+        mine[(wm * WM + fm * 32 + acc_row(r) + 4 * (lane >> 5)) * LDT + wn * WN + fn * 32 +
+             (lane & 31)] = acc[fm][fn][r];
   __syncthreads();
+  if constexpr (KG > 1) {
+    // sum the K-groups' partials in group order into slice 0 (fixed order:
+    // the result does not depend on scheduling)
+    for (int c = tid; c < BM * CPR; c += NT) {
+      const int rl = c / CPR, cl = (c % CPR) * 8;
+      float v[8], t[8];
+      load8(stage + rl * LDT + cl, v);
+#pragma unroll
+      for (int q = 1; q < KG; ++q) {
+        load8(stage + q * SLICE + rl * LDT + cl, t);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += t[e];
+      }
+      store8_f32(stage + rl * LDT + cl, v);
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = tid + k * NT;
+    if (c >= BM * CPR) continue;
     const int rl = c / CPR, cl = (c % CPR) * 8;
     const int row = m0 + rl, col = n0 + cl;
     if (row >= p.M || col >= p.N) continue;
@@ -505,11 +549,11 @@ constexpr int lds_waves_per_simd(int BM, int BN, int NW, int S, int BK) {
   return w < 1 ? 1 : (w > 8 ? 8 : w);
 }
 
-template <int BM, int BN, int NWM, int NWN, int AMODE, int kStages, int BK>
-__global__ void __launch_bounds__(64 * NWM * NWN,
-                                  lds_waves_per_simd(BM, BN, NWM * NWN, kStages, BK))
+template <int BM, int BN, int NWM, int NWN, int AMODE, int kStages, int BK, int KG = 1>
+__global__ void __launch_bounds__(64 * NWM * NWN * KG,
+                                  lds_waves_per_simd(BM, BN, NWM * NWN * KG, kStages * KG, BK))
 k_gemm(GemmP p) {
-  constexpr int NW = NWM * NWN;
+  constexpr int NW = NWM * NWN;   // waves of one K-group
   constexpr int WM = BM / NWM, WN = BN / NWN;
   constexpr int FM = WM / 32, FN = WN / 32;
   // One LDS-DMA wave instruction moves 64 lanes x 16 B = RPI tile rows of
@@ -522,7 +566,7 @@ k_gemm(GemmP p) {
   static_assert(WM % 32 == 0 && WN % 32 == 0, "32x32 accumulator blocks");
   constexpr int PERW = AW + BW;
   constexpr int STAGE = (BM + BN) * BK;
-  __shared__ __attribute__((aligned(1024))) f16 smem[kStages * STAGE];
+  __shared__ __attribute__((aligned(1024))) f16 smem[KG * kStages * STAGE];
 
   const int g = blockIdx.z;
   const int nwg = p.tiles_m * p.tiles_n;
@@ -533,7 +577,9 @@ k_gemm(GemmP p) {
   const int tn = p.col_major ? tile / p.tiles_m : tile % p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = wave_all / NW;            // K-group of this wave
+  const int wave = wave_all % NW;          // wave within its K-group
   const int wm = wave / NWN, wn = wave % NWN;
   const int M = p.M, N = p.N, K = p.K;
   const f16* __restrict__ A = p.A[g];
@@ -571,7 +617,7 @@ k_gemm(GemmP p) {
       a_img[j] = (int64_t)b * p.cH * p.cW * p.cC;
       a_iy0[j] = oy * p.st - p.pad;
       a_ix0[j] = ox * p.st - p.pad;
-      const int k = kt_begin * BK + a_kc[j] * 8, tap = k / p.cC;
+      const int k = (kt_begin + kg) * BK + a_kc[j] * 8, tap = k / p.cC;
       c_ci[j] = k - tap * p.cC;
       c_ky[j] = tap / p.ks;
       c_kx[j] = tap - c_ky[j] * p.ks;
@@ -598,8 +644,9 @@ k_gemm(GemmP p) {
 
   // Issue the LDS-DMA loads of K tile kt into stage st (tiles are issued in
   // order kt = 0, 1, 2, ...: the conv state advances one tile per call).
+  f16* const ring = smem + kg * kStages * STAGE;   // this K-group's stages
   auto issue = [&](int kt, int st) {
-    f16* As = smem + st * STAGE;
+    f16* As = ring + st * STAGE;
     f16* Bs = As + BM * BK;
     const int k0 = kt * BK;
     const bool tail = k_tail && (k0 + BK > K);   // wave-uniform
@@ -616,7 +663,7 @@ k_gemm(GemmP p) {
         if (a_ok[j] && !(tail && k0 + a_kc[j] * 8 >= K) && iy >= 0 && iy < p.cH && ix >= 0 &&
             ix < p.cW)
           off = (uint32_t)((a_img[j] + ((int64_t)iy * p.cW + ix) * p.cC + c_ci[j]) * 2);
-        c_ci[j] += BK;
+        c_ci[j] += BK * KG;
         while (c_ci[j] >= p.cC) {
           c_ci[j] -= p.cC;
           if (++c_kx[j] == p.ks) { c_kx[j] = 0; ++c_ky[j]; }
@@ -640,21 +687,26 @@ k_gemm(GemmP p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  // kStages-deep ring: tiles kt+1 .. kt+kStages-2 stay in flight while
-  // tile kt is consumed; one raw barrier per K tile.
+  // kStages-deep ring per K-group: tiles kt+1 .. kt+kStages-2 stay in
+  // flight while tile kt is consumed; one raw barrier per K step.  K-group
+  // kg owns the workgroup's K tiles kg, kg + KG, ...; every group runs IT
+  // steps (the largest count) so the barriers pair up.
   constexpr int AHEAD = kStages - 1;
-  const int KT = (p.debug & 8) ? 0 : kt_end - kt_begin;   // this workgroup's K tiles
+  const int KT_wg = (p.debug & 8) ? 0 : kt_end - kt_begin;   // this workgroup's K tiles
+  const int KT = KT_wg > kg ? (KT_wg - kg + KG - 1) / KG : 0;  // this K-group's
+  const int IT = (KT_wg + KG - 1) / KG;
 #pragma unroll
   for (int i = 0; i < AHEAD; ++i)
-    if (i < KT) issue(kt_begin + i, i);
-  for (int kt = 0; kt < KT; ++kt) {
+    if (i < KT) issue(kt_begin + kg + i * KG, i);
+  for (int kt = 0; kt < IT; ++kt) {
     // Tile kt has landed once at most (tiles issued after it) x PERW DMA
     // instructions of this wave are still outstanding.
-    wait_tiles<PERW, AHEAD - 1>(KT - 1 - kt);
+    if (kt < KT) wait_tiles<PERW, AHEAD - 1>(KT - 1 - kt);
     // Everyone's DMA for tile kt is visible, and everyone finished reading
     // the stage that tile kt+AHEAD overwrites (read during iteration kt-1).
     __builtin_amdgcn_s_barrier();
-    const f16* As = smem + (kt % kStages) * STAGE;
+    if (kt >= KT) continue;
+    const f16* As = ring + (kt % kStages) * STAGE;
     const f16* Bs = As + BM * BK;
     // All fragments of this K tile first (their LDS latency overlaps the
     // next tile's DMA issue below), then the MFMA chain.
@@ -673,7 +725,7 @@ k_gemm(GemmP p) {
         bf[ks][fn] = *reinterpret_cast<const f16x8*>(Bs + row * BK + swz<BK>(row, kc) * 8);
       }
     }
-    if (kt + AHEAD < KT) issue(kt_begin + kt + AHEAD, (kt + AHEAD) % kStages);
+    if (kt + AHEAD < KT) issue(kt_begin + kg + (kt + AHEAD) * KG, (kt + AHEAD) % kStages);
     if (p.debug & 1) continue;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
@@ -694,16 +746,46 @@ k_gemm(GemmP p) {
 
   // ---- epilogue ----
   if (p.debug & 4) return;
-  // the LDS-staged vector epilogue where the fp32 tile fits the ring
+  // the LDS-staged vector epilogue where the fp32 tile fits the ring (one
+  // partial-tile slice per K-group, summed in group order inside)
   constexpr bool kVecFits = BM * BN * 4 <= kStages * STAGE * 2;
   if constexpr (kVecFits) {
     if (p.vec_epi) {
       // row pitch BN + 4 floats where it fits (rows 16 B apart in the banks)
       constexpr int LDT = BM * (BN + 4) * 4 <= kStages * STAGE * 2 ? BN + 4 : BN;
-      epilogue_vec<BM, BN, NWM, NWN, FM, FN, LDT, kStages * STAGE * 2>(
+      epilogue_vec<BM, BN, NWM, NWN, FM, FN, LDT, KG * kStages * STAGE * 2, KG>(
           p, g, m0, n0, acc, reinterpret_cast<float*>(smem));
       return;
     }
+  }
+  if constexpr (KG > 1) {
+    // register epilogue: groups 1.. hand their accumulators to group 0
+    // through LDS (lane-contiguous), group 0 adds them in group order
+    static_assert((KG - 1) * BM * BN * 4 <= KG * kStages * STAGE * 2, "K-group partials in LDS");
+    float* part = reinterpret_cast<float*>(smem);
+    __syncthreads();
+    if (kg > 0) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            part[((((kg - 1) * NW + wave) * FM + fm) * FN + fn) * 1024 + r * 64 + lane] =
+                acc[fm][fn][r];
+    }
+    __syncthreads();
+    if (kg > 0) return;
+#pragma unroll
+    for (int q = 1; q < KG; ++q)
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            acc[fm][fn][r] += part[((((q - 1) * NW + wave) * FM + fm) * FN + fn) * 1024 +
+                                   r * 64 + lane];
   }
   epilogue_regs<BM, BN, NWM, NWN, FM, FN>(p, g, m0, n0, acc);
 }
@@ -735,13 +817,14 @@ __global__ void __launch_bounds__(kThreads) k_splitk_reduce(GemmP p) {
   }
 }
 
-template <int BM, int BN, int S, int NWM = 2, int NWN = 2, int BK = 64>
+template <int BM, int BN, int S, int NWM = 2, int NWN = 2, int BK = 64, int KG = 1>
 int launch(const GemmP& p, hipStream_t st) {
   S3_REQUIRE(!p.tail_w[0] || p.N == BN,
              "s3n_gemm: the fused tail needs N == the tile width (%d, N = %d)", BN, p.N);
   S3_REQUIRE(!p.tail_w[0] || BM * BN * 4 <= S * (BM + BN) * BK * 2,
              "s3n_gemm: the fused tail needs a tile whose fp32 image fits its LDS ring");
-  constexpr int NT = 64 * NWM * NWN;
+  S3_REQUIRE(KG == 1 || !p.tail_w[0], "s3n_gemm: the fused tail runs with one K-group");
+  constexpr int NT = 64 * NWM * NWN * KG;
   GemmP q = p;
   q.tiles_m = (p.M + BM - 1) / BM;
   q.tiles_n = (p.N + BN - 1) / BN;
@@ -754,11 +837,11 @@ int launch(const GemmP& p, hipStream_t st) {
   q.col_major = (int64_t)p.N * p.K > a_bytes;
   dim3 grid(q.tiles_m * q.tiles_n, q.split_k, p.groups);
   if (p.a_mode == S3N_A_DENSE)
-    k_gemm<BM, BN, NWM, NWN, kDense, S, BK><<<grid, NT, 0, st>>>(q);
+    k_gemm<BM, BN, NWM, NWN, kDense, S, BK, KG><<<grid, NT, 0, st>>>(q);
   else if (p.relu_in)
-    k_gemm<BM, BN, NWM, NWN, kConvRelu, S, BK><<<grid, NT, 0, st>>>(q);
+    k_gemm<BM, BN, NWM, NWN, kConvRelu, S, BK, KG><<<grid, NT, 0, st>>>(q);
   else
-    k_gemm<BM, BN, NWM, NWN, kConv, S, BK><<<grid, NT, 0, st>>>(q);
+    k_gemm<BM, BN, NWM, NWN, kConv, S, BK, KG><<<grid, NT, 0, st>>>(q);
   S3_LAUNCH_CHECK();
   if (q.split_k > 1) {
     if (p.N % 4 == 0) {
@@ -777,6 +860,20 @@ int launch(const GemmP& p, hipStream_t st) {
 }  // namespace
 
 static int g_gemm_debug = 0;
+
+int s3n_ln_f16_saturations(int reset);   // net_ops.hip
+
+extern "C" int s3n_f16_saturations(int reset) {
+  uint32_t v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_f16_sat), sizeof(v)) != hipSuccess) return -1;
+  if (reset && v) {
+    const uint32_t z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_f16_sat), &z, sizeof(z)) != hipSuccess) return -1;
+  }
+  const int l = s3n_ln_f16_saturations(reset);
+  if (l < 0) return -1;
+  return (v ? 1 : 0) + l;
+}
 extern "C" void s3n_gemm_set_debug(int flags) { g_gemm_debug = flags; }
 
 extern "C" size_t s3n_gemm_workspace_bytes(const s3n_gemm_args* a) {
@@ -888,6 +985,13 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   // 256x256 output tiles, 8 waves of 128x64 (half the operand bytes per MFMA
   // of 128x128; only 2 stages fit, so it wins only on some large shapes)
   if (a->tile == 14) return launch<256, 256, 2, 2, 4>(p, st);
+  // in-workgroup split-K: KG groups of 4 waves on one output tile
+  if (a->tile == 15) return launch<64, 64, 3, 2, 2, 64, 2>(p, st);
+  if (a->tile == 16) return launch<64, 64, 2, 2, 2, 64, 4>(p, st);
+  if (a->tile == 17) return launch<64, 128, 2, 2, 2, 64, 2>(p, st);
+  if (a->tile == 18) return launch<128, 128, 2, 2, 2, 64, 2>(p, st);
+  if (a->tile == 19) return launch<64, 64, 2, 2, 2, 128, 2>(p, st);
+  if (a->tile == 20) return launch<64, 128, 2, 2, 2, 64, 3>(p, st);
   // the fused tail needs one column tile per row block
   if (tail) {
     S3_REQUIRE(a->N == 64 || a->N == 128, "s3n_gemm: the fused tail needs N of 64 or 128");

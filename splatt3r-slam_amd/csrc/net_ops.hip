@@ -27,6 +27,17 @@ struct LnP {
   int64_t ld32;
 };
 
+// fp16 range guard of the LayerNorm fp16 outputs (see net_gemm.hip sat_f16)
+__device__ uint32_t g_ln_f16_sat;
+
+__device__ __forceinline__ _Float16 ln_sat_f16(float v) {
+  if (!(fabsf(v) <= 65504.0f)) {
+    g_ln_f16_sat = 1u + (threadIdx.x & 63);
+    if (!isnan(v)) v = copysignf(65504.0f, v);
+  }
+  return (_Float16)v;
+}
+
 template <int VPL>  // float4 vectors per lane
 __global__ void __launch_bounds__(kThreads) k_layernorm(LnP p) {
   const int g = blockIdx.y;
@@ -78,7 +89,7 @@ __global__ void __launch_bounds__(kThreads) k_layernorm(LnP p) {
     if (o32) *reinterpret_cast<f32x4*>(o32 + (int64_t)row * p.ld32 + c) = y;
     if (o16) {
       typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-      const f16x4 h = {(f16)y[0], (f16)y[1], (f16)y[2], (f16)y[3]};
+      const f16x4 h = {ln_sat_f16(y[0]), ln_sat_f16(y[1]), ln_sat_f16(y[2]), ln_sat_f16(y[3])};
       *reinterpret_cast<f16x4*>(o16 + (int64_t)row * p.ld16 + c) = h;
     }
   }
@@ -312,3 +323,13 @@ int s3n_cast_f16(const float* in, int64_t ld_in, void* out, int64_t ld_out, int6
 }
 
 }  // extern "C"
+
+int s3n_ln_f16_saturations(int reset) {
+  uint32_t v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ln_f16_sat), sizeof(v)) != hipSuccess) return -1;
+  if (reset && v) {
+    const uint32_t z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ln_f16_sat), &z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return v ? 1 : 0;
+}

@@ -43,7 +43,7 @@ class Backend:
         self.retrieval = retrieval if retrieval is not None else RetrievalDatabase(
             synthetic_retrieval_weights(self.device), self.device)
         self.stats = dict(optimized=0, edges=0, reloc_attempts=0, reloc_success=0,
-                          retrieval_candidates=0)
+                          retrieval_candidates=0, last_reloc_candidates=[])
         self._q = None
         self._thread = None
         self._stream = None
@@ -87,6 +87,7 @@ class Backend:
         kf_idx = list(self.retrieval.update(frame, add_after_query=False,
                                             k=config["retrieval"]["k"],
                                             min_thresh=config["retrieval"]["min_thresh"]))
+        self.stats["last_reloc_candidates"] = list(kf_idx)
         success = False
         if kf_idx:
             self.keyframes.append(frame)

@@ -538,13 +538,31 @@ class Splatt3RNet:
         return self._pair[key]
 
     # ------------------------------------------------- reference API -----
+    @staticmethod
+    def _is_portrait(true_shape) -> bool:
+        """All images of the batch portrait (true_shape rows (h, w), h > w);
+        mixed batches are not supported (the reference splits them)."""
+        if true_shape is None:
+            return False
+        ts = torch.as_tensor(true_shape).reshape(-1, 2)
+        portrait = ts[:, 1] < ts[:, 0]
+        if bool(portrait.any()) and not bool(portrait.all()):
+            raise NotImplementedError("mixed portrait/landscape batch")
+        return bool(portrait.all())
+
     def _encode_image(self, image: torch.Tensor, true_shape=None):
+        """ManyAR_PatchEmbed + encoder (dust3r/patch_embed.py:42-70,
+        model.py:121-136).  The image tensor is landscape (W >= H, asserted
+        like the reference); a portrait true_shape means the tensor holds the
+        transposed image, which is encoded on the transposed token grid."""
         B, C, H, W = image.shape
-        if W < H:
-            raise NotImplementedError("portrait input: transpose to landscape first "
-                                      "(ManyAR_PatchEmbed asserts W >= H)")
+        assert W >= H, f"img should be in landscape mode, but got W={W} H={H}"
+        img = image.to(device=self.device, dtype=F32)
+        if self._is_portrait(true_shape):
+            img = img.transpose(-1, -2)
+            H, W = W, H
         ep = self.encoder_plan(B, H, W)
-        feat, pos = self._timed("encoder", ep, image.to(device=self.device, dtype=F32))
+        feat, pos = self._timed("encoder", ep, img)
         return feat.clone(), pos.clone(), None
 
     def infer_pair(self, feat1, pos1, feat2, pos2, hw, tag=None):
@@ -592,12 +610,19 @@ class Splatt3RNet:
         return self.pair_plan(Bp, H, W, keep_tokens=True)
 
     def _downstream_head(self, head_num, decout, img_shape):
-        """GaussianHead.forward for one head on the given 13 token tensors."""
+        """GaussianHead.forward for one head on the given 13 token tensors,
+        through _LandscapeWrapperYes (utils/misc.py:80-116): a portrait
+        true_shape runs the head on the transposed grid and returns the
+        outputs transposed back (swapaxes(1, 2))."""
         cfg = self.cfg
+        portrait = False
         if torch.is_tensor(img_shape):
             H, W = int(img_shape.min()), int(img_shape.max())
+            portrait = self._is_portrait(img_shape)
         else:
             H, W = int(img_shape[0]), int(img_shape[1])
+        if portrait:
+            H, W = W, H
         Bp, N, _ = decout[-1].shape
         pp = self.pair_plan(Bp, H, W, keep_tokens=True)
         E, D = cfg.enc_dim, cfg.dec_dim
@@ -612,4 +637,6 @@ class Splatt3RNet:
             ops.cast_f16(decout[hk].reshape(M, D).float().contiguous(), pp.hook16[hk][b], rows=M,
                          cols=D, ld_in=D, ld_out=D)(st)
         pp.head_plan.run()
+        if portrait:
+            return {k: v.swapaxes(1, 2).contiguous() for k, v in pp.res[b].items()}
         return {k: v.clone() for k, v in pp.res[b].items()}

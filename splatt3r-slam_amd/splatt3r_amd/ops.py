@@ -75,7 +75,19 @@ _lib.register({
                                                 ctypes.c_int] + [P] * 10 + [P]),
     "s3n_prng_fill": (ctypes.c_int, [P, I64, ctypes.c_uint64, ctypes.c_float, ctypes.c_float, P]),
     "s3n_cast_f16": (ctypes.c_int, [P, I64, P, I64, I64, ctypes.c_int, P]),
+    "s3n_f16_saturations": (ctypes.c_int, [ctypes.c_int]),
 })
+
+
+def f16_saturations(reset: bool = False) -> int:
+    """How many fp16-store guards fired (GEMM epilogue, LayerNorm) since the
+    last reset: > 0 means some activation exceeded the fp16 range (+-65504)
+    and was saturated instead of becoming inf.  Synchronises the device."""
+    torch.cuda.synchronize()
+    n = _lib.lib().s3n_f16_saturations(int(bool(reset)))
+    if n < 0:
+        raise RuntimeError("s3n_f16_saturations: HIP error")
+    return n
 
 ACT = {"none": 0, "gelu": 1, "relu": 2}
 
@@ -148,7 +160,11 @@ _TUNE_CACHE: dict = {}
 TUNE_LOG = os.environ.get("S3_GEMM_TUNE_LOG", "0") == "1"
 _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128, 128),
                 6: (64, 64), 8: (64, 128), 9: (64, 64), 10: (64, 64), 11: (64, 128),
-                12: (128, 128), 14: (256, 256)}
+                12: (128, 128), 14: (256, 256),
+                # in-workgroup K-groups (net_gemm.hip KG > 1)
+                15: (64, 64), 16: (64, 64), 17: (64, 128), 18: (128, 128), 19: (64, 64),
+                20: (64, 128)}
+_TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14}   # the fused tail runs with one K-group
 
 
 def _tune_key(a):
@@ -163,7 +179,7 @@ def _tune_candidates(a, split_ok):
     kt = -(-a.K // 64)
     out = []
     for tile, (bm, bn) in _TILE_SHAPES.items():
-        if a.tail_n and bn != a.N:
+        if a.tail_n and (bn != a.N or tile not in _TAIL_OK):
             continue
         tiles = a.groups * -(-a.M // bm) * -(-a.N // bn)
         for sk in (1, 2, 3, 4, 6, 8):

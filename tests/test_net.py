@@ -164,6 +164,9 @@ def _full_size(parity, H, W_, name):
             rel = abs(s - float(g[f"res{ri}_{k}_sum"])) / float(g[f"res{ri}_{k}_abs"])
             parity(f"res{ri}_{k}_sum", rel=rel, tol=TOL["sum"])
             assert rel <= TOL["sum"], (ri, k, rel)
+    # no fp16 activation of the full network left the fp16 range
+    from splatt3r_amd import ops
+    assert ops.f16_saturations(reset=True) == 0
 
 
 @pytest.mark.gpu
@@ -279,3 +282,30 @@ def test_inference_mono_vs_reference_golden(parity):
     for k in ("means", "opacities", "sh", "scales"):
         _check(parity, f"mono_pred_{k}", f.gaussian_pred[k], g["res11_" + k], TOL["head"])
         _check(parity, f"mono_cross_{k}", f.gaussian_pred_cross[k], g["res21_" + k], TOL["head"])
+
+
+@pytest.mark.gpu
+def test_portrait_true_shape_vs_reference_golden(parity):
+    """A landscape image tensor with a portrait true_shape (the reference's
+    ManyAR_PatchEmbed transpose + _LandscapeWrapperYes heads): encoder
+    features, positions and both heads vs the reference golden; a portrait
+    tensor is rejected with the reference's assertion."""
+    from splatt3r_amd import weights as W
+    from splatt3r_amd.net import Splatt3RNet
+    g = np.load(os.path.join(GOLDEN, "net_small_portrait.npz"))
+    net = Splatt3RNet(W.SMALL, seed=1234, graphs=False)
+    shape = torch.from_numpy(g["true_shape"])
+    f1, p1, _ = net._encode_image(torch.from_numpy(g["img1"]).cuda(), shape)
+    f2, p2, _ = net._encode_image(torch.from_numpy(g["img2"]).cuda(), shape)
+    _check(parity, "portrait_feat1", f1, g["feat1"], TOL["tokens"])
+    np.testing.assert_array_equal(p1.cpu().numpy(), g["pos1"])
+    dec1, dec2 = net._decoder(f1, p1, f2, p2)
+    dec1, dec2 = list(dec1), list(dec2)
+    r1 = net._downstream_head(1, [t.float() for t in dec1], shape)
+    r2 = net._downstream_head(2, [t.float() for t in dec2], shape)
+    assert r1["pts3d"].shape == g["res1_pts3d"].shape == (1, 48, 64, 3)
+    for k in ("pts3d", "conf", "opacities", "means"):
+        _check(parity, f"portrait_res1_{k}", r1[k], g["res1_" + k], TOL["head"])
+        _check(parity, f"portrait_res2_{k}", r2[k], g["res2_" + k], TOL["head"])
+    with pytest.raises(AssertionError, match="landscape"):
+        net._encode_image(torch.zeros(1, 3, 64, 48, device="cuda"), None)

@@ -44,7 +44,13 @@ def test_gemm_dense_bias_residual(M, N, K, groups):
     (300, 200, 1000, 1, 1, 6), (130, 96, 2000, 2, 1, 7), (600, 256, 200, 1, 1, 8),
     (768, 1024, 1000, 1, 1, 9), (300, 200, 1000, 2, 3, 10), (130, 300, 968, 1, 2, 11),
     (700, 256, 2304, 2, 1, 12), (64, 64, 136, 1, 1, 9), (700, 256, 1000, 2, 2, 14),
-    (520, 300, 640, 1, 1, 14), (300, 500, 1000, 1, 3, 14)])
+    (520, 300, 640, 1, 1, 14), (300, 500, 1000, 1, 3, 14),
+    # in-workgroup K-groups (tiles 15-20), incl. K-tile counts not divisible
+    # by the group count, a single K tile, and global split-K on top
+    (768, 1024, 1024, 1, 1, 15), (768, 1024, 4096, 1, 1, 16), (300, 200, 1000, 2, 1, 16),
+    (768, 768, 768, 2, 1, 17), (700, 256, 2304, 1, 1, 18), (130, 300, 968, 1, 1, 19),
+    (768, 1024, 1088, 1, 1, 20), (64, 64, 64, 1, 1, 16), (520, 384, 640, 2, 2, 16),
+    (300, 256, 200, 1, 1, 20)])
 def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
     """Split-K partials + ordered reduce + the full epilogue (bias, GELU,
     fp32 residual, fp16 out + fp16 copy) for every tile shape."""
@@ -65,7 +71,9 @@ def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
 
 @pytest.mark.parametrize("split,tile,Cin", [(3, 1, 768), (9, 0, 768), (2, 3, 768), (1, 4, 768),
                                             (1, 5, 768), (1, 9, 768), (2, 10, 768), (1, 11, 96),
-                                            (1, 12, 768), (1, 9, 96), (2, 9, 136)])
+                                            (1, 12, 768), (1, 9, 96), (2, 9, 136), (1, 15, 768),
+                                            (1, 16, 96), (1, 17, 768), (2, 18, 256), (1, 19, 136),
+                                            (1, 20, 768)])
 def test_gemm_implicit_conv_split_k(split, tile, Cin):
     from splatt3r_amd import ops, _lib
     B, H, W, Cout, k, stride, pad = 1, 12, 16, 256, 3, 1, 1
@@ -340,7 +348,8 @@ def test_gaussian_postprocess_vs_torch():
         assert rel_err(out[k], v) < 1e-5, k
 
 
-@pytest.mark.parametrize("case", ["plain", "res16", "split", "rope", "convt", "tile3", "tile4"])
+@pytest.mark.parametrize("case", ["plain", "res16", "split", "rope", "convt", "tile3", "tile4",
+                                  "tile16", "tile17_rope", "tile20"])
 def test_gemm_vector_epilogue_matches_register_epilogue(case):
     """The LDS-staged 8-column epilogue and the per-register epilogue
     (s3n_gemm_set_debug(16)) apply the same operations in the same order:
@@ -369,6 +378,13 @@ def test_gemm_vector_epilogue_matches_register_epilogue(case):
         kw.update(tile=3, split_k=1)
     if case == "tile4":
         kw.update(tile=4, split_k=1)
+    if case in ("tile16", "tile20"):
+        kw.update(tile=int(case[4:]), split_k=1)
+    if case == "tile17_rope":
+        cos, sin = rope_tables(64, "cuda")
+        pos = [positions(3, 10, 10, "cuda").reshape(-1, 2) for _ in range(g)]
+        kw.update(rope=(cos, sin), rope_pos=pos, rope_ncols=256, act="none", tile=17)
+        out_dt = torch.float16
     if case == "convt":
         s, cout = 2, 96                                  # N = s*s*cout = 384
         kw.update(store=("convt", 15, 20, s, cout), act="none")
@@ -390,7 +406,7 @@ def test_gemm_vector_epilogue_matches_register_epilogue(case):
             L.s3n_gemm_set_debug(0)
         outs.append([c.clone() for c in C] + ([c.clone() for c in C2] if case != "convt" else []))
     for x, y in zip(*outs):
-        if case == "rope":   # the two paths may contract x*cos -/+ x'*sin differently
+        if case in ("rope", "tile17_rope"):   # the paths may contract x*cos -/+ x'*sin differently
             assert rel_err(y, x.float()) < 2e-3
         else:
             assert torch.equal(x, y)
@@ -421,3 +437,28 @@ def test_gemm_conv_fused_1x1_tail(tile, tn, store_c):
         assert rel_err(out[i], ref) < 2e-3, (i, rel_err(out[i], ref))
         if store_c:
             assert rel_err(C[i], y.permute(0, 2, 3, 1)) < 2e-3
+
+
+def test_gemm_and_layernorm_fp16_range_guard():
+    """fp16 activations saturate at +-65504 (not inf) and raise the device
+    flag s3n_f16_saturations reports; in-range outputs leave it clear."""
+    from splatt3r_amd import ops, _lib
+    ops.f16_saturations(reset=True)
+    M, N, K = 128, 128, 64
+    A = torch.full((M, K), 60.0, device="cuda", dtype=torch.float16)
+    W = torch.full((N, K), 60.0, device="cuda", dtype=torch.float16)   # dot = 230400
+    C = torch.empty(M, N, device="cuda", dtype=torch.float16)
+    ops.gemm([A], [W * 0.001], [C], M, N, K, lda=K)(_lib.stream())
+    assert ops.f16_saturations(reset=True) == 0
+    assert torch.isfinite(C).all()
+    ops.gemm([A], [W], [C], M, N, K, lda=K)(_lib.stream())
+    assert ops.f16_saturations(reset=True) == 1
+    assert float(C.float().max()) == 65504.0 and torch.isfinite(C).all()
+    assert ops.f16_saturations() == 0
+    x = torch.zeros(4, 256, device="cuda")
+    x[:, 0] = 1.0
+    g = torch.full((256,), 1e5, device="cuda")
+    o = torch.empty(4, 256, device="cuda", dtype=torch.float16)
+    ops.layernorm([x], [g], [torch.zeros(256, device="cuda")], rows=4, C=256, ldx=256,
+                  out16=[o], ld16=256)(_lib.stream())
+    assert ops.f16_saturations(reset=True) == 1 and torch.isfinite(o).all()

@@ -191,7 +191,9 @@ def _beat(rank, msg):
 
 
 def _gpu_shard_worker(rank, ws, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # static GEMM launch policy: the per-process tuner times candidates and
+    # may pick other tiles in another process (same math, other rounding)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), S3_GEMM_TUNE="0")
     import datetime
     _beat(rank, "init")
     dist.init_process_group("gloo", rank=rank, world_size=ws,
