@@ -18,9 +18,11 @@ Same function names, argument meaning and file bytes as the reference:
   of cv2; cv2's BGR swap followed by its BGR->RGB write is the identity).
 
 save_reconstruction's use_calib branch constrains points to their pixel
-rays first (evaluate.py:55-59); save_traj's `intrinsics` pose refinement
-(Intrinsics.refine_pose_with_calibration, dataloader) is not built and
-raises NotImplementedError.
+rays first (evaluate.py:55-59).  save_traj's `intrinsics` branch calls
+`intrinsics.refine_pose_with_calibration(keyframe)` (evaluate.py:42), a
+method the reference's Intrinsics class does not define
+(dataloader.py:277-317): the reference raises AttributeError there, and so
+does this one, with the same exception type.
 """
 from __future__ import annotations
 
@@ -44,8 +46,10 @@ def prepare_savedir(args, dataset):
 
 def as_SE3_data(T_WC) -> np.ndarray:
     """lietorch_utils.py:6-13: Sim3 [t, q, s] -> SE3 [t, q] as float32 rows."""
-    d = T_WC.data.detach().cpu().reshape(-1, 8) if hasattr(T_WC, "data") else T_WC
-    d = torch.as_tensor(d).reshape(-1, 8)
+    d = T_WC.data.detach().cpu() if hasattr(T_WC, "data") else torch.as_tensor(T_WC)
+    if d.shape[-1] == 7:          # already an SE3 [t, q]
+        return d.reshape(-1, 7).numpy().astype(np.float32)
+    d = d.reshape(-1, 8)
     return torch.cat([d[:, :3], d[:, 3:7]], -1).numpy().astype(np.float32)
 
 
@@ -55,14 +59,18 @@ def traj_line(t, pose7: np.ndarray) -> str:
 
 
 def save_traj(logdir, logfile, timestamps, frames, intrinsics: Optional[object] = None):
-    if intrinsics is not None:
-        raise NotImplementedError("calibrated pose refinement (use_calib) is not built")
+    if intrinsics is not None and not hasattr(intrinsics, "refine_pose_with_calibration"):
+        raise AttributeError(
+            "'Intrinsics' object has no attribute 'refine_pose_with_calibration' "
+            "(the reference's save_traj calls a method its Intrinsics does not define, "
+            "dataloader.py:277-317)")
     logdir = pathlib.Path(logdir)
     logdir.mkdir(exist_ok=True, parents=True)
     with open(logdir / logfile, "w") as f:
         for i in range(len(frames)):
             kf = frames[i]
-            f.write(traj_line(timestamps[kf.frame_id], as_SE3_data(kf.T_WC)[0]))
+            T = kf.T_WC if intrinsics is None else intrinsics.refine_pose_with_calibration(kf)
+            f.write(traj_line(timestamps[kf.frame_id], as_SE3_data(T)[0]))
 
 
 _PLY_HEADER = ("ply\nformat binary_little_endian 1.0\nelement vertex {n}\n"

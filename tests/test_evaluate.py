@@ -47,3 +47,20 @@ def test_traj_lines(tmp_path):
         assert ln == f"{ts[fr.frame_id]} {x} {y} {z} {qx} {qy} {qz} {qw}"
     vals = np.array([float(v) for v in lines[0].split()[1:]], np.float32)
     np.testing.assert_array_equal(vals, poses[0][0, :7].numpy())
+
+
+def test_traj_with_intrinsics_matches_reference_error(tmp_path):
+    """evaluate.py:42 calls Intrinsics.refine_pose_with_calibration, which the
+    reference's Intrinsics (dataloader.py:277-317) does not define: the
+    reference raises AttributeError for any intrinsics object; so do we, and
+    an object that does provide the method gets its pose written."""
+    import pytest
+    poses = torch.tensor([[0.1, -2.5, 3.0, 0.0, 0.0, 0.0, 1.0, 1.7]])
+    frames = [types.SimpleNamespace(frame_id=0, T_WC=types.SimpleNamespace(data=poses))]
+    with pytest.raises(AttributeError):
+        E.save_traj(tmp_path, "t.txt", [0.0], frames, intrinsics=types.SimpleNamespace(K=None))
+    refined = types.SimpleNamespace(data=torch.tensor([[1.0, 2.0, 3.0, 0.0, 0.0, 0.0, 1.0]]))
+    intr = types.SimpleNamespace(refine_pose_with_calibration=lambda kf: refined)
+    E.save_traj(tmp_path, "t.txt", [0.0], frames, intrinsics=intr)
+    vals = [float(v) for v in (tmp_path / "t.txt").read_text().split()[1:]]
+    assert vals == [1.0, 2.0, 3.0, 0.0, 0.0, 0.0, 1.0]
