@@ -1,18 +1,21 @@
 // Tile-binned Gaussian splat rasterizer (include/gsr.h), written for gfx950.
 //
-// Forward:  preprocess (1 lane / Gaussian) -> inclusive scan of tiles touched
-//           -> stable depth sort of the P Gaussians (32-bit keys) -> duplicate
-//           in depth order -> stable sort of the instances by tile id alone
-//           (tile_bits passes, 32-bit keys) -> tile ranges -> blend (one 256-lane workgroup per 16x16 tile,
-//           Gaussians staged through LDS in 256-record batches, block-wide
-//           early exit).
+// Forward:  preprocess (1 lane / Gaussian; per-workgroup reduction of the
+//           instance total and visible count fused in) -> stable depth sort
+//           of the P Gaussians (3 hand-written 11-bit LSD radix passes) ->
+//           tile binning: one stable counting pass over the instances by
+//           tile id, enumerated in depth order straight from the kept-tile
+//           masks (no instance key array, no second sort; tile ranges fall
+//           out of the scan) -> blend (one 256-lane workgroup per 16x16
+//           tile, Gaussians staged through LDS in 256-record batches,
+//           block-wide early exit).
 // Backward: per-tile back-to-front replay; per-Gaussian gradients are
 //           reduced across the wave with DPP/shuffles before one lane issues
 //           the global atomics (64x fewer atomics than one per pixel), then a
 //           per-Gaussian pass for the EWA / projection / SH chain rule.
 // Tile blocks are remapped so that each XCD (private L2) receives a
 // contiguous band of tiles: neighbouring tiles share most of their splats.
-#include <hipcub/hipcub.hpp>
+#include <algorithm>
 
 #include "common.hpp"
 #include "gsr.h"
@@ -38,6 +41,31 @@ struct Carver {
   }
 };
 
+// Filled by k_preprocess (one set of atomics per workgroup, spread over
+// kRedSlots 64-B slots so the atomics do not queue on one address) and read
+// back by gsr_preprocess: instance total (num_rendered) and the depth-key
+// range of the Gaussians that emit instances (it sets the number of depth
+// sort passes).
+constexpr int kRedSlots = 64;
+struct RedSlot {
+  unsigned long long total;  // instances (64-bit: no wrap)
+  uint32_t kmax;             // max depth key
+  uint32_t kmin_inv;         // ~min depth key (memset-0 start)
+  uint32_t pad[12];
+};
+struct Reduce {
+  RedSlot slot[kRedSlots];
+};
+
+// Hand-written stable LSD radix passes (see "sorting" below).
+constexpr int kMaxDigitBits = 9, kMaxBins = 1 << kMaxDigitBits;
+constexpr int kSortThreads = 512;
+constexpr int kSortPerLane = 8;
+constexpr int kSegItems = kSortThreads * kSortPerLane;  // 4096 items per segment
+
+constexpr int kDupRanks = 512;  // depth ranks per duplication wave
+inline int64_t nsegs(int64_t n) { return std::max<int64_t>(1, s3::cdiv(n, kSegItems)); }
+
 struct GeomState {
   float* depth;
   float4* rec0;  // x, y, conic.a, conic.b
@@ -45,60 +73,19 @@ struct GeomState {
   float* rgb;    // [P,3]
   float* cov3D;  // [P,6] (scale/rotation path)
   uint8_t* clamped;  // [P,3]
-  uint32_t* tiles;
   // duplication record per Gaussian: x = x0 | y0 << 16, y = rect w | h << 16,
   // z/w = kept-tile mask (bit (y - y0) * w + (x - x0)) for rects of 2..64
   // tiles; one 16-B gather serves the depth-ordered passes
   uint4* dup;
-  uint64_t* total;         // instances over all Gaussians (64-bit: no wrap)
-  void* scan_tmp;
-  size_t scan_bytes;
-  // depth-ordered duplication (gsr_render)
-  uint32_t* dkey;          // depth bits (visible) / ~0u, index order
-  uint32_t* dkey_sorted;
-  // sort values: Gaussian index | kept-tile count << 32, so the depth-ordered
-  // tile counts come out of the sort instead of a random gather
-  uint64_t* iota;
-  uint64_t* order;         // (index | count << 32) per depth rank (stable)
-  uint32_t* offsets_sorted;
-  void* dsort_tmp;
-  size_t dsort_bytes;
+  Reduce* red;
+  // depth sort ping-pong: keys = depth bits (visible) / ~0u; values = index
+  uint32_t* dkey[2];
+  uint32_t* dval[2];
+  uint32_t* dhist;  // [bins][segments]: digit counts -> exclusive offsets
+  uint32_t* dtot;   // [bins]
+  uint4* dup_sorted;  // dup records in depth order (k_order_gather)
+  uint32_t* cnt_seg;  // [P / kDupRanks]: instances per depth-rank segment -> offsets
 };
-
-// tiles touched per depth rank = high word of the depth-sorted value
-struct HighWord {
-  __host__ __device__ uint32_t operator()(uint64_t v) const { return (uint32_t)(v >> 32); }
-};
-typedef hipcub::TransformInputIterator<uint32_t, HighWord, const uint64_t*> TilesIt;
-
-// tiles touched per Gaussian, widened so the total cannot wrap
-struct Widen {
-  __host__ __device__ uint64_t operator()(uint32_t v) const { return (uint64_t)v; }
-};
-typedef hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t*> Tiles64It;
-
-size_t scan_temp_bytes(int64_t P) {
-  size_t bytes = 0, b2 = 0;
-  hipcub::DeviceReduce::Sum(nullptr, bytes, Tiles64It(nullptr, Widen()), (uint64_t*)nullptr,
-                            (int)P);
-  hipcub::DeviceScan::InclusiveSum(nullptr, b2, TilesIt(nullptr, HighWord()),
-                                   (uint32_t*)nullptr, (int)P);
-  return bytes > b2 ? bytes : b2;
-}
-
-size_t key32_sort_temp_bytes(int64_t n) {
-  size_t bytes = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                     (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-  return bytes;
-}
-
-size_t depth_sort_temp_bytes(int64_t n) {
-  size_t bytes = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                     (uint64_t*)nullptr, (uint64_t*)nullptr, (int)n);
-  return bytes;
-}
 
 // One layout routine serves both sizing (base == nullptr) and carving.
 GeomState carve_geom(void* base, int64_t P, size_t* total = nullptr) {
@@ -110,18 +97,16 @@ GeomState carve_geom(void* base, int64_t P, size_t* total = nullptr) {
   g.rgb = c.take<float>(P * 3);
   g.cov3D = c.take<float>(P * 6);
   g.clamped = c.take<uint8_t>(P * 3);
-  g.tiles = c.take<uint32_t>(P);
   g.dup = c.take<uint4>(P);
-  g.total = c.take<uint64_t>(1);
-  g.scan_bytes = scan_temp_bytes(P);
-  g.scan_tmp = c.take<char>(g.scan_bytes);
-  g.dkey = c.take<uint32_t>(P);
-  g.dkey_sorted = c.take<uint32_t>(P);
-  g.iota = c.take<uint64_t>(P);
-  g.order = c.take<uint64_t>(P);
-  g.offsets_sorted = c.take<uint32_t>(P);
-  g.dsort_bytes = depth_sort_temp_bytes(P);
-  g.dsort_tmp = c.take<char>(g.dsort_bytes);
+  g.red = c.take<Reduce>(1);
+  g.dkey[0] = c.take<uint32_t>(P);
+  g.dkey[1] = c.take<uint32_t>(P);
+  g.dval[0] = c.take<uint32_t>(P);
+  g.dval[1] = c.take<uint32_t>(P);
+  g.dhist = c.take<uint32_t>((size_t)kMaxBins * nsegs(P));
+  g.dtot = c.take<uint32_t>(kMaxBins);
+  g.dup_sorted = c.take<uint4>(P);
+  g.cnt_seg = c.take<uint32_t>(std::max<int64_t>(1, s3::cdiv(P, kDupRanks)));
   if (total) *total = c.off;
   return g;
 }
@@ -132,25 +117,21 @@ size_t geom_bytes(int64_t P) {
 }
 
 struct BinningState {
-  uint32_t* keys_unsorted;   // tile id per instance (depth order)
-  uint32_t* keys;
-  uint32_t* vals_unsorted;
-  uint32_t* vals;  // point_list: Gaussian index per sorted instance
-  void* sort_tmp;
-  size_t sort_bytes;
+  uint32_t* keys[2];  // tile id per instance (ping-pong)
+  uint32_t* vals[2];  // Gaussian index per instance (ping-pong)
+  uint32_t* hist;     // [bins][segments]
+  uint32_t* tot;      // [bins]
 };
-
-size_t sort_temp_bytes(int64_t R) { return key32_sort_temp_bytes(R); }
 
 BinningState carve_binning(void* base, int64_t R, size_t* total = nullptr) {
   Carver c{static_cast<char*>(base)};
   BinningState b;
-  b.keys_unsorted = c.take<uint32_t>(R);
-  b.keys = c.take<uint32_t>(R);
-  b.vals_unsorted = c.take<uint32_t>(R);
-  b.vals = c.take<uint32_t>(R);
-  b.sort_bytes = sort_temp_bytes(R);
-  b.sort_tmp = c.take<char>(b.sort_bytes);
+  b.keys[0] = c.take<uint32_t>(R);
+  b.keys[1] = c.take<uint32_t>(R);
+  b.vals[0] = c.take<uint32_t>(R);
+  b.vals[1] = c.take<uint32_t>(R);
+  b.hist = c.take<uint32_t>((size_t)kMaxBins * nsegs(R));
+  b.tot = c.take<uint32_t>(kMaxBins);
   if (total) *total = c.off;
   return b;
 }
@@ -181,9 +162,9 @@ size_t image_bytes(int H, int W) {
   return n;
 }
 
-int tile_bits(int tiles) {
+int bit_length(uint64_t v) {
   int b = 0;
-  while ((1u << b) <= (unsigned)tiles) ++b;
+  while (b < 64 && (v >> b) != 0) ++b;
   return b;
 }
 
@@ -204,26 +185,25 @@ struct Cam {
   bool prefiltered;
 };
 
-__global__ void __launch_bounds__(kThreads)
-k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
+// One Gaussian: returns its kept-tile count (0 = culled) and its depth key.
+__device__ __forceinline__ uint32_t
+preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
              const float* __restrict__ scales, const float* __restrict__ rots,
              const float* __restrict__ cov_pre, const float* __restrict__ shs,
              const float* __restrict__ colors_pre, const float* __restrict__ opac,
              const float* __restrict__ vm, const float* __restrict__ pm,
-             const float* __restrict__ campos, int32_t* __restrict__ radii, GeomState g) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P) return;
+             const float* __restrict__ campos, int32_t* __restrict__ radii, GeomState g,
+             uint32_t* key_out) {
   radii[i] = 0;
-  g.tiles[i] = 0;
   g.dup[i] = make_uint4(0u, 0u, 0u, 0u);
   // depth-sort key/value (fused here instead of a separate pass): culled
   // Gaussians sort last and emit nothing
-  g.dkey[i] = 0xFFFFFFFFu;
-  g.iota[i] = (uint64_t)i;
+  g.dkey[0][i] = 0xFFFFFFFFu;
+  g.dval[0][i] = (uint32_t)i;
   const float mx = means[i * 3 + 0], my = means[i * 3 + 1], mz = means[i * 3 + 2];
   float pv[3];
   xform43(vm, mx, my, mz, pv);
-  if (pv[2] <= 0.2f) return;  // in_frustum near-plane cull
+  if (pv[2] <= 0.2f) return 0u;  // in_frustum near-plane cull
   float ph[4];
   xform44(pm, mx, my, mz, ph);
   const float pw = 1.0f / (ph[3] + 0.0000001f);
@@ -241,7 +221,7 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
   Ewa e = ewa_project(mx, my, mz, cov3, vm, cam.fx, cam.fy, cam.tanfx, cam.tanfy);
   const float a = e.a + 0.3f, b = e.b, c = e.c + 0.3f;
   const float det = a * c - b * b;
-  if (det == 0.0f) return;
+  if (det == 0.0f) return 0u;
   const float det_inv = 1.0f / det;
   const float mid = 0.5f * (a + c);
   const float disc = sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -250,7 +230,7 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
   const float px = ndc2pix(ppx, cam.W), py = ndc2pix(ppy, cam.H);
   int x0, y0, x1, y1;
   get_rect(px, py, r, cam.gx, cam.gy, &x0, &y0, &x1, &y1);
-  if ((x1 - x0) * (y1 - y0) == 0) return;
+  if ((x1 - x0) * (y1 - y0) == 0) return 0u;
 
   float rgb[3];
   if (colors_pre) {
@@ -296,31 +276,87 @@ k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
   g.dup[i] = make_uint4((uint32_t)x0 | ((uint32_t)y0 << 16),
                         (uint32_t)rw | ((uint32_t)(y1 - y0) << 16), (uint32_t)mask,
                         (uint32_t)(mask >> 32));
-  g.tiles[i] = n;
   // stable depth sort key: positive depth bits order like the floats
-  g.dkey[i] = n > 0 ? __float_as_uint(pv[2]) : 0xFFFFFFFFu;
-  g.iota[i] = (uint64_t)i | ((uint64_t)n << 32);
+  // (~0u is reserved for culled Gaussians so that every emitting Gaussian
+  // ranks below `visible`; no finite depth reaches it)
+  const uint32_t key = n > 0 ? min(__float_as_uint(pv[2]), 0xFFFFFFFEu) : 0xFFFFFFFFu;
+  g.dkey[0][i] = key;
+  g.dval[0][i] = (uint32_t)i;
+  *key_out = key;
+  return n;
 }
 
-// ------------------------------------------------------------- binning ----
-
-// tiles kept by Gaussian d (its duplication record)
-__device__ __forceinline__ uint32_t dup_count(const uint4 d) {
-  const uint32_t w = d.y & 0xFFFFu, h = d.y >> 16;
-  return w * h <= 64u ? (uint32_t)__popcll((uint64_t)d.z | ((uint64_t)d.w << 32)) : w * h;
+__global__ void __launch_bounds__(kThreads)
+k_preprocess(int64_t P, Cam cam, const float* __restrict__ means,
+             const float* __restrict__ scales, const float* __restrict__ rots,
+             const float* __restrict__ cov_pre, const float* __restrict__ shs,
+             const float* __restrict__ colors_pre, const float* __restrict__ opac,
+             const float* __restrict__ vm, const float* __restrict__ pm,
+             const float* __restrict__ campos, int32_t* __restrict__ radii, GeomState g) {
+  __shared__ unsigned long long s_sum[kThreads / 64];
+  __shared__ uint32_t s_max[kThreads / 64], s_min[kThreads / 64];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t n = 0, key = 0;
+  if (i < P)
+    n = preprocess_one(i, cam, means, scales, rots, cov_pre, shs, colors_pre, opac, vm, pm,
+                       campos, radii, g, &key);
+  // workgroup total and key range, then one set of atomics (replaces a
+  // reduction pass)
+  unsigned long long s = n;
+  uint32_t kmax = n > 0 ? key : 0u, kmin_inv = n > 0 ? ~key : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    kmax = max(kmax, (uint32_t)__shfl_xor(kmax, o, 64));
+    kmin_inv = max(kmin_inv, (uint32_t)__shfl_xor(kmin_inv, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_sum[threadIdx.x >> 6] = s;
+    s_max[threadIdx.x >> 6] = kmax;
+    s_min[threadIdx.x >> 6] = kmin_inv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long bs = 0;
+    uint32_t bmax = 0, bmin = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) {
+      bs += s_sum[w];
+      bmax = max(bmax, s_max[w]);
+      bmin = max(bmin, s_min[w]);
+    }
+    if (bs > 0) {
+      RedSlot* sl = &g.red->slot[blockIdx.x & (kRedSlots - 1)];
+      atomicAdd(&sl->total, bs);
+      atomicMax(&sl->kmax, bmax);
+      atomicMax(&sl->kmin_inv, bmin);
+    }
+  }
 }
 
-
-// Instances in depth order: the wave's 64 depth ranks k own the contiguous
-// output range [start(k0), end(k0 + 63)).  It is produced in chunks of DCH
-// slots: every lane enumerates its own instances that fall in the chunk
-// (kept-tile mask bits in rect order, or the plain rect for rects of more
-// than 64 tiles) into the wave's LDS slice, then the wave copies the slice
-// out with coalesced stores.  A stable sort by tile id then yields the
-// reference's (tile, depth, index) order (rasterizer_impl.cu
-// duplicateWithKeys + SortPairs over tile<<32 | depth): equal depths keep
-// index order from the stable depth sort.
-constexpr int DCH = 512;
+// ------------------------------------------------------------- sorting ----
+//
+// The reference binning (rasterizer_impl.cu duplicateWithKeys + SortPairs
+// over tile << 32 | depth) orders instances by (tile, depth, index).  Here
+// two hand-written stable LSD radix sorts, each pass over <= 9-bit digits:
+//
+//   depth sort   the P Gaussians by depth key (equal keys keep index
+//                order).  Keys are offset by the minimum visible key (read
+//                back with num_rendered), so the pass count follows the live
+//                key width: 24 bits -> 3 passes of 8 bits.
+//   gather       the duplication records in depth order + instances per
+//                512-rank segment, scanned (k_order_gather, k_seg_scan).
+//   duplication  instances written in depth order (wave-cooperative,
+//                coalesced), tile id as key.
+//   tile sort    the instances by tile id (11 bits at 960x540 -> 6 + 5).
+//
+// Each pass: k_rs_hist (digit counts of every 4096-item segment ->
+// hist[digit][segment]) -> k_row_scan (one wave per digit row, exclusive
+// offsets in place, row total) -> k_rs_scatter: per-wave digit counts in
+// LDS, the segment's items ranked within each 64-item window by a ballot
+// match on the digit (stable by construction), staged in LDS in digit order
+// and written out as runs of consecutive addresses (a random scatter of
+// single words would cost one partial-line write-back per item).
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -328,63 +364,373 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ void __launch_bounds__(kThreads)
-k_duplicate(int64_t P, int gx, int gy, const int32_t* __restrict__ radii, GeomState g,
-            uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  __shared__ uint32_t s_key[kThreads / 64][DCH];
-  __shared__ uint32_t s_val[kThreads / 64][DCH];
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
+
+// lanes of `active` holding the same `bits`-bit value as this lane
+__device__ __forceinline__ uint64_t match_peers(uint32_t d, bool active, int bits) {
+  uint64_t peers = __ballot(active);
+  for (int b = 0; b < bits; ++b) {
+    const bool set = (d >> b) & 1u;
+    const uint64_t m = __ballot(active && set);
+    peers &= set ? m : ~m;
+  }
+  return peers;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// exclusive scan of one value per thread across the workgroup; total too
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w,
+                                                    uint32_t* total = nullptr) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t i = 0, cnt = 0, start = g.offsets_sorted[P - 1];
-  int x0 = 0, y0 = 0, rw = 1;
-  uint64_t mask = 0;
-  bool use_mask = false;
-  if (k < P) {
-    const uint64_t o = g.order[k];
-    i = (uint32_t)o;
-    cnt = (uint32_t)(o >> 32);
-    start = k == 0 ? 0u : g.offsets_sorted[k - 1];
-    if (cnt > 0) {
-      const uint4 d = g.dup[i];
-      x0 = (int)(d.x & 0xFFFFu);
-      y0 = (int)(d.x >> 16);
-      rw = (int)(d.y & 0xFFFFu);
-      use_mask = rw * (int)(d.y >> 16) <= 64;
-      mask = (uint64_t)d.z | ((uint64_t)d.w << 32);
+  const uint32_t inc = wave_incl_scan(v, lane);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; ++k) {
+    base += k < w ? s_w[k] : 0u;
+    all += s_w[k];
+  }
+  __syncthreads();
+  if (total) *total = all;
+  return base + inc - v;
+}
+
+// Per row: exclusive scan over `cols` columns in place, row total to
+// tot[row].  One workgroup per row; wave w owns a contiguous quarter of the
+// columns: quarter totals first, then the scan with the quarter's carry-in.
+__global__ void __launch_bounds__(kThreads)
+k_row_scan(uint32_t* __restrict__ hist, int64_t cols, uint32_t* __restrict__ tot) {
+  constexpr int NW = kThreads / 64, kCh = 8;
+  __shared__ uint32_t s_q[NW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t* h = hist + (size_t)blockIdx.x * cols;
+  const int64_t per = (cols + NW - 1) / NW;
+  const int64_t q0 = min(cols, (int64_t)w * per), q1 = min(cols, q0 + per);
+  uint32_t sum = 0;
+  for (int64_t c0 = q0; c0 < q1; c0 += kCh * 64) {
+    uint32_t v[kCh];
+#pragma unroll
+    for (int j = 0; j < kCh; ++j) {
+      const int64_t c = c0 + j * 64 + lane;
+      v[j] = c < q1 ? h[c] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kCh; ++j) sum += v[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if (lane == 0) s_q[w] = sum;
+  __syncthreads();
+  uint32_t carry = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    carry += k < w ? s_q[k] : 0u;
+    all += s_q[k];
+  }
+  for (int64_t c0 = q0; c0 < q1; c0 += kCh * 64) {
+    uint32_t v[kCh];
+#pragma unroll
+    for (int j = 0; j < kCh; ++j) {
+      const int64_t c = c0 + j * 64 + lane;
+      v[j] = c < q1 ? h[c] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kCh; ++j) {
+      const int64_t c = c0 + j * 64 + lane;
+      const uint32_t inc = wave_incl_scan(v[j], lane);
+      if (c < q1) h[c] = carry + inc - v[j];
+      carry += __shfl(inc, 63, 64);
     }
   }
-  const uint32_t lo = __shfl(start, 0, 64);
-  const uint32_t hi = __shfl(start + cnt, 63, 64);
-  uint32_t* sk = s_key[w];
-  uint32_t* sv = s_val[w];
-  for (uint32_t c0 = lo; c0 < hi; c0 += DCH) {
-    const uint32_t c1 = min(c0 + (uint32_t)DCH, hi);
-    if (cnt > 0 && start < c1 && start + cnt > c0) {
-      if (use_mask) {
-        uint64_t m = mask;
-        const uint32_t e = min(c1, start + cnt);
-        for (uint32_t s = start; m && s < e; ++s) {
-          const int pos = __builtin_ctzll(m);
-          m &= m - 1;
-          if (s >= c0) {
-            sk[s - c0] = (uint32_t)((y0 + pos / rw) * gx + x0 + pos % rw);
-            sv[s - c0] = i;
-          }
-        }
-      } else {
-        const uint32_t j0 = max(c0, start) - start, j1 = min(c1, start + cnt) - start;
-        for (uint32_t j = j0; j < j1; ++j) {
-          sk[start + j - c0] = (uint32_t)((y0 + (int)j / rw) * gx + x0 + (int)j % rw);
-          sv[start + j - c0] = i;
+  if (threadIdx.x == 0) tot[blockIdx.x] = all;
+}
+
+// digit of a key: (min(key - kmin, span) >> shift) & mask
+struct Digit {
+  uint32_t kmin, span;
+  int shift, bits;
+  __device__ __forceinline__ uint32_t operator()(uint32_t key) const {
+    uint32_t k = key - kmin;
+    k = k < span ? k : span;
+    return (k >> shift) & ((1u << bits) - 1u);
+  }
+};
+
+__global__ void __launch_bounds__(kSortThreads)
+k_rs_hist(int64_t n, const uint32_t* __restrict__ keys, Digit dg, int64_t nseg,
+          uint32_t* __restrict__ hist) {
+  __shared__ uint32_t cnt[kMaxBins];
+  const int bins = 1 << dg.bits;
+  for (int d = threadIdx.x; d < bins; d += kSortThreads) cnt[d] = 0u;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t s = blockIdx.x;
+  const int64_t i0 = s * kSegItems;
+  uint32_t key[kSortPerLane];
+#pragma unroll
+  for (int j = 0; j < kSortPerLane; ++j) {
+    const int64_t i = i0 + j * kSortThreads + threadIdx.x;
+    key[j] = i < n ? keys[i] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < kSortPerLane; ++j) {
+    const bool ok = i0 + j * kSortThreads + threadIdx.x < n;
+    const uint32_t d = dg(key[j]);
+    // one LDS atomic per distinct digit of the window
+    const uint64_t peers = match_peers(d, ok, dg.bits);
+    if (ok && (peers & lanemask_lt(lane)) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < bins; d += kSortThreads) hist[(size_t)d * nseg + s] = cnt[d];
+}
+
+// One segment of kSegItems items: wave w owns items [w * 512, (w + 1) *
+// 512) of it, in 8 windows of 64.
+template <typename V>
+__global__ void __launch_bounds__(kSortThreads)
+k_rs_scatter(int64_t n, const uint32_t* __restrict__ kin, const V* __restrict__ vin,
+             uint32_t* __restrict__ kout, V* __restrict__ vout, Digit dg, int64_t nseg,
+             const uint32_t* __restrict__ hist, const uint32_t* __restrict__ tot) {
+  constexpr int NW = kSortThreads / 64;
+  __shared__ uint32_t cnt[NW][kMaxBins];  // per-wave counts -> local slots
+  __shared__ uint32_t gdelta[kMaxBins];   // global slot - local slot, per digit
+  __shared__ uint32_t s_w[NW];
+  __shared__ uint32_t sk[kSegItems];
+  __shared__ V sv[kSegItems];
+  const int bins = 1 << dg.bits;
+  for (int d = threadIdx.x; d < NW * kMaxBins; d += kSortThreads) (&cnt[0][0])[d] = 0u;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t s = blockIdx.x;
+  const int64_t seg0 = s * kSegItems;
+  const int64_t base_w = seg0 + (int64_t)w * 64 * kSortPerLane;
+  uint32_t key[kSortPerLane];
+  V val[kSortPerLane];
+  // phase A: every load issued first, then digits, window matches and
+  // per-wave counts
+#pragma unroll
+  for (int j = 0; j < kSortPerLane; ++j) {
+    const int64_t i = base_w + j * 64 + lane;
+    key[j] = i < n ? kin[i] : 0u;
+    val[j] = i < n ? vin[i] : V(0);
+  }
+#pragma unroll
+  for (int j = 0; j < kSortPerLane; ++j) {
+    const bool ok = base_w + j * 64 + lane < n;
+    const uint32_t d = dg(key[j]);
+    const uint64_t peers = match_peers(d, ok, dg.bits);
+    if (ok && (peers & lanemask_lt(lane)) == 0) atomicAdd(&cnt[w][d], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  // phase B: local slots (digit-major within the segment) and the global
+  // offset of each digit's run; bins <= 2 * kSortThreads
+  {
+    constexpr int PER = kMaxBins / kSortThreads;
+    uint32_t tb[PER], gt[PER], lsum = 0, gsum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int d = threadIdx.x * PER + q;
+      tb[q] = 0;
+      gt[q] = 0;
+      if (d < bins) {
+#pragma unroll
+        for (int k = 0; k < NW; ++k) tb[q] += cnt[k][d];
+        gt[q] = tot[d];
+      }
+      lsum += tb[q];
+      gsum += gt[q];
+    }
+    uint32_t lbase = block_excl_scan<kSortThreads>(lsum, s_w);
+    uint32_t gbase = block_excl_scan<kSortThreads>(gsum, s_w);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int d = threadIdx.x * PER + q;
+      if (d < bins) {
+        gdelta[d] = gbase + hist[(size_t)d * nseg + s] - lbase;
+        uint32_t b = lbase;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+          const uint32_t c = cnt[k][d];
+          cnt[k][d] = b;
+          b += c;
         }
       }
+      lbase += tb[q];
+      gbase += gt[q];
+    }
+  }
+  __syncthreads();
+  // phase C: local slot = wave's running slot + rank among equal digits in
+  // the window; stage key and value there
+#pragma unroll
+  for (int j = 0; j < kSortPerLane; ++j) {
+    const bool ok = base_w + j * 64 + lane < n;
+    const uint32_t d = dg(key[j]);
+    const uint64_t peers = match_peers(d, ok, dg.bits);
+    if (ok) {
+      const uint32_t b = cnt[w][d];
+      const uint32_t lp = b + (uint32_t)__popcll(peers & lanemask_lt(lane));
+      if ((peers >> lane) == 1ull) cnt[w][d] = b + (uint32_t)__popcll(peers);
+      sk[lp] = key[j];
+      sv[lp] = val[j];
     }
     wave_lds_sync();
-    for (uint32_t t = lane; t < c1 - c0; t += 64) {
-      keys[c0 + t] = sk[t];
-      vals[c0 + t] = sv[t];
+  }
+  __syncthreads();
+  // phase D: runs of equal digits go to consecutive global slots
+  const int m = (int)min<int64_t>(kSegItems, n - seg0);
+#pragma unroll
+  for (int j = 0; j < kSortPerLane; ++j) {
+    const int lp = j * kSortThreads + threadIdx.x;
+    if (lp < m) {
+      const uint32_t k = sk[lp];
+      const uint32_t gp = (uint32_t)lp + gdelta[dg(k)];
+      if (kout) kout[gp] = k;
+      vout[gp] = sv[lp];
     }
-    wave_lds_sync();
+  }
+}
+
+__device__ __forceinline__ uint32_t dup_count(const uint4 d) {
+  const uint32_t w = d.y & 0xFFFFu, h = d.y >> 16;
+  return w * h <= 64u ? (uint32_t)__popcll((uint64_t)d.z | ((uint64_t)d.w << 32)) : w * h;
+}
+
+// The duplication records in depth order (one coalesced copy instead of a
+// random gather inside the emission loop), and the instances of every
+// kDupRanks-rank segment (one wave each; all gathers of a lane in flight).
+__global__ void __launch_bounds__(kThreads)
+k_order_gather(int64_t P, const uint32_t* __restrict__ order, const uint4* __restrict__ dup,
+               int64_t nwseg, uint4* __restrict__ dsorted, uint32_t* __restrict__ cnt_seg) {
+  constexpr int NWIN = kDupRanks / 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t ws = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (ws >= nwseg) return;
+  uint4 d[NWIN];
+#pragma unroll
+  for (int j = 0; j < NWIN; ++j) {
+    const int64_t k = ws * kDupRanks + j * 64 + lane;
+    d[j] = k < P ? dup[order[k]] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < NWIN; ++j) {
+    const int64_t k = ws * kDupRanks + j * 64 + lane;
+    if (k < P) {
+      dsorted[k] = d[j];
+      c += dup_count(d[j]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane == 0) cnt_seg[ws] = c;
+}
+
+// exclusive scan of the segment counts in place (one workgroup)
+__global__ void __launch_bounds__(1024) k_seg_scan(uint32_t* __restrict__ cnt_seg, int64_t nseg) {
+  __shared__ uint32_t s_w[16];
+  uint32_t carry = 0;
+  for (int64_t c0 = 0; c0 < nseg; c0 += 1024) {
+    const int64_t c = c0 + threadIdx.x;
+    const uint32_t v = c < nseg ? cnt_seg[c] : 0u;
+    uint32_t total = 0;
+    const uint32_t ex = block_excl_scan<1024>(v, s_w, &total);
+    if (c < nseg) cnt_seg[c] = carry + ex;
+    carry += total;
+  }
+}
+
+// Instances in depth order.  Each wave owns kDupRanks consecutive depth
+// ranks, which start at the segment's scanned offset; 64 ranks at a time own
+// a contiguous output range, produced in chunks of DCH slots: every lane
+// enumerates its own instances that fall in the chunk (kept-tile mask bits
+// in rect order, or the plain rect for rects of more than 64 tiles) into the
+// wave's LDS slice, then the wave copies the slice out with coalesced
+// stores.  Waves are independent (no workgroup barriers).
+constexpr int DCH = 512;
+
+__global__ void __launch_bounds__(kThreads)
+k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ order,
+            const uint4* __restrict__ dsorted,
+            const uint32_t* __restrict__ seg_off, int64_t nwseg, uint32_t* __restrict__ keys,
+            uint32_t* __restrict__ vals) {
+  __shared__ uint32_t s_key[kThreads / 64][DCH];
+  __shared__ uint32_t s_val[kThreads / 64][DCH];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t ws = (int64_t)blockIdx.x * (kThreads / 64) + w;
+  if (ws >= nwseg) return;
+  uint32_t* sk = s_key[w];
+  uint32_t* sv = s_val[w];
+  uint32_t running = seg_off[ws];
+  const int64_t k_base = ws * kDupRanks + lane;
+  // records are in depth order (coalesced); windows r + 1 and r + 2 are in
+  // flight while window r is emitted
+  constexpr int NWIN = kDupRanks / 64;
+  auto ld_o = [&](int r) { const int64_t k = k_base + r * 64; return k < P ? order[k] : 0u; };
+  auto ld_d = [&](int r) {
+    const int64_t k = k_base + r * 64;
+    return k < P ? dsorted[k] : make_uint4(0u, 0u, 0u, 0u);
+  };
+  uint32_t o1 = ld_o(0), o2 = NWIN > 1 ? ld_o(1) : 0u;
+  uint4 d1 = ld_d(0), d2 = NWIN > 1 ? ld_d(1) : make_uint4(0u, 0u, 0u, 0u);
+  for (int r = 0; r < NWIN; ++r) {
+    const uint32_t i = o1;
+    const uint4 d = d1;
+    o1 = o2;
+    d1 = d2;
+    if (r + 2 < NWIN) {
+      o2 = ld_o(r + 2);
+      d2 = ld_d(r + 2);
+    }
+    const uint32_t cnt = dup_count(d);
+    const int x0 = (int)(d.x & 0xFFFFu), y0 = (int)(d.x >> 16);
+    const int rw = max(1, (int)(d.y & 0xFFFFu));
+    const bool use_mask = rw * (int)(d.y >> 16) <= 64;
+    const uint64_t mask = (uint64_t)d.z | ((uint64_t)d.w << 32);
+    const uint32_t inc = wave_incl_scan(cnt, lane);
+    const uint32_t start = running + inc - cnt;
+    const uint32_t lo = running;
+    const uint32_t hi = running + __shfl(inc, 63, 64);
+    running = hi;
+    for (uint32_t c0 = lo; c0 < hi; c0 += DCH) {
+      const uint32_t c1 = min(c0 + (uint32_t)DCH, hi);
+      if (cnt > 0 && start < c1 && start + cnt > c0) {
+        if (use_mask) {
+          uint64_t m = mask;
+          const uint32_t e = min(c1, start + cnt);
+          for (uint32_t q = start; m && q < e; ++q) {
+            const int pos = __builtin_ctzll(m);
+            m &= m - 1;
+            if (q >= c0) {
+              sk[q - c0] = (uint32_t)((y0 + pos / rw) * gx + x0 + pos % rw);
+              sv[q - c0] = i;
+            }
+          }
+        } else {
+          const uint32_t j0 = max(c0, start) - start, j1 = min(c1, start + cnt) - start;
+          for (uint32_t j = j0; j < j1; ++j) {
+            sk[start + j - c0] = (uint32_t)((y0 + (int)j / rw) * gx + x0 + (int)j % rw);
+            sv[start + j - c0] = i;
+          }
+        }
+      }
+      wave_lds_sync();
+      for (uint32_t t = lane; t < c1 - c0; t += 64) {
+        keys[c0 + t] = sk[t];
+        vals[c0 + t] = sv[t];
+      }
+      wave_lds_sync();
+    }
   }
 }
 
@@ -403,6 +749,36 @@ k_ranges(int64_t R, const uint32_t* __restrict__ keys, uint2* __restrict__ range
     }
   }
   if (i == R - 1) ranges[cur].y = (uint32_t)R;
+}
+
+// One stable LSD sort: passes over `bits` bits of (key - kmin), each of
+// <= kMaxDigitBits.  Returns the index (0/1) of the ping-pong buffers that
+// hold the result.
+inline int sort_passes(int bits) { return std::max(1, (bits + kMaxDigitBits - 1) / kMaxDigitBits); }
+// ping-pong index holding the tile-sorted instances (gsr_render, gsr_backward)
+inline int tile_sort_buffer(int ntiles) {
+  return sort_passes(bit_length((uint64_t)(ntiles - 1))) & 1;
+}
+
+template <typename V>
+int radix_sort(int64_t n, uint32_t* keys[2], V* vals[2], uint32_t kmin, uint32_t span, int bits,
+               bool keep_keys, uint32_t* hist, uint32_t* tot, hipStream_t st) {
+  const int passes = sort_passes(bits);
+  const int width = (bits + passes - 1) / passes;
+  const int64_t nseg = nsegs(n);
+  int src = 0;
+  for (int p = 0; p < passes; ++p) {
+    const int hi = std::min(bits, (p + 1) * width);
+    const Digit dg{kmin, span, p * width, std::max(1, hi - p * width)};
+    k_rs_hist<<<(unsigned)nseg, kSortThreads, 0, st>>>(n, keys[src], dg, nseg, hist);
+    k_row_scan<<<1u << dg.bits, kThreads, 0, st>>>(hist, nseg, tot);
+    const bool last = p == passes - 1;
+    k_rs_scatter<V><<<(unsigned)nseg, kSortThreads, 0, st>>>(
+        n, keys[src], vals[src], (!last || keep_keys) ? keys[src ^ 1] : nullptr, vals[src ^ 1],
+        dg, nseg, hist, tot);
+    src ^= 1;
+  }
+  return src;
 }
 
 // --------------------------------------------------------------- blend ----
@@ -852,6 +1228,15 @@ struct Timing {
 };
 thread_local Timing g_timing;
 
+// depth-key range of the last gsr_preprocess on this thread (read back with
+// num_rendered), keyed by its geometry buffer
+struct KeyRange {
+  const void* geom = nullptr;
+  int64_t P = 0;
+  uint32_t kmin = 0, kmax = 0;
+};
+thread_local KeyRange g_keyrange;
+
 void tmark(int k, hipStream_t s) {
   if (!g_timing.enabled) return;
   if (!g_timing.created) {
@@ -892,8 +1277,9 @@ void gsr_set_timing(int enabled) { g_timing.enabled = enabled != 0; }
 int gsr_last_timing(float* phases_ms, int n) {
   if (!g_timing.valid) return S3_ERR_INVALID;
   S3_HIP(hipEventSynchronize(g_timing.ev[6]));
-  // (preprocess, scan, duplicate+sort, ranges, blend); event 2 -> 3 spans the
-  // host read-back of num_rendered and is not a device phase.
+  // (preprocess, reduce (fused into preprocess: ~0), depth sort, tile
+  // binning, blend); event 2 -> 3 spans the host read-back of num_rendered
+  // and is not a device phase.
   const int from[5] = {0, 1, 3, 4, 5};
   for (int k = 0; k < n && k < 5; ++k) {
     float ms = 0.f;
@@ -922,22 +1308,28 @@ int gsr_preprocess(const gsr_settings* s, int64_t P, int M, const float* means3D
   Cam cam = make_cam(s, M);
   GeomState g = carve_geom(geom, P);
   tmark(0, st);
+  S3_HIP(hipMemsetAsync(g.red, 0, sizeof(Reduce), st));
   k_preprocess<<<(unsigned)s3::cdiv(P, kThreads), kThreads, 0, st>>>(
       P, cam, means3D, scales, rotations, cov3D_precomp, shs, colors_precomp, opacities,
       s->viewmatrix, s->projmatrix, s->campos, radii, g);
   S3_LAUNCH_CHECK();
   tmark(1, st);
-  size_t tb = g.scan_bytes;
-  S3_HIP(hipcub::DeviceReduce::Sum(g.scan_tmp, tb, Tiles64It(g.tiles, Widen()), g.total, (int)P,
-                                   st));
   tmark(2, st);
-  uint64_t total = 0;
-  S3_HIP(hipMemcpyAsync(&total, g.total, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  static thread_local Reduce red;
+  S3_HIP(hipMemcpyAsync(&red, g.red, sizeof(Reduce), hipMemcpyDeviceToHost, st));
   S3_HIP(hipStreamSynchronize(st));
+  unsigned long long total = 0;
+  uint32_t kmax = 0, kmin_inv = 0;
+  for (int k = 0; k < kRedSlots; ++k) {
+    total += red.slot[k].total;
+    kmax = std::max(kmax, red.slot[k].kmax);
+    kmin_inv = std::max(kmin_inv, red.slot[k].kmin_inv);
+  }
   // the binning pass indexes instances with 32-bit offsets
-  S3_REQUIRE(total < ((uint64_t)1 << 32), "gsr_preprocess: %llu tile instances exceed 2^32",
-             (unsigned long long)total);
+  S3_REQUIRE(total < ((unsigned long long)1 << 32),
+             "gsr_preprocess: %llu tile instances exceed 2^32", total);
   *num_rendered = (int64_t)total;
+  g_keyrange = {geom, P, ~kmin_inv, kmax};
   return S3_OK;
 }
 
@@ -945,6 +1337,7 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
                void* geom, void* binning, void* image, float* out_color, void* stream) {
   S3_REQUIRE(s && P >= 0 && R >= 0, "gsr_render: bad arguments");
   S3_REQUIRE(R < ((int64_t)1 << 32), "gsr_render: too many tile instances");
+  (void)radii;
   hipStream_t st = s3::as_stream(stream);
   const int W = s->image_width, H = s->image_height;
   const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY, ntiles = gx * gy;
@@ -957,30 +1350,40 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
   ImageState im = carve_image(image, H, W);
   tmark(3, st);
   S3_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * ntiles, st));
+  const uint32_t* point_list = b.vals[0];
   if (R > 0) {
-    const unsigned pb = (unsigned)s3::cdiv(P, kThreads);
-    size_t db = g.dsort_bytes;
-    S3_HIP(hipcub::DeviceRadixSort::SortPairs(g.dsort_tmp, db, g.dkey, g.dkey_sorted, g.iota,
-                                              g.order, (int)P, 0, 32, st));
-    size_t sb = g.scan_bytes;
-    S3_HIP(hipcub::DeviceScan::InclusiveSum(g.scan_tmp, sb,
-                                            TilesIt(g.order, HighWord()), g.offsets_sorted,
-                                            (int)P, st));
-    k_duplicate<<<pb, kThreads, 0, st>>>(P, gx, gy, radii, g, b.keys_unsorted,
-                                         b.vals_unsorted);
+    // the depth-key range of this geometry buffer, from gsr_preprocess's
+    // read-back (full 32-bit width if the buffer was filled elsewhere)
+    uint32_t kmin = 0, kmax = 0xFFFFFFFEu;
+    if (g_keyrange.geom == geom && g_keyrange.P == P) {
+      kmin = g_keyrange.kmin;
+      kmax = g_keyrange.kmax;
+    }
+    // visible keys map to [0, kmax - kmin], culled ones (~0u) to span
+    const uint32_t span = kmax - kmin + 1u;
+    const int dsrc = radix_sort<uint32_t>(P, g.dkey, g.dval, kmin, span, bit_length(span), false,
+                                          g.dhist, g.dtot, st);
+    const uint32_t* order = g.dval[dsrc];
+    tmark(4, st);
+    const int64_t nwseg = s3::cdiv(P, kDupRanks);
+    const unsigned dup_blocks = (unsigned)s3::cdiv(nwseg, kThreads / 64);
+    k_order_gather<<<dup_blocks, kThreads, 0, st>>>(P, order, g.dup, nwseg, g.dup_sorted,
+                                                    g.cnt_seg);
+    k_seg_scan<<<1, 1024, 0, st>>>(g.cnt_seg, nwseg);
+    k_duplicate<<<dup_blocks, kThreads, 0, st>>>(P, gx, order, g.dup_sorted, g.cnt_seg, nwseg,
+                                                 b.keys[0], b.vals[0]);
+    const int tsrc = radix_sort<uint32_t>(R, b.keys, b.vals, 0u, 0xFFFFFFFFu,
+                                          bit_length((uint64_t)(ntiles - 1)), true, b.hist, b.tot,
+                                          st);
+    S3_REQUIRE(tsrc == tile_sort_buffer(ntiles), "gsr_render: tile sort buffer mismatch");
+    point_list = b.vals[tsrc];
+    k_ranges<<<(unsigned)s3::cdiv(R, kThreads), kThreads, 0, st>>>(R, b.keys[tsrc], im.ranges);
     S3_LAUNCH_CHECK();
-    size_t tb = b.sort_bytes;
-    S3_HIP(hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, tb, b.keys_unsorted, b.keys,
-                                              b.vals_unsorted, b.vals, (int)R, 0,
-                                              tile_bits(ntiles), st));
-  }
-  tmark(4, st);
-  if (R > 0) {
-    k_ranges<<<(unsigned)s3::cdiv(R, kThreads), kThreads, 0, st>>>(R, b.keys, im.ranges);
-    S3_LAUNCH_CHECK();
+  } else {
+    tmark(4, st);
   }
   tmark(5, st);
-  k_blend<<<ntiles, BS, 0, st>>>(W, H, gx, ntiles, im.ranges, b.vals, g, s->bg, im.final_T,
+  k_blend<<<ntiles, BS, 0, st>>>(W, H, gx, ntiles, im.ranges, point_list, g, s->bg, im.final_T,
                                  im.n_contrib, out_color);
   S3_LAUNCH_CHECK();
   tmark(6, st);
@@ -1022,7 +1425,8 @@ int gsr_backward(const gsr_settings* s, int64_t P, int M, int64_t R, const float
   GeomState g = carve_geom(const_cast<void*>(geom), P);
   BinningState b = carve_binning(const_cast<void*>(binning), R);
   ImageState im = carve_image(const_cast<void*>(image), H, W);
-  k_blend_backward<<<ntiles, BS, 0, st>>>(W, H, gx, ntiles, im.ranges, b.vals, g, s->bg,
+  k_blend_backward<<<ntiles, BS, 0, st>>>(W, H, gx, ntiles, im.ranges,
+                                          b.vals[R > 0 ? tile_sort_buffer(ntiles) : 0], g, s->bg,
                                           im.final_T, im.n_contrib, dL_dout, dL_dmeans2D,
                                           dL_dconic, dL_dopacity, dL_dcolors);
   S3_LAUNCH_CHECK();

@@ -89,7 +89,7 @@ def run(P=4_194_304, iters=10, warmup=3, backward=True, device="cuda"):
     fwd = float(np.median(f_ms))
     out = dict(P=P, H=H, W=W, fwd_ms=fwd, msplats_per_s=P / (fwd * 1e-3) / 1e6,
                fwd_GBps=fwd_bytes(P, H, W) / (fwd * 1e-3) / 1e9,
-               phases_ms=dict(zip(["preprocess", "scan", "dup_sort", "ranges", "blend"], ph)),
+               phases_ms=dict(zip(["preprocess", "reduce", "depth_sort", "binning", "blend"], ph)),
                num_rendered=int(dgr.last_num_rendered), visible=int((radii > 0).sum()))
     if backward:
         bwd = float(np.median(b_ms))
