@@ -403,6 +403,8 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if ws > 1:
+        # ranks > 0 wait for rank 0's single-GPU legs, then all leave together
+        _barrier(ws)
         dist.destroy_process_group()
 
 

@@ -426,11 +426,31 @@ class PairPlan:
         n = Bp * H * W
         self.res = []
         self.desc16 = e(2, Bp, H, W, cfg.desc_dim)
+        # Output layout: the matching outputs of both heads in one block
+        # ([pts3d | conf | desc | desc_conf], each [2 heads, ...]) and each
+        # head's Gaussian parameters in one block, so the host-side copies
+        # the reference semantics need (torch.stack of the two heads, the
+        # gaussian_pred clones) are one copy per block (splatt3r_utils).
+        mkeys = ("pts3d", "conf", "desc", "desc_conf")
+        gkeys = ("means", "scales", "rotations", "sh", "opacities")
+        width = lambda k: max(1, self.KEYS[k])
+        blk_m = torch.empty(2 * n * sum(width(k) for k in mkeys), device=dev, dtype=F32)
+        views, off = {}, 0
+        for k in mkeys:
+            sz = 2 * n * width(k)
+            views[k] = blk_m[off:off + sz].view(2, n * width(k))
+            off += sz
         for hd in range(2):
             out = {}
-            for k, c in self.KEYS.items():
-                shape = (Bp, H, W) if c == 0 else (Bp, H, W, c)
-                out[k] = torch.empty(*shape, device=dev, dtype=F32)
+            for k in mkeys:
+                c = self.KEYS[k]
+                out[k] = views[k][hd].view((Bp, H, W) if c == 0 else (Bp, H, W, c))
+            blk_g = torch.empty(n * sum(width(k) for k in gkeys), device=dev, dtype=F32)
+            off = 0
+            for k in gkeys:
+                sz = n * width(k)
+                out[k] = blk_g[off:off + sz].view(Bp, H, W, self.KEYS[k])
+                off += sz
             out["sh"] = out["sh"].view(Bp, H, W, 3, 1)
             P.add(ops.gaussian_postprocess(n, self.dpt_out[2 * hd], w.NOUT, self.feat25[hd],
                                            self.dpt_out[2 * hd + 1], w.NOUT, cfg.use_offsets, out,

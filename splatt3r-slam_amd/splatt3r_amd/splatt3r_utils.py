@@ -102,9 +102,44 @@ def downsample(X, C, D, Q):
     return X, C, D, Q
 
 
+def _adjacent(a, b):
+    return (a.dtype == b.dtype and a.shape == b.shape and a.is_contiguous() and
+            b.is_contiguous() and
+            a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr() and
+            b.storage_offset() == a.storage_offset() + a.numel())
+
+
+def _pair_view(a, b):
+    """[2, *a.shape] over a and the adjacent b (no copy)."""
+    return torch.empty(0, dtype=a.dtype, device=a.device).set_(
+        a.untyped_storage(), a.storage_offset(), (2,) + tuple(a.shape))
+
+
+def _clone_together(ts):
+    """Fresh copies of the tensors `ts`.  When they tile one contiguous fp32
+    range of a single storage (the pair plan's output blocks, net.py) that
+    range is copied once and the copies are views into it; otherwise one
+    clone each."""
+    ts = list(ts)
+    st = ts[0].untyped_storage()
+    ok = all(t.dtype == torch.float32 and t.is_contiguous() and
+             t.untyped_storage().data_ptr() == st.data_ptr() for t in ts)
+    if ok:
+        spans = sorted((t.storage_offset(), t.numel()) for t in ts)
+        lo, hi = spans[0][0], spans[-1][0] + spans[-1][1]
+        ok = all(a + n == b for (a, n), (b, _) in zip(spans, spans[1:]))
+    if not ok:
+        return [t.clone() for t in ts]
+    copy = torch.empty(0, dtype=torch.float32, device=ts[0].device).set_(
+        st, lo, (hi - lo,)).clone()
+    return [copy[t.storage_offset() - lo:t.storage_offset() - lo + t.numel()].view(t.shape)
+            for t in ts]
+
+
 def _extract_gaussian_params(res):
-    """splatt3r_utils.py:120-137 (clones: the plan buffers are reused)."""
-    d = {k: res[k].clone() for k in ("means", "scales", "rotations", "sh", "opacities")}
+    """splatt3r_utils.py:120-137 (copies: the plan buffers are reused)."""
+    keys = ("means", "scales", "rotations", "sh", "opacities")
+    d = dict(zip(keys, _clone_together(res[k] for k in keys)))
     if "conf" in res:
         d["conf"] = res["conf"].clone()
     return d
@@ -116,6 +151,13 @@ def _ensure_encoded(model, frame):
 
 
 def _stack_outputs(res):
+    """torch.stack of the two heads' (pts3d, conf, desc, desc_conf) at batch
+    element 0: one copy when the plan keeps them in one block (net.py)."""
+    keys = ("pts3d", "conf", "desc", "desc_conf")
+    r0, r1 = res
+    if all(r0[k].shape[0] == 1 and _adjacent(r0[k], r1[k]) for k in keys):
+        X, C, D, Q = (t[:, 0] for t in _clone_together(_pair_view(r0[k], r1[k]) for k in keys))
+        return downsample(X, C, D, Q)
     X = torch.stack([r["pts3d"][0] for r in res])
     C = torch.stack([r["conf"][0] for r in res])
     D = torch.stack([r["desc"][0] for r in res])
@@ -173,10 +215,9 @@ def splatt3r_decode_symmetric_batch(model, feat_i, pos_i, feat_j, pos_j, shape_i
     b = feat_i.shape[0]
     H, W = _hw(shape_i)
     r11, r21, _ = model.encoder.infer_pair(feat_i, pos_i, feat_j, pos_j, (H, W), tag=tag)
-    Xa = [r11["pts3d"].clone(), r21["pts3d"].clone()]
-    Ca = [r11["conf"].clone(), r21["conf"].clone()]
-    Da = [r11["desc"].clone(), r21["desc"].clone()]
-    Qa = [r11["desc_conf"].clone(), r21["desc_conf"].clone()]
+    keys = ("pts3d", "conf", "desc", "desc_conf")
+    c11 = _clone_together([r11[k] for k in keys] + [r21[k] for k in keys])
+    Xa, Ca, Da, Qa = ([c11[i], c11[4 + i]] for i in range(4))
     r22, r12, _ = model.encoder.infer_pair(feat_j, pos_j, feat_i, pos_i, (H, W), tag=tag)
     Xa += [r22["pts3d"], r12["pts3d"]]
     Ca += [r22["conf"], r12["conf"]]

@@ -103,3 +103,31 @@ def test_load_splatt3r_from_file_matches_prng_model(tmp_path):
     rb, _, _ = ref.infer_pair(fb, pb, fb, pb, (48, 64))
     for k in ("pts3d", "conf", "desc", "means", "opacities"):
         assert torch.equal(ra[k], rb[k]), k
+
+
+def test_block_copies_equal_per_tensor_clones():
+    """splatt3r_utils._clone_together / _pair_view (the pair plan keeps its
+    outputs in blocks so the reference's clones and head stack are one copy
+    each): same values as per-tensor clones / torch.stack, fresh storage, and
+    the per-tensor fallback when the tensors do not tile one range."""
+    import torch
+    from splatt3r_amd.splatt3r_utils import _adjacent, _clone_together, _pair_view
+    n, widths = 6, {"pts3d": 3, "conf": 1, "desc": 24, "desc_conf": 1}
+    blk = torch.randn(2 * n * sum(widths.values()))
+    heads, off = [{}, {}], 0
+    for k, c in widths.items():
+        v = blk[off:off + 2 * n * c].view(2, n * c)
+        off += 2 * n * c
+        for h in range(2):
+            heads[h][k] = v[h].view(1, 2, 3, c) if c > 1 else v[h].view(1, 2, 3)
+    assert all(_adjacent(heads[0][k], heads[1][k]) for k in widths)
+    out = _clone_together(_pair_view(heads[0][k], heads[1][k]) for k in widths)
+    for t, k in zip(out, widths):
+        assert torch.equal(t, torch.stack((heads[0][k], heads[1][k])))
+        assert t.untyped_storage().data_ptr() != blk.untyped_storage().data_ptr()
+    assert len({t.untyped_storage().data_ptr() for t in out}) == 1   # one copy
+    g = torch.randn(40)
+    gap = [g[0:10], g[20:40]]                                        # not one range
+    c = _clone_together(gap)
+    assert all(torch.equal(a, b) for a, b in zip(c, gap))
+    assert len({t.untyped_storage().data_ptr() for t in c}) == 2
