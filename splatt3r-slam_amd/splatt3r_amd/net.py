@@ -30,6 +30,7 @@ MI355X-first execution:
 from __future__ import annotations
 
 import math
+import threading
 
 import torch
 
@@ -539,7 +540,7 @@ class Splatt3RNet:
             # in place by later calls made outside it)
             with torch.inference_mode(False):
                 ep = EncoderPlan(self, B, H, W)
-            if self.graphs:
+            if self._capture_here():
                 ep.plan.capture()
             self._enc[key] = ep
         return self._enc[key]
@@ -551,11 +552,19 @@ class Splatt3RNet:
         if key not in self._pair:
             with torch.inference_mode(False):
                 pp = PairPlan(self, Bp, H, W, keep_tokens)
-            if self.graphs and not keep_tokens:
+            if self._capture_here() and not keep_tokens:
                 pp.decoder_plan.capture()
                 pp.head_plan.capture()
             self._pair[key] = pp
         return self._pair[key]
+
+    def _capture_here(self) -> bool:
+        """Plans are captured into HIP graphs only from the main thread: a
+        capture is a device-global state (hipStreamCaptureModeGlobal), so a
+        capture on the backend worker thread would make the frontend
+        thread's concurrent launches fail and invalidate the capture.  Plans
+        first built on a worker thread run eagerly (same kernels)."""
+        return self.graphs and threading.current_thread() is threading.main_thread()
 
     # ------------------------------------------------- reference API -----
     @staticmethod

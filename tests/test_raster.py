@@ -152,6 +152,54 @@ def test_hip_forward_bitexact_vs_oracle(P, seed, mode):
     np.testing.assert_array_equal(img.detach().cpu().numpy(), ref["color"])
 
 
+def _restage(sc, z):
+    """Move every Gaussian to depth z along its own ray (same pixel)."""
+    sc = dict(sc)
+    m = sc["means"].copy()
+    r = (z / m[:, 2]).astype(np.float32)
+    sc["means"] = (m * r[:, None]).astype(np.float32)
+    sc["cov6"] = (sc["cov6"] * (r * r)[:, None]).astype(np.float32)
+    return sc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["plane", "two_depths", "wide_range", "all_culled", "tail_4097",
+                                  "tiles_3600", "tiles_8160"])
+def test_hip_binning_edge_cases_bitexact_vs_oracle(case):
+    """The hand-written depth / tile sorts (raster.hip "sorting"): equal
+    depths (stability by index), a 1-2 pass key width, a 4-pass key width,
+    nothing visible (R = 0), a segment tail, and tile ids of 12 and 13 bits
+    (two 6/7-bit tile passes) -- bit-exact against the oracle."""
+    rng = np.random.default_rng(7)
+    P, H, W, fx = 3000, 48, 64, 60.0
+    if case == "tail_4097":
+        P = 4097
+    if case == "tiles_3600":
+        H, W, fx = 720, 1280, 900.0
+    if case == "tiles_8160":
+        H, W, fx = 1088, 1920, 1300.0
+    sc = small_scene(P, 11, H=H, W=W, fx=fx)
+    if case == "plane":
+        sc = _restage(sc, np.full(P, 3.0, np.float32))
+    elif case == "two_depths":
+        sc = _restage(sc, np.where(rng.random(P) < 0.5, 3.0, 3.0001).astype(np.float32))
+    elif case == "wide_range":
+        sc = _restage(sc, np.exp(rng.uniform(np.log(0.3), np.log(500.0), P)).astype(np.float32))
+    elif case == "all_culled":
+        # in front of the 0.2 near-plane cull even after the settings'
+        # scale-invariant rescale of the means
+        sc = _restage(sc, np.full(P, 1e-5, np.float32))
+    rs, scale, img, radii, kw = _gpu_render(sc, "colors")
+    sd = settings_to_dict(rs)
+    ref = oracle.raster(sd, sc["means"] * scale, sc["opacities"],
+                        colors_precomp=np.clip(sc["shs"][:, 0, :] + 0.5, 0, 1),
+                        cov3D_precomp=sc["cov6"] * scale * scale)
+    np.testing.assert_array_equal(radii.cpu().numpy(), ref["radii"])
+    np.testing.assert_array_equal(img.detach().cpu().numpy(), ref["color"])
+    if case == "all_culled":
+        assert int(radii.max()) == 0
+
+
 @pytest.mark.gpu
 def test_hip_forward_c3_resolution_vs_oracle():
     sc = raster_microbench_scene(200_000, seed=0)
