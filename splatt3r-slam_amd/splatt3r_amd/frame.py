@@ -43,6 +43,7 @@ class Frame:
     K: Optional[torch.Tensor] = None
     gaussian_pred: Optional[dict] = None
     gaussian_pred_cross: Optional[dict] = None
+    gs_world: Optional[list] = None   # [(records [n,13], device count)] (slam.py _to_world)
 
     def __post_init__(self):
         if self.T_WC is None:

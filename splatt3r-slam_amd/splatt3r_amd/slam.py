@@ -36,7 +36,7 @@ import lietorch
 from splatt3r_amd.config import config
 from splatt3r_amd.frame import Frame, Keyframes, Mode, create_frame
 from splatt3r_amd.gaussian_map import SharedGaussians, should_append_gaussians
-from splatt3r_amd.splatt3r_utils import (_sim3_to_4x4, gaussians_to_world, splatt3r_inference_mono,
+from splatt3r_amd.splatt3r_utils import (_sim3_to_4x4, splatt3r_inference_mono,
                                          splatt3r_render, world_records)
 from splatt3r_amd.tracker import FrameTracker
 
@@ -84,7 +84,8 @@ class Frontend:
         self.last_append_idx = -(10 ** 9)                       # main.py:341-342
         self.min_translation, self.min_frame_gap = 0.12, 3   # main.py:339-340
         self.new_kf_frames: list[int] = []
-        self.stats = dict(frames=0, tracked=0, reloc=0, keyframes=0, gn_iters=0,
+        self._gw_count = None   # device count of world records (no-viz path)
+        self._stats = dict(frames=0, tracked=0, reloc=0, keyframes=0, gn_iters=0,
                           gaussians_world=0, rendered=0)
         self._last_render = None
         # host read-back of the render: double-buffered pinned images filled by
@@ -151,7 +152,7 @@ class Frontend:
             return
         img = splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=target)
         if img is not None:
-            self.stats["rendered"] += 1
+            self._stats["rendered"] += 1
             out = img[0, 0].clamp(0, 1).permute(1, 2, 0)
             if not self.readback:
                 self._last_render, self._rb_event = out, None
@@ -186,10 +187,34 @@ class Frontend:
                                          a["min_confidence"])
                 self.gmap.append_records(rec, cnt, kf_idx, self.map_opacity_threshold)
             return True
-        gs = gaussians_to_world(frame, **self.gs_args)
-        if gs is not None:
-            self.stats["gaussians_world"] += int(gs[0].shape[0])
-        return gs
+        # viz off: the reference computes gaussians_to_world and drops the
+        # result (main.py:467-488); the same records are computed here and
+        # kept on the device with their device count (frame.gs_world), so
+        # the tracked frame pays no host sync for the count
+        a = self.gs_args
+        if frame.gaussian_pred is None:
+            return None
+        T = _sim3_to_4x4(frame.T_WC)[0].to(frame.img.device)
+        pred = frame.gaussian_pred
+        recs = []
+        for b in range(pred["means"].shape[0]):
+            view = {k: v[b] for k, v in pred.items()}
+            rec, cnt = world_records(view, frame.img[min(b, frame.img.shape[0] - 1)], T,
+                                     max(1, int(a["spatial_stride"])), 0.05,
+                                     a["depth_max_percentile"], a["max_scale"],
+                                     a["min_confidence"])
+            recs.append((rec, cnt))
+            self._gw_count = cnt.clone() if self._gw_count is None else self._gw_count + cnt
+        frame.gs_world = recs
+        return recs
+
+    @property
+    def stats(self) -> dict:
+        """Frame counters; `gaussians_world` is read from its device counter
+        here (a host sync), never inside step()."""
+        if self._gw_count is not None:
+            self._stats["gaussians_world"] = int(self._gw_count.item())
+        return self._stats
 
     def _kf_added(self, frame):
         """states.queue_global_optimization (main.py:409, 525-526)."""
@@ -251,14 +276,14 @@ class Frontend:
             pending = None
         if e0 is not None:
             e0[0] = self._event()
-        self.stats["frames"] += 1
+        self._stats["frames"] += 1
         add_new_kf = False
         if self.mode == Mode.INIT:
             X, C = splatt3r_inference_mono(self.model, frame)
             frame.update_pointmap(X, C)
             self.keyframes.append(frame)
             self.new_kf_frames.append(i)
-            self.stats["keyframes"] += 1
+            self._stats["keyframes"] += 1
             self._kf_added(frame)
             self.mode = Mode.TRACKING
             if self._to_world(frame, len(self.keyframes) - 1) is not None and self.viz:
@@ -270,8 +295,8 @@ class Frontend:
             add_new_kf, _, try_reloc = self.tracker.track(frame)
             if pending is not None:
                 self._prefetch(*pending)
-            self.stats["gn_iters"] += self.tracker.last_iters
-            self.stats["tracked"] += 1
+            self._stats["gn_iters"] += self.tracker.last_iters
+            self._stats["tracked"] += 1
             if try_reloc:
                 self.mode = Mode.RELOC
             if not try_reloc and should_append_gaussians(
@@ -289,18 +314,18 @@ class Frontend:
             # from an unverified pose)
             X, C = splatt3r_inference_mono(self.model, frame)
             frame.update_pointmap(X, C)
-            self.stats["reloc"] += 1
+            self._stats["reloc"] += 1
             if self.backend is not None:
                 self.backend.wait()
                 if self.backend.relocalization(frame):
-                    self.stats["keyframes"] += 1
+                    self._stats["keyframes"] += 1
                     self.new_kf_frames.append(i)
                     self.tracker.reset_idx_f2k()
                     self.mode = Mode.TRACKING
         if add_new_kf:
             self.keyframes.append(frame)
             self.new_kf_frames.append(i)
-            self.stats["keyframes"] += 1
+            self._stats["keyframes"] += 1
             self.tracker.reset_idx_f2k()
             self._kf_added(frame)
         self.last_T_WC = frame.T_WC
