@@ -39,6 +39,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -122,6 +123,50 @@ def _kernel_profile(net, reps=3):
         a[1] += flops
         a[2] += e0.elapsed_time(e1)
     return {k: [v[0] // reps, v[1] / reps, v[2] / reps] for k, v in agg.items()}
+
+
+_KFAM = re.compile(r"k_gemm<([^>]*)>")
+
+
+def _kernel_trace(net, reps=5):
+    """{family: [launches per frame, ms per frame]} of the network kernels:
+    a torch.profiler (roctracer) kernel trace of `reps` serial replays of
+    every plan's HIP graph (the graphs the frontend replays per frame), one
+    stream, nothing else running -- the per-kernel durations a rocprofv3
+    kernel trace of the bench reports (its streams run serialised too), with
+    no event packets between the kernels.  gemm.dense / gemm.conv = k_gemm
+    by its A-operand mode (template argument 5); split-K reduces are timed
+    with the dense family (the conv launches do not split at these shapes)."""
+    from torch.profiler import ProfilerActivity, profile
+    plans = list(net.plans())
+    for pl in plans:
+        pl.replay()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for _ in range(reps):
+            for pl in plans:
+                pl.replay()
+        torch.cuda.synchronize()
+    fam = {}
+    for e in prof.events():
+        if "CUDA" not in str(e.device_type):
+            continue
+        m = _KFAM.search(e.name)
+        if m:
+            k = "gemm.dense" if m.group(1).split(",")[4].strip() == "0" else "gemm.conv"
+        elif "k_splitk_reduce" in e.name:
+            k = "gemm.dense"
+        elif "k_attn" in e.name:
+            k = "s3n_attention"
+        elif "k_layernorm" in e.name:
+            k = "s3n_layernorm"
+        else:
+            continue
+        f = fam.setdefault(k, [0, 0.0])
+        if "k_splitk_reduce" not in e.name:
+            f[0] += 1
+        f[1] += e.device_time_total / 1e3
+    return {k: [c / reps, ms / reps] for k, (c, ms) in fam.items()}
 
 
 def _pmc_traffic(kind: str):
@@ -355,11 +400,23 @@ def main():
                             "rendered": st["rendered"], "tracked": st["tracked"]},
     }
     if rank == 0 and not a.no_kprof:
+        # after the timed region: kernel durations of the plans' graph
+        # replays (roctracer trace) and a per-launch eager profile
+        trace = _kernel_trace(model.encoder)
         prof = _kernel_profile(model.encoder)
         flops_frame = sum(v[1] for v in prof.values())
         net_tflops = sum(v[1] for v in prof.values()) / (sum(v[2] for v in prof.values()) * 1e-3) / 1e12
         dom = max((k for k in prof if prof[k][1] > 0), key=lambda k: prof[k][2])
         n_l, fl, ms = prof[dom]
+        source = "HIP event pair around each launch of an eager replay of the plans"
+        if trace and dom in trace and abs(trace[dom][0] - n_l) < 0.5:
+            # the traced frames ran exactly this frame's launches of the
+            # family: time them as they run inside the graphs (the event
+            # pairs of the eager replay flush caches between launches)
+            ms = trace[dom][1]
+            source = (f"roctracer kernel timestamps (torch.profiler) of serial replays of the "
+                      f"plans' HIP graphs after the timed region; eager per-launch event "
+                      f"timing: {prof[dom][2]:.3f} ms/frame")
         achieved = fl / (ms * 1e-3) / 1e12
         tr = _pmc_traffic(dom)
         result["roofline"] = {
@@ -368,7 +425,10 @@ def main():
             "frac": achieved / PEAK_F16_TFLOPS,
             "traffic": tr["bytes_per_launch"] if tr else None,
             "launches_per_frame": n_l, "avg_launch_us": ms / n_l * 1e3,
+            "ms_per_frame": ms, "timing": source,
             "algorithmic_gflop_per_frame": fl / 1e9}
+        if trace:
+            result["roofline"]["trace_ms_per_frame"] = {k: v[1] for k, v in trace.items()}
         if tr:
             result["roofline"]["traffic_detail"] = tr
         result["network"] = {"kernels": {k: {"launches": v[0], "gflop": v[1] / 1e9, "ms": v[2]}
