@@ -75,8 +75,9 @@ def _args():
     ap.add_argument("--enc-batch", type=int, default=1,
                     help="frames per encoder replay (lookahead over the sequence); "
                          "the timed region then holds steps/enc-batch encoder replays")
-    ap.add_argument("--main-priority", type=int, default=None,
-                    help="HIP stream priority of the frame's main chain (e.g. -1 = high)")
+    ap.add_argument("--main-priority", type=int, default=-1,
+                    help="HIP stream priority of the frame's main chain (-1 = high, the "
+                         "default: the next frame's encoder yields to it); 0 = normal")
     ap.add_argument("--late-prefetch", action="store_true",
                     help="queue the next frame's encoder after the tracker's GN sync")
     ap.add_argument("--no-pipeline", action="store_true",
