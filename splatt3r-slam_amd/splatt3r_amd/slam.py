@@ -150,7 +150,27 @@ class Frontend:
     def _render(self, frame, ref, target):
         if not self.render:
             return
-        img = splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=target)
+        self._finish_render(splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=target))
+
+    def _speculate(self, frame, ref):
+        """Hook for FrameTracker.track: with the map off, the tracked frame's
+        world records and render depend only on its pose, so they are queued
+        from the device-side pose of the first GN chunk, ahead of the
+        tracker's decision sync; kept when that pose is final and the frame
+        is not lost (the common case), recomputed otherwise."""
+        def hook(T_WC):
+            saved = frame.T_WC
+            frame.T_WC = T_WC
+            try:
+                recs = self._world_records(frame)
+                img = (splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=T_WC)
+                       if self.render else None)
+            finally:
+                frame.T_WC = saved
+            return recs, img
+        return hook
+
+    def _finish_render(self, img):
         if img is not None:
             self._stats["rendered"] += 1
             out = img[0, 0].clamp(0, 1).permute(1, 2, 0)
@@ -191,6 +211,9 @@ class Frontend:
         # result (main.py:467-488); the same records are computed here and
         # kept on the device with their device count (frame.gs_world), so
         # the tracked frame pays no host sync for the count
+        return self._keep_world_records(frame, self._world_records(frame))
+
+    def _world_records(self, frame):
         a = self.gs_args
         if frame.gaussian_pred is None:
             return None
@@ -199,11 +222,16 @@ class Frontend:
         recs = []
         for b in range(pred["means"].shape[0]):
             view = {k: v[b] for k, v in pred.items()}
-            rec, cnt = world_records(view, frame.img[min(b, frame.img.shape[0] - 1)], T,
-                                     max(1, int(a["spatial_stride"])), 0.05,
-                                     a["depth_max_percentile"], a["max_scale"],
-                                     a["min_confidence"])
-            recs.append((rec, cnt))
+            recs.append(world_records(view, frame.img[min(b, frame.img.shape[0] - 1)], T,
+                                      max(1, int(a["spatial_stride"])), 0.05,
+                                      a["depth_max_percentile"], a["max_scale"],
+                                      a["min_confidence"]))
+        return recs
+
+    def _keep_world_records(self, frame, recs):
+        if recs is None:
+            return None
+        for _, cnt in recs:
             self._gw_count = cnt.clone() if self._gw_count is None else self._gw_count + cnt
         frame.gs_world = recs
         return recs
@@ -292,7 +320,10 @@ class Frontend:
             self.last_T_WC = frame.T_WC
             return frame
         if self.mode == Mode.TRACKING:
-            add_new_kf, _, try_reloc = self.tracker.track(frame)
+            hook = self._speculate(frame, self.keyframes.last_keyframe()) if self.gmap is None \
+                else None
+            add_new_kf, _, try_reloc = self.tracker.track(frame, before_sync=hook)
+            spec = self.tracker.spec if (self.tracker.spec_valid and not try_reloc) else None
             if pending is not None:
                 self._prefetch(*pending)
             self._stats["gn_iters"] += self.tracker.last_iters
@@ -302,10 +333,15 @@ class Frontend:
             if not try_reloc and should_append_gaussians(
                     add_new_kf, i, frame.T_WC, self.last_append_T_WC, self.last_append_idx,
                     self.min_translation, self.min_frame_gap):
-                if self._to_world(frame, len(self.keyframes)) is not None and self.viz:
+                if spec is not None:
+                    self._keep_world_records(frame, spec[0])
+                elif self._to_world(frame, len(self.keyframes)) is not None and self.viz:
                     self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
             if not try_reloc:
-                self._render(frame, self.keyframes.last_keyframe(), frame.T_WC)
+                if spec is not None:
+                    self._finish_render(spec[1])
+                else:
+                    self._render(frame, self.keyframes.last_keyframe(), frame.T_WC)
         elif self.mode == Mode.RELOC:
             # main.py:508-517 + relocalization (main.py:76-119): with a
             # backend the frame is matched against the retrieval database and

@@ -190,8 +190,15 @@ class FrameTracker:
     def reset_idx_f2k(self):
         self.idx_f2k = None
 
-    def track(self, frame):
-        """tracker.py:28-127; returns (new_kf, match_info, try_reloc)."""
+    def track(self, frame, before_sync=None):
+        """tracker.py:28-127; returns (new_kf, match_info, try_reloc).
+
+        before_sync(T_WC): called with the device-side pose after the first
+        queued GN chunk, before the host waits for it, so the caller can
+        queue work that depends only on that pose (the frontend's render).
+        Its result is kept in self.spec; self.spec_valid says whether that
+        pose is the final one (GN stopped inside the first chunk)."""
+        self.spec, self.spec_valid = None, False
         from splatt3r_amd.splatt3r_utils import splatt3r_match_asymmetric
         keyframe = self.keyframes.last_keyframe()
         idx_f2k, valid_match_k, Xff, Cff, Qff, Xkf, Ckf, Qkf = splatt3r_match_asymmetric(
@@ -234,6 +241,8 @@ class FrameTracker:
         ne.pose.copy_(T_CkCf.data.reshape(8))
         ne.gn_begin(self.cfg)
         ne.gn_queue(Xf, Xk, Q, valid_c, self.cfg, GN_CHUNK, calib)
+        if before_sync is not None:
+            self.spec = before_sync(T_WCk * lietorch.Sim3(ne.pose.clone().view(1, 8)))
         torch.cuda.current_stream(ne.device).synchronize()
         n_opt, n_kf, n_unique = stats_host.tolist()
 
@@ -287,12 +296,15 @@ class FrameTracker:
         """Drive the device-side GN loop (first chunk already queued and
         synced) to its flag; returns (T_WCf, T_CkCf)."""
         cfg, ne = self.cfg, self.normal_eqs
+        extra = 0
         while True:
             iters, flag = int(ne.state_host[1]), int(ne.state_host[2])
             if flag != 0 or iters >= cfg["max_iters"]:
                 break
             ne.gn_queue(Xf, Xk, Q, valid, cfg, min(GN_CHUNK, cfg["max_iters"] - iters), calib)
             torch.cuda.current_stream(ne.device).synchronize()
+            extra += 1
+        self.spec_valid = extra == 0
         self.last_iters = iters
         if _DEBUG:
             print(f"[gn] iters={iters} flag={flag} cost={float(ne.state_host[3]):.6g}", flush=True)
