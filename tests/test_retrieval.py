@@ -95,7 +95,15 @@ def test_hip_prep_features_vs_oracle(whiten):
     _check_topk(io.cpu(), ao.cpu(), ref_i, ref_a, proj.norm(dim=-1), 1e-4)
     # the selected rows: the oracle's postwhitened tokens at the chosen indices
     sel = post_t[0, io.cpu()[0]]
-    assert torch.allclose(got[0], sel, rtol=1e-4, atol=1e-4)
+    # rows may differ only where the device path's own projection broke a
+    # near-tie of attention values the other way: such a row must be the
+    # postwhitened token whose attention is within tol of that rank's value
+    row_ok = torch.isclose(got[0], sel, rtol=1e-4, atol=1e-4).all(-1)
+    norms = proj.norm(dim=-1)[0]
+    for c in (~row_ok).nonzero().flatten().tolist():
+        j = int((post_t[0] - got[0, c]).abs().amax(-1).argmin())
+        assert torch.allclose(post_t[0, j], got[0, c], rtol=1e-4, atol=1e-4)
+        assert abs(float(norms[j]) - float(ao.cpu()[0, c])) <= 1e-4, (c, j)
     assert torch.allclose(got[0][:50], ref_f[0][:50], rtol=1e-4, atol=1e-4) or \
         bool((io.cpu()[0, :50] != ref_i[0, :50]).any())
 
