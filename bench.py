@@ -441,6 +441,10 @@ def main():
     if not a.no_pairs:
         from splatt3r_amd.pairs import bench_pairs
         result["pairs"] = bench_pairs(model, frames, ws, rank, dev, a.pairs_per_rank)
+        # C4 (EuRoC MH_01 shape): 512x320 frames, 640 tokens, same pair path
+        c4 = tum_like_sequence(12, 320, 512, seed=200 + rank, step_px=2.0, device=dev)
+        result["pairs_c4"] = dict(bench_pairs(model, c4, ws, rank, dev, a.pairs_per_rank),
+                                  image="512x320 (C4, EuRoC MH_01 shape)")
     if rank == 0 and ws == 1 and not a.no_backend:
         result["backend"] = bench_backend(model, dev, a.backend_steps, rank)
     if rank == 0 and not a.no_map:
