@@ -98,6 +98,9 @@ DEBUG_SYNC = os.environ.get("S3_SYNC_DEBUG", "0") == "1"
 # library's automatic tile choice (only where a call leaves tile=0)
 TILE_OVERRIDE = int(os.environ.get("S3_GEMM_TILE", "0"))
 GRAPHS_ENABLED = os.environ.get("S3_GRAPHS", "1") != "0"
+# S3_ATTN_VARIANT=<n>: the no-RoPE attention kernel variant (net_attn.hip
+# s3n_attention_set_variant; experiments only)
+ATTN_VARIANT = int(os.environ["S3_ATTN_VARIANT"]) if "S3_ATTN_VARIANT" in os.environ else None
 
 
 def _ptr(x):
@@ -379,6 +382,8 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
 
 def attention(Q, K, V, O, *, B, Nq, Nk, H, q_stride, k_stride, v_stride, o_stride, qpos=None,
               kpos=None, rope=None, scale=0.125) -> Call:
+    if ATTN_VARIANT is not None:
+        _lib.lib().s3n_attention_set_variant(ATTN_VARIANT)
     a = AttnArgs()
     a.B, a.Nq, a.Nk, a.H, a.groups = B, Nq, Nk, H, len(Q)
     a.Q, a.K, a.V, a.O = _parr(Q), _parr(K), _parr(V), _parr(O)
