@@ -462,9 +462,11 @@ __device__ __forceinline__ float xchg32(float x) { return __shfl_xor(x, 32, 64);
 // the groups' (max, sum, O) partials are merged through LDS at the end.
 // More waves per SIMD for the same 64-query tile, half the serial tile
 // chain per wave.
-template <int SPLIT, int STAGES>
-__global__ void __launch_bounds__(kThreads * SPLIT) k_attn_st(AttnP p) {
+template <int QW, int SPLIT, int STAGES>
+__global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
   constexpr int RING = STAGES * 2 * KT * D;        // fp16 elements per group
+  constexpr int NJ = 8 / QW;                       // K (and V) DMA pieces per wave per tile
+  static_assert(QW == 1 || QW == 2 || QW == 4, "query waves");
   __shared__ __attribute__((aligned(1024))) f16 smem[SPLIT * RING];
   const int qtile = blockIdx.x;
   const int bh = blockIdx.y;
@@ -472,12 +474,12 @@ __global__ void __launch_bounds__(kThreads * SPLIT) k_attn_st(AttnP p) {
   const int g = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int sp = wid >> 2, wave = wid & 3;         // key group, query wave
+  const int sp = wid / QW, wave = wid % QW;         // key group, query wave
   const int grp = lane >> 4, li = lane & 15;
   const f16* __restrict__ Qg = p.Q[g];
   f16* ring = smem + sp * RING;
 
-  const int qrow = qtile * QT + wave * 16 + li;
+  const int qrow = qtile * 16 * QW + wave * 16 + li;
   const bool qok = qrow < p.Nq;
   f16x8 qf[2];
   {
@@ -494,11 +496,11 @@ __global__ void __launch_bounds__(kThreads * SPLIT) k_attn_st(AttnP p) {
   const __amdgpu_buffer_rsrc_t rv =
       make_rsrc(p.V[g], (((int64_t)b + 1) * p.Nk - 1) * p.vs * 2 + (h + 1) * D * 2);
   const int lr = lane >> 3, lc = lane & 7;
-  uint32_t k_off[2], v_off[2];
-  int k_key[2];
+  uint32_t k_off[NJ], v_off[NJ];
+  int k_key[NJ];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = (wave * 2 + j) * 8 + lr;
+  for (int j = 0; j < NJ; ++j) {
+    const int row = (wave * NJ + j) * 8 + lr;
     k_key[j] = row;
     k_off[j] = (uint32_t)((((int64_t)b * p.Nk + row) * p.ks + h * D + kswz(row, lc) * 8) * 2);
     v_off[j] = (uint32_t)((((int64_t)b * p.Nk + row) * p.vs + h * D + lc * 8) * 2);
@@ -511,10 +513,10 @@ __global__ void __launch_bounds__(kThreads * SPLIT) k_attn_st(AttnP p) {
     f16* Vs = Ks + KT * D;
     const int key0 = (i * SPLIT + sp) * KT;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const bool ok = key0 + k_key[j] < p.Nk;
-      S3_BLDS(rk, Ks + (wave * 2 + j) * 512, ok ? k_off[j] : kOOB, (int64_t)key0 * p.ks * 2);
-      S3_BLDS(rv, Vs + (wave * 2 + j) * 512, ok ? v_off[j] : kOOB, (int64_t)key0 * p.vs * 2);
+      S3_BLDS(rk, Ks + (wave * NJ + j) * 512, ok ? k_off[j] : kOOB, (int64_t)key0 * p.ks * 2);
+      S3_BLDS(rv, Vs + (wave * NJ + j) * 512, ok ? v_off[j] : kOOB, (int64_t)key0 * p.vs * 2);
     }
   };
 
@@ -528,7 +530,7 @@ __global__ void __launch_bounds__(kThreads * SPLIT) k_attn_st(AttnP p) {
   for (int i = 0; i < AHEAD; ++i)
     if (i < NTs) issue(i, i);
   for (int i = 0; i < NTmax; ++i) {
-    if (i < NTs) wait_tiles<4, AHEAD - 1>(NTs - 1 - i);
+    if (i < NTs) wait_tiles<2 * NJ, AHEAD - 1>(NTs - 1 - i);
     __builtin_amdgcn_s_barrier();
     if (i >= NTs) continue;
     if (i + AHEAD < NTs) issue(i + AHEAD, (i + AHEAD) % STAGES);
@@ -602,11 +604,11 @@ __global__ void __launch_bounds__(kThreads * SPLIT) k_attn_st(AttnP p) {
     // merge the key groups: groups 1.. publish (m, l, O) per lane, group 0
     // rescales to the common max and sums
     constexpr int REC = 18;                        // m, l, 16 O values
-    static_assert(SPLIT * 256 * REC * 4 <= SPLIT * RING * 2, "merge scratch");
+    static_assert(SPLIT * QW * 64 * REC * 4 <= SPLIT * RING * 2, "merge scratch");
     float* xs = reinterpret_cast<float*>(smem);
     __syncthreads();                               // all rings drained
     if (sp > 0) {
-      float* rec = xs + (((sp - 1) * 4 + wave) * 64 + lane) * REC;
+      float* rec = xs + (((sp - 1) * QW + wave) * 64 + lane) * REC;
       rec[0] = m_run;
       rec[1] = l_run;
 #pragma unroll
@@ -618,7 +620,7 @@ __global__ void __launch_bounds__(kThreads * SPLIT) k_attn_st(AttnP p) {
     if (sp > 0) return;
 #pragma unroll
     for (int s2 = 1; s2 < SPLIT; ++s2) {
-      const float* rec = xs + (((s2 - 1) * 4 + wave) * 64 + lane) * REC;
+      const float* rec = xs + (((s2 - 1) * QW + wave) * 64 + lane) * REC;
       const float m2 = rec[0];
       const float m = fmaxf(m_run, m2);
       const float a1 = exp2f(m_run - m), a2 = exp2f(m2 - m);
@@ -681,11 +683,16 @@ extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
   else if (g_attn_variant == 1)
     k_attn_dma<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
   else if (g_attn_variant == 2)
-    k_attn_st<1, kStages><<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+    k_attn_st<4, 1, kStages><<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
   else if (g_attn_variant == 3)
-    k_attn_st<4, 2><<<grid, kThreads * 4, 0, s3::as_stream(stream)>>>(p);
-  else
-    k_attn_st<2, 2><<<grid, kThreads * 2, 0, s3::as_stream(stream)>>>(p);
+    k_attn_st<4, 4, 2><<<grid, kThreads * 4, 0, s3::as_stream(stream)>>>(p);
+  else if (g_attn_variant == 4) {
+    // 32-query workgroups (2 query waves): twice the workgroups per head
+    // (in-graph 0.83 vs 0.75 ms/frame for the default: not used)
+    dim3 g32((a->Nq + 31) / 32, a->B * a->H, a->groups);
+    k_attn_st<2, 2, 2><<<g32, 64 * 2 * 2, 0, s3::as_stream(stream)>>>(p);
+  } else
+    k_attn_st<4, 2, 2><<<grid, kThreads * 2, 0, s3::as_stream(stream)>>>(p);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

@@ -1,14 +1,14 @@
 // Tile-binned Gaussian splat rasterizer (include/gsr.h), written for gfx950.
 //
 // Forward:  preprocess (1 lane / Gaussian; per-workgroup reduction of the
-//           instance total and visible count fused in) -> stable depth sort
-//           of the P Gaussians (3 hand-written 11-bit LSD radix passes) ->
-//           tile binning: one stable counting pass over the instances by
-//           tile id, enumerated in depth order straight from the kept-tile
-//           masks (no instance key array, no second sort; tile ranges fall
-//           out of the scan) -> blend (one 256-lane workgroup per 16x16
+//           instance total and depth-key range fused in) -> stable depth
+//           sort of the P Gaussians (hand-written LSD radix passes of <= 9
+//           bits over the live key width) -> tile binning: duplication
+//           records gathered into depth order, instances emitted in depth
+//           order (wave-cooperative), a stable LSD sort of the instances by
+//           tile id, tile ranges -> blend (one 256-lane workgroup per 16x16
 //           tile, Gaussians staged through LDS in 256-record batches,
-//           block-wide early exit).
+//           block-wide early exit).  See "sorting" below.
 // Backward: per-tile back-to-front replay; per-Gaussian gradients are
 //           reduced across the wave with DPP/shuffles before one lane issues
 //           the global atomics (64x fewer atomics than one per pixel), then a

@@ -253,7 +253,7 @@ def test_attention_rope_vs_torch(B, N, Nk, H, cross):
                                                      (2, 100, 70, 4, 1, False),
                                                      (3, 5, 130, 2, 2, True),
                                                      (1, 200, 330, 3, 1, False)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_attention_no_rope_dma_path(B, N, Nk, H, groups, strided, variant):
     """The LDS-DMA ring kernel (q/k pre-rotated by the GEMM epilogue): plain
     softmax(QK^T s)V, K/V read from strided views like the fused QKV buffer."""
