@@ -296,25 +296,10 @@ def bench_map(dev, n=8_388_608, iters=5, warmup=2, seed=0):
     near 0.05 / far 100 (visualization.py:467-600).  Synthetic Gaussians in
     a 4 m x 2.5 m x 4 m room in front of the camera."""
     from splatt3r_amd.gaussian_map import SharedGaussians, render_map
-    g = torch.Generator(device=dev).manual_seed(seed)
+    from splatt3r_amd.synthetic import c5_map_batches
     gm = SharedGaussians(max_gaussians=n, device=dev)
-    chunk = 1 << 20
-    for s in range(0, n, chunk):
-        m = min(chunk, n - s)
-        u = lambda *sh: torch.rand(*sh, generator=g, device=dev)
-        means = (u(m, 3) - 0.5) * torch.tensor([4.0, 2.5, 4.0], device=dev) + \
-            torch.tensor([0.0, 0.0, 4.0], device=dev)
-        sc = torch.exp(torch.log(torch.tensor(0.004, device=dev)) + u(m, 3) * 2.0)
-        q = torch.nn.functional.normalize(torch.randn(m, 4, generator=g, device=dev), dim=1)
-        x, y, z, w = q.unbind(1)
-        R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
-                         2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
-                         2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)],
-                        1).reshape(m, 3, 3)
-        cov = torch.einsum("nik,nk,njk->nij", R, sc * sc, R)
-        iu = torch.triu_indices(3, 3, device=dev)
-        gm.append(means, cov[:, iu[0], iu[1]], u(m, 3), 0.35 + 0.65 * u(m), kf_idx=s // chunk,
-                  opacity_threshold=0.3)
+    for k, (means, cov, col, op) in enumerate(c5_map_batches(n, seed=seed, device=dev)):
+        gm.append(means, cov, col, op, kf_idx=k, opacity_threshold=0.3)
     out = {"map_gaussians": gm.n_gaussians, "image": "960x540", "vfov_deg": 45.0}
     T = np.eye(4, dtype=np.float32)
     import diff_gaussian_rasterization as dgr

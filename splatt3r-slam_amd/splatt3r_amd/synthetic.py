@@ -109,3 +109,28 @@ def tum_like_sequence(n: int, H: int = 384, W: int = 512, seed: int = 0, step_px
         ox = int(round(step_px * i)) + 4
         out[i, 0] = (texd[:, oy:oy + H, ox:ox + W] - 0.5) / 0.5
     return out
+
+
+def c5_map_batches(n: int, seed: int = 0, device="cuda", chunk: int = 1 << 20):
+    """C5 stand-in map content (bench.py bench_map, tests): n synthetic
+    world Gaussians in a 4 m x 2.5 m x 4 m room in front of an identity
+    camera, in keyframe-sized batches of `chunk` of the reference's
+    SharedGaussians.append arguments (means [m,3], cov_triu [m,6],
+    colours [m,3], opacities [m] >= 0.35, so the 0.3 filter keeps all)."""
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    iu = torch.triu_indices(3, 3, device=dev)
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        u = lambda *sh: torch.rand(*sh, generator=g, device=dev)
+        means = (u(m, 3) - 0.5) * torch.tensor([4.0, 2.5, 4.0], device=dev) + \
+            torch.tensor([0.0, 0.0, 4.0], device=dev)
+        sc = torch.exp(torch.log(torch.tensor(0.004, device=dev)) + u(m, 3) * 2.0)
+        q = torch.nn.functional.normalize(torch.randn(m, 4, generator=g, device=dev), dim=1)
+        x, y, z, w = q.unbind(1)
+        R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+                         2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                         2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)],
+                        1).reshape(m, 3, 3)
+        cov = torch.einsum("nik,nk,njk->nij", R, sc * sc, R)
+        yield means, cov[:, iu[0], iu[1]].contiguous(), u(m, 3), 0.35 + 0.65 * u(m)

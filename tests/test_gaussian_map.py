@@ -134,3 +134,54 @@ def test_hip_full_map_render_matches_reference_viz(parity):
     d = np.abs(own.astype(np.float64) - g["image_hwc"])
     parity("viz_full_map_render_own_camera", max_abs=d.max(), mean_l1=d.mean(), tol=1e-6)
     assert d.mean() <= 1e-6
+
+
+@pytest.mark.gpu
+def test_hip_c5_map_8m_append_evict_and_render_bitexact(parity):
+    """C5 at its own size: the 8,388,608-Gaussian map of bench.py bench_map
+    built through s3w_map_append in 1M keyframe batches (== the numpy
+    restatement MapRef, bit-exact), rendered full-map at 960x540 with the
+    viz camera == oracle.raster on the same scaled inputs (bit-exact), then
+    one more keyframe batch: FIFO half-eviction at capacity (== MapRef)."""
+    from splatt3r_amd.gaussian_map import SharedGaussians, VIZ_BG, render_map, viz_camera
+    from splatt3r_amd.synthetic import c5_map_batches
+    import oracle
+    n = 8_388_608
+    gm = SharedGaussians(max_gaussians=n, device="cuda")
+    ref = MapRef(n)
+    batches = list(c5_map_batches(n + (1 << 20), seed=0, device="cuda"))
+    h = lambda t: t.cpu().numpy()
+
+    def check(tag):
+        k = ref.n
+        assert gm.n_gaussians == k, tag
+        for name, a, b in (("means", gm.means, ref.means), ("cov", gm.cov_triu, ref.cov),
+                           ("colors", gm.colors, ref.colors), ("opac", gm.opacities, ref.opac),
+                           ("kf", gm.kf_id, ref.kf)):
+            np.testing.assert_array_equal(h(a[:k]), b[:k], err_msg=f"{tag} {name}")
+
+    for k, b in enumerate(batches[:-1]):
+        gm.append(*b, kf_idx=k, opacity_threshold=0.3)
+        ref.append(*(h(x) for x in b), kf_idx=k, thr=0.3)
+    check("filled")
+    T = np.eye(4, dtype=np.float32)
+    W_, H_ = 960, 540
+    cam = viz_camera(T, W_, H_, 45.0)
+    img = render_map(gm, T, W_, H_, 45.0, camera=cam, clamp=False).cpu().numpy()
+    tx, ty, view_t, proj, campos, s, s2 = cam
+    sd = dict(image_height=H_, image_width=W_, tanfovx=tx, tanfovy=ty,
+              bg=np.asarray(VIZ_BG, np.float32), scale_modifier=1.0,
+              viewmatrix=view_t.numpy().ravel(), projmatrix=proj.numpy().ravel(), sh_degree=0,
+              campos=campos.numpy().ravel())
+    out = oracle.raster(sd, ref.means[:n] * np.float32(s), ref.opac[:n].reshape(-1, 1),
+                        colors_precomp=ref.colors[:n], cov3D_precomp=ref.cov[:n] * np.float32(s2),
+                        nthreads=16)
+    import diff_gaussian_rasterization as dgr
+    parity("c5_full_map_render_8m", mismatched_px=float((img != out["color"]).sum()),
+           instances=dgr.last_num_rendered, oracle_instances=out["num_rendered"], tol=0.0)
+    np.testing.assert_array_equal(img, out["color"])
+    # one more keyframe at capacity: newest half to the front, then append
+    gm.append(*batches[-1], kf_idx=len(batches) - 1, opacity_threshold=0.3)
+    ref.append(*(h(x) for x in batches[-1]), kf_idx=len(batches) - 1, thr=0.3)
+    assert ref.n == n // 2 + (1 << 20)
+    check("evicted")
