@@ -69,7 +69,7 @@ inline int64_t nsegs(int64_t n) { return std::max<int64_t>(1, s3::cdiv(n, kSegIt
 struct GeomState {
   float* depth;
   float4* rec0;  // x, y, conic.a, conic.b
-  float4* rec1;  // conic.c, opacity, -, -
+  float4* rec1;  // conic.c, opacity, rgb.r, rgb.g (the blend's staged record)
   float* rgb;    // [P,3]
   float* cov3D;  // [P,6] (scale/rotation path)
   uint8_t* clamped;  // [P,3]
@@ -194,16 +194,20 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
              const float* __restrict__ vm, const float* __restrict__ pm,
              const float* __restrict__ campos, int32_t* __restrict__ radii, GeomState g,
              uint32_t* key_out) {
-  radii[i] = 0;
-  g.dup[i] = make_uint4(0u, 0u, 0u, 0u);
   // depth-sort key/value (fused here instead of a separate pass): culled
-  // Gaussians sort last and emit nothing
-  g.dkey[0][i] = 0xFFFFFFFFu;
+  // Gaussians sort last and emit nothing.  Every per-Gaussian output is
+  // stored once: a culled Gaussian's here, a kept one's at the end.
   g.dval[0][i] = (uint32_t)i;
+  auto cull = [&]() -> uint32_t {
+    radii[i] = 0;
+    g.dup[i] = make_uint4(0u, 0u, 0u, 0u);
+    g.dkey[0][i] = 0xFFFFFFFFu;
+    return 0u;
+  };
   const float mx = means[i * 3 + 0], my = means[i * 3 + 1], mz = means[i * 3 + 2];
   float pv[3];
   xform43(vm, mx, my, mz, pv);
-  if (pv[2] <= 0.2f) return 0u;  // in_frustum near-plane cull
+  if (pv[2] <= 0.2f) return cull();  // in_frustum near-plane cull
   float ph[4];
   xform44(pm, mx, my, mz, ph);
   const float pw = 1.0f / (ph[3] + 0.0000001f);
@@ -221,7 +225,7 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
   Ewa e = ewa_project(mx, my, mz, cov3, vm, cam.fx, cam.fy, cam.tanfx, cam.tanfy);
   const float a = e.a + 0.3f, b = e.b, c = e.c + 0.3f;
   const float det = a * c - b * b;
-  if (det == 0.0f) return 0u;
+  if (det == 0.0f) return cull();
   const float det_inv = 1.0f / det;
   const float mid = 0.5f * (a + c);
   const float disc = sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -230,7 +234,7 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
   const float px = ndc2pix(ppx, cam.W), py = ndc2pix(ppy, cam.H);
   int x0, y0, x1, y1;
   get_rect(px, py, r, cam.gx, cam.gy, &x0, &y0, &x1, &y1);
-  if ((x1 - x0) * (y1 - y0) == 0) return 0u;
+  if ((x1 - x0) * (y1 - y0) == 0) return cull();
 
   float rgb[3];
   if (colors_pre) {
@@ -255,7 +259,7 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
   g.depth[i] = pv[2];
   radii[i] = r;
   g.rec0[i] = make_float4(px, py, c * det_inv, -b * det_inv);
-  g.rec1[i] = make_float4(a * det_inv, opac[i], 0.0f, 0.0f);
+  g.rec1[i] = make_float4(a * det_inv, opac[i], rgb[0], rgb[1]);
   // tiles the blend can actually use (tile_hit); the reference lists every
   // tile of the rect, whose extra entries are all skipped per pixel
   // rects of <= 64 tiles: keep only the tiles the blend can use (tile_cull /
@@ -281,7 +285,6 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
   // ranks below `visible`; no finite depth reaches it)
   const uint32_t key = n > 0 ? min(__float_as_uint(pv[2]), 0xFFFFFFFEu) : 0xFFFFFFFFu;
   g.dkey[0][i] = key;
-  g.dval[0][i] = (uint32_t)i;
   *key_out = key;
   return n;
 }
@@ -809,9 +812,8 @@ k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
     const int prog = rd * BS + threadIdx.x;
     if ((int64_t)range.x + prog < range.y) {
       const uint32_t id = point_list[range.x + prog];
-      const float4 r1 = g.rec1[id];
       s_r0[threadIdx.x] = g.rec0[id];
-      s_r1[threadIdx.x] = make_float4(r1.x, r1.y, g.rgb[id * 3 + 0], g.rgb[id * 3 + 1]);
+      s_r1[threadIdx.x] = g.rec1[id];
       s_b[threadIdx.x] = g.rgb[id * 3 + 2];
     }
     __syncthreads();
@@ -986,10 +988,9 @@ k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ran
     const int prog = rd * BS + threadIdx.x;
     if (prog < todo_total) {
       const uint32_t id = point_list[end - prog - 1];
-      const float4 r1 = g.rec1[id];
       s_id[threadIdx.x] = id;
       s_r0[threadIdx.x] = g.rec0[id];
-      s_r1[threadIdx.x] = make_float4(r1.x, r1.y, g.rgb[id * 3 + 0], g.rgb[id * 3 + 1]);
+      s_r1[threadIdx.x] = g.rec1[id];
       s_b[threadIdx.x] = g.rgb[id * 3 + 2];
     }
 #pragma unroll

@@ -53,7 +53,7 @@ def main():
     for mod, names in ((su, ["splatt3r_asymmetric_inference", "_extract_gaussian_params"]),
                        (su.matching, ["match"]),
                        (trk.FrameTracker, ["_gn_finish"]),
-                       (sl, ["gaussians_to_world", "splatt3r_render"])):
+                       (sl, ["world_records", "splatt3r_render"])):
         for nm in names:
             wrap(mod, nm)
     fe.spans = []
