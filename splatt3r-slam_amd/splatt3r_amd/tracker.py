@@ -223,11 +223,14 @@ class FrameTracker:
         valid_opt = valid_match_k & valid_Cf & valid_Ck & valid_Q
         valid_kf = valid_match_k & valid_Q
         n = valid_opt.numel()
-        # unique(idx_f2k[valid_match_k]) counted without a host sync:
-        # mark the hit keyframe pixels, then count them
-        hit = torch.zeros(idx_f2k.shape[0], dtype=torch.uint8, device=idx_f2k.device)
-        hit.scatter_reduce_(0, idx_f2k, valid_match_k[:, 0].to(torch.uint8), "amax")
-        stats = torch.stack([valid_opt.sum(), valid_kf.sum(), hit.sum()]).to(torch.float64)
+        # unique(idx_f2k[valid_match_k]) counted without a host sync: mark
+        # the hit keyframe pixels (invalid matches mark a spare slot n; every
+        # write stores the same 1, so duplicates need no atomics), then the
+        # three counts in one reduction
+        vm = valid_match_k[:, 0]
+        hit = torch.zeros(n + 1, dtype=torch.bool, device=idx_f2k.device)
+        hit.index_fill_(0, torch.where(vm, idx_f2k, n), True)
+        stats = torch.stack([valid_opt.view(-1), valid_kf.view(-1), hit[:n]]).sum(1, dtype=torch.float64)
         stats_host = torch.empty(3, dtype=torch.float64, pin_memory=True)
         stats_host.copy_(stats, non_blocking=True)
         # queue the first GN chunk at the device-side relative pose, then one
