@@ -230,8 +230,8 @@ class FrameTracker:
         vm = valid_match_k[:, 0]
         hit = torch.zeros(n + 1, dtype=torch.bool, device=idx_f2k.device)
         hit.index_fill_(0, torch.where(vm, idx_f2k, n), True)
-        stats = torch.stack([valid_opt.view(-1), valid_kf.view(-1), hit[:n]]).sum(1, dtype=torch.float64)
-        stats_host = torch.empty(3, dtype=torch.float64, pin_memory=True)
+        stats = torch.stack([valid_opt.view(-1), valid_kf.view(-1), hit[:n]]).sum(1)
+        stats_host = torch.empty(3, dtype=torch.int64, pin_memory=True)
         stats_host.copy_(stats, non_blocking=True)
         # queue the first GN chunk at the device-side relative pose, then one
         # sync covers the decision statistics and (usually) the whole GN
