@@ -36,6 +36,10 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21,
                        int n, int fdim, int radius, int dilation_max,
                        void* stream);
 
+/* Tuning hook (not on the product path): lanes per query point of the
+ * cooperative refine kernel (8, 16 = default, 32, 64); results identical. */
+void s3m_refine_set_lanes(int lanes);
+
 /* Fused prep_for_iter_proj (matching.py:25-49 + image.py:5-38):
  * rays = normalize(X11); rays_with_grad = [rays, Scharr_x(rays)/32,
  * Scharr_y(rays)/32] with reflect padding; pts = normalize(X21);

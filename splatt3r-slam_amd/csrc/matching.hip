@@ -192,14 +192,15 @@ k_refine(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
 // score beats the maximum carried in from the previous levels.  The fp16
 // dot product keeps the reference's rounding of every product and partial
 // sum (v_mul_f16 / v_add_f16, no contraction in this file).
-constexpr int kRefLanes = 16;
-constexpr int kRefMaxPer = 4;   // candidates per lane -> (2r+1)^2 <= 64, r <= 3
-
-template <int F>
+// kRefLanes lanes per query point, kRefMaxPer = 64 / kRefLanes candidate
+// slots each -> (2r+1)^2 <= 64, r <= 3.  The result does not depend on the
+// split (ties resolve to the smallest candidate index).
+template <int F, int kRefLanes = 16>
 __global__ void __launch_bounds__(kBlock)
 k_refine_coop(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
               const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
               int n, int radius, int dilation_max) {
+  constexpr int kRefMaxPer = 64 / kRefLanes;
   static_assert(F % 8 == 0, "16-B descriptor chunks");
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   constexpr int NC = F / 8;
@@ -379,6 +380,13 @@ int s3m_iter_proj(const float* rays_img_with_grad, const float* pts_3d_norm,
   return S3_OK;
 }
 
+// lanes per query point of the cooperative refine (8, 16, 32, 64; tuning
+// hook, not on the product path)
+static int g_refine_lanes = 16;
+extern "C" void s3m_refine_set_lanes(int lanes) {
+  g_refine_lanes = (lanes == 8 || lanes == 32 || lanes == 64) ? lanes : 16;
+}
+
 int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
                        int64_t* p1_new, int b, int h, int w, int n, int fdim,
                        int radius, int dilation_max, void* stream) {
@@ -390,12 +398,20 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* 
   auto d11 = reinterpret_cast<const _Float16*>(D11);
   auto d21 = reinterpret_cast<const _Float16*>(D21);
   const int side = 2 * radius + 1;
-  if (side * side <= kRefLanes * kRefMaxPer && (fdim == 24 || fdim == 16 || fdim == 32)) {
-    dim3 cg((unsigned)s3::cdiv((int64_t)n * kRefLanes, kBlock), (unsigned)b);
+  if (side * side <= 64 && (fdim == 24 || fdim == 16 || fdim == 32)) {
+    const int lanes = g_refine_lanes;
+    dim3 cg((unsigned)s3::cdiv((int64_t)n * lanes, kBlock), (unsigned)b);
     auto go = [&](auto tag) {
       constexpr int F = decltype(tag)::value;
-      k_refine_coop<F><<<cg, kBlock, 0, s3::as_stream(stream)>>>(d11, d21, p1, p1_new, h, w, n,
-                                                               radius, dilation_max);
+      auto st = s3::as_stream(stream);
+      if (lanes == 8)
+        k_refine_coop<F, 8><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max);
+      else if (lanes == 32)
+        k_refine_coop<F, 32><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max);
+      else if (lanes == 64)
+        k_refine_coop<F, 64><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max);
+      else
+        k_refine_coop<F, 16><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max);
     };
     if (fdim == 24) go(std::integral_constant<int, 24>{});
     else if (fdim == 16) go(std::integral_constant<int, 16>{});

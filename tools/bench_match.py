@@ -24,6 +24,19 @@ def main():
     cfg["radius"] = 0
     us0 = timeit(lambda: matching.match_iterative_proj(X11, X21, D11, D21, cfg=cfg), reps=10)
     print(f"match without refine {us0:7.1f} us -> refine ~{us - us0:7.1f} us", flush=True)
+    import ctypes
+    from splatt3r_amd import _lib
+    L = _lib.lib()
+    L.s3m_refine_set_lanes.argtypes = [ctypes.c_int]
+    ref_idx = matching.match(X11, X21, D11, D21)[0].clone()
+    for lanes in (8, 16, 32, 64, 8, 16, 32, 64):
+        L.s3m_refine_set_lanes(lanes)
+        idx = matching.match(X11, X21, D11, D21)[0]
+        same = bool(torch.equal(idx, ref_idx))
+        us_l = timeit(lambda: matching.match(X11, X21, D11, D21), reps=10)
+        print(f"refine lanes {lanes:2d}: match {us_l:7.1f} us -> refine ~{us_l - us0:7.1f} us "
+              f"(idx identical: {same})", flush=True)
+    L.s3m_refine_set_lanes(16)
 
 
 if __name__ == "__main__":
