@@ -114,6 +114,11 @@ int s3n_gemm(const s3n_gemm_args* args, void* stream);
  * valid).  0 restores normal operation. */
 void s3n_gemm_set_debug(int flags);
 
+/* Tuning hook (not on the product path): 1 = place tiles on the 8 XCDs by
+ * the band split only (no 2-D partition of the tile grid); 0 = default.
+ * Results are identical either way (only the tile -> workgroup map moves). */
+void s3n_gemm_set_xcd_flags(int flags);
+
 /* Fused multi-head attention softmax(Q K^T * scale) V with 2-D RoPE
  * (pos_embed.py:142-159, base 100, F0 1) applied to Q and K on load.
  * Q rows at Q + (b*Nq + n)*q_stride + h*64, K/V likewise; O rows at

@@ -18,6 +18,8 @@
 // alone leaves one 4-wave workgroup per CU waiting on its DMA; KG groups give
 // each SIMD KG waves to overlap load latency with MFMA without the fp32
 // workspace round trip of a split-K launch.
+#include <algorithm>
+
 #include "common.hpp"
 #include "s3n.h"
 
@@ -28,6 +30,8 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kThreads = 256;
+// tuning hook s3n_gemm_set_xcd_flags: 1 = no 2-D XCD partition (band split only)
+int g_xcd_flags = 0;
 
 struct GemmP {
   int M, N, K, groups;
@@ -61,6 +65,7 @@ struct GemmP {
   int tail_n;
   int64_t ld_tail;
   int col_major;   // tile order: 1 = M fastest (each XCD owns a band of N)
+  int xcd_px;      // > 0: each XCD owns a (tiles_m / xcd_px) x (tiles_n * xcd_px / 8) block
   const float* rope_cos;
   const float* rope_sin;
   int rope_ncols;
@@ -570,11 +575,25 @@ k_gemm(GemmP p) {
 
   const int g = blockIdx.z;
   const int nwg = p.tiles_m * p.tiles_n;
-  const int tile = xcd_remap(blockIdx.x, nwg);
-  // xcd_remap gives each XCD a contiguous run of tile ids; the order makes
-  // that run share the larger operand (its slice stays in the XCD's L2).
-  const int tm = p.col_major ? tile % p.tiles_m : tile / p.tiles_n;
-  const int tn = p.col_major ? tile / p.tiles_m : tile % p.tiles_n;
+  int tm, tn;
+  if (p.xcd_px > 0) {
+    // 2-D XCD partition (host-checked divisibility, nwg % 8 == 0): XCD x
+    // (= blockIdx.x % 8 under round-robin dispatch) owns one block of the
+    // tile grid, so it reads 1/xcd_px of A and xcd_px/8 of B instead of all
+    // of one operand -- the L2-miss traffic of the operand that a band
+    // split leaves whole on every XCD
+    const int px = p.xcd_px, py = 8 / px;
+    const int xcd = blockIdx.x % 8, k = blockIdx.x / 8;
+    const int rm = p.tiles_m / px, rn = p.tiles_n / py;
+    tm = (xcd / py) * rm + k % rm;
+    tn = (xcd % py) * rn + k / rm;
+  } else {
+    const int tile = xcd_remap(blockIdx.x, nwg);
+    // xcd_remap gives each XCD a contiguous run of tile ids; the order makes
+    // that run share the larger operand (its slice stays in the XCD's L2).
+    tm = p.col_major ? tile % p.tiles_m : tile / p.tiles_n;
+    tn = p.col_major ? tile / p.tiles_m : tile % p.tiles_n;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -835,6 +854,20 @@ int launch(const GemmP& p, hipStream_t st) {
   const int64_t a_bytes = p.a_mode == S3N_A_DENSE ? (int64_t)p.M * p.K
                                                   : (int64_t)p.M / (p.oH * p.oW) * p.cH * p.cW * p.cC;
   q.col_major = (int64_t)p.N * p.K > a_bytes;
+  // 2-D XCD partition for dense A: the split px x (8 / px) of the tile grid
+  // that minimises the per-XCD operand reads 8 (A / px + B px / 8)
+  q.xcd_px = 0;
+  if (p.a_mode == S3N_A_DENSE && !(g_xcd_flags & 1)) {
+    const double A = (double)p.M * p.K, Bw = (double)p.N * p.K;
+    double best = A * 8 + Bw;   // the band split the fallback does (either way)
+    best = std::min(best, A + Bw * 8);
+    for (int px = 1; px <= 8; px *= 2) {
+      const int py = 8 / px;
+      if (q.tiles_m % px || q.tiles_n % py) continue;
+      const double c = 8.0 * (A / px + Bw / py);
+      if (c < best) { best = c; q.xcd_px = px; }
+    }
+  }
   dim3 grid(q.tiles_m * q.tiles_n, q.split_k, p.groups);
   if (p.a_mode == S3N_A_DENSE)
     k_gemm<BM, BN, NWM, NWN, kDense, S, BK, KG><<<grid, NT, 0, st>>>(q);
@@ -875,6 +908,7 @@ extern "C" int s3n_f16_saturations(int reset) {
   return (v ? 1 : 0) + l;
 }
 extern "C" void s3n_gemm_set_debug(int flags) { g_gemm_debug = flags; }
+extern "C" void s3n_gemm_set_xcd_flags(int flags) { g_xcd_flags = flags; }
 
 extern "C" size_t s3n_gemm_workspace_bytes(const s3n_gemm_args* a) {
   if (!a || a->split_k <= 1) return 0;

@@ -63,6 +63,7 @@ _lib.register({
     "s3n_gemm": (ctypes.c_int, [_GP, P]),
     "s3n_gemm_workspace_bytes": (ctypes.c_size_t, [_GP]),
     "s3n_gemm_set_debug": (None, [ctypes.c_int]),
+    "s3n_gemm_set_xcd_flags": (None, [ctypes.c_int]),
     "s3n_attention_set_variant": (None, [ctypes.c_int]),
     "s3n_attention": (ctypes.c_int, [_AP, P]),
     "s3n_layernorm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _PP, I64, _PP, _PP,
@@ -101,6 +102,10 @@ GRAPHS_ENABLED = os.environ.get("S3_GRAPHS", "1") != "0"
 # S3_ATTN_VARIANT=<n>: the no-RoPE attention kernel variant (net_attn.hip
 # s3n_attention_set_variant; experiments only)
 ATTN_VARIANT = int(os.environ["S3_ATTN_VARIANT"]) if "S3_ATTN_VARIANT" in os.environ else None
+# S3_GEMM_XCD=1: tiles placed on the XCDs by the band split only (A/B of the
+# 2-D XCD partition, net_gemm.hip; experiments only)
+if os.environ.get("S3_GEMM_XCD", "0") == "1":
+    _lib.lib().s3n_gemm_set_xcd_flags(1)
 
 
 def _ptr(x):
