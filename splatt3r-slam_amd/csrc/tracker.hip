@@ -341,3 +341,66 @@ extern "C" int s3t_gn_iterations_calib(const float* Xf, const float* Xk, const f
   }
   return S3_OK;
 }
+
+// ------------------------------------------------------------ track prep --
+// FrameTracker.track's correspondence filter (include/s3t.h s3t_track_prep):
+// gathers, the three validity masks and the decision counts in one pass.
+// Counts: wave ballots, one 64-bit atomic per wave and count (exact
+// integers, so the result does not depend on the order).  Unique hits: the
+// first writer of hit[j] (atomicExch returns 0) counts it.
+namespace {
+
+__global__ void __launch_bounds__(kThreads)
+k_track_prep(const int64_t* __restrict__ idx, const uint8_t* __restrict__ vm,
+             const float* __restrict__ Xf, const float* __restrict__ Cf,
+             const float* __restrict__ Ck, const float* __restrict__ Qff,
+             const float* __restrict__ Qkf, int64_t n, float C_conf, float Q_conf,
+             float* __restrict__ Xf_out, float* __restrict__ Q_out,
+             uint8_t* __restrict__ valid_opt, uint32_t* __restrict__ hit,
+             unsigned long long* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool vopt = false, vkf = false, uniq = false;
+  if (i < n) {
+    const int64_t j = idx[i];
+    const bool m = vm[i] != 0;
+    Xf_out[i * 3 + 0] = Xf[j * 3 + 0];
+    Xf_out[i * 3 + 1] = Xf[j * 3 + 1];
+    Xf_out[i * 3 + 2] = Xf[j * 3 + 2];
+    const float prod = Qff[j] * Qkf[i];
+    const float q = sqrtf(prod);
+    Q_out[i] = q;
+    const bool vq = q > Q_conf;
+    vopt = m && Cf[j] > C_conf && Ck[i] > C_conf && vq;
+    vkf = m && vq;
+    valid_opt[i] = vopt ? 1 : 0;
+    if (m) uniq = atomicExch(&hit[j], 1u) == 0u;
+  }
+  const unsigned long long b0 = __ballot(vopt), b1 = __ballot(vkf), b2 = __ballot(uniq);
+  if ((threadIdx.x & 63) == 0) {
+    if (b0) atomicAdd(&counts[0], (unsigned long long)__popcll(b0));
+    if (b1) atomicAdd(&counts[1], (unsigned long long)__popcll(b1));
+    if (b2) atomicAdd(&counts[2], (unsigned long long)__popcll(b2));
+  }
+}
+
+}  // namespace
+
+extern "C" int s3t_track_prep(const int64_t* idx, const uint8_t* vm, const float* Xf,
+                              const float* Cf, const float* Ck, const float* Qff,
+                              const float* Qkf, int64_t n, float C_conf, float Q_conf,
+                              float* Xf_out, float* Q_out, uint8_t* valid_opt, uint32_t* hit,
+                              int64_t* counts, void* stream) {
+  S3_REQUIRE(n >= 0, "s3t_track_prep: bad n");
+  S3_REQUIRE(n == 0 || (idx && vm && Xf && Cf && Ck && Qff && Qkf && Xf_out && Q_out &&
+                        valid_opt && hit && counts),
+             "s3t_track_prep: null operand");
+  hipStream_t st = s3::as_stream(stream);
+  if (counts) S3_HIP(hipMemsetAsync(counts, 0, 3 * sizeof(int64_t), st));
+  if (n == 0) return S3_OK;
+  S3_HIP(hipMemsetAsync(hit, 0, (size_t)n * sizeof(uint32_t), st));
+  k_track_prep<<<(unsigned)s3::cdiv(n, kThreads), kThreads, 0, st>>>(
+      idx, vm, Xf, Cf, Ck, Qff, Qkf, n, C_conf, Q_conf, Xf_out, Q_out, valid_opt, hit,
+      reinterpret_cast<unsigned long long*>(counts));
+  S3_LAUNCH_CHECK();
+  return S3_OK;
+}

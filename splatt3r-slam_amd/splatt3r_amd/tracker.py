@@ -40,7 +40,31 @@ _lib.register({
                                                ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                                ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                                ctypes.c_float, P_, P_, P_, P_, P_]),
+    "s3t_track_prep": (ctypes.c_int, [P_, P_, P_, P_, P_, P_, P_, ctypes.c_int64, ctypes.c_float,
+                                      ctypes.c_float, P_, P_, P_, P_, P_, P_]),
 })
+
+
+def track_prep(idx, vm, Xf, Cf, Ck, Qff, Qkf, C_conf, Q_conf):
+    """tracker.py:28-91's correspondence filter in one HIP pass
+    (include/s3t.h s3t_track_prep): returns (Xf[idx] [n,3], Qk =
+    sqrt(Qff[idx] * Qkf) [n,1], valid_opt [n,1] bool, counts int64 [3] =
+    (valid_opt.sum(), (vm & Qk > Q_conf).sum(), unique(idx[vm]).numel())),
+    all on the device, no host sync."""
+    n = idx.shape[0]
+    dev = idx.device
+    t = [x.contiguous() for x in (idx, vm, Xf.float(), Cf.float(), Ck.float(), Qff.float(),
+                                  Qkf.float())]
+    _lib.require_cuda(*t)
+    Xo = torch.empty(n, 3, device=dev)
+    Qo = torch.empty(n, 1, device=dev)
+    vo = torch.empty(n, 1, device=dev, dtype=torch.bool)
+    hit = torch.empty(n, device=dev, dtype=torch.int32)
+    cnt = torch.empty(3, device=dev, dtype=torch.int64)
+    _lib.call("s3t_track_prep", *(x.data_ptr() for x in t), n, float(C_conf), float(Q_conf),
+              Xo.data_ptr(), Qo.data_ptr(), vo.data_ptr(), hit.data_ptr(), cnt.data_ptr(),
+              _lib.stream(dev))
+    return Xo, Qo, vo, cnt
 GN_CHUNK = 8   # iterations queued per host check of the device-side GN state
 
 _TRIU = [(a, b) for a in range(7) for b in range(a, 7)]
@@ -206,7 +230,6 @@ class FrameTracker:
         self.idx_f2k = idx_f2k.clone()
         idx_f2k = idx_f2k[0]
         valid_match_k = valid_match_k[0]
-        Qk = torch.sqrt(Qff[idx_f2k] * Qkf)
         frame.update_pointmap(Xff, Cff)
 
         use_calib = config["use_calib"]
@@ -214,23 +237,14 @@ class FrameTracker:
         calib = None
         if use_calib:
             calib = (self._host_K(keyframe.K), img_size)
-        Xf, Xk, T_WCf, T_WCk, Cf, Ck = self.get_points_poses(frame, keyframe, idx_f2k, img_size,
-                                                             use_calib, keyframe.K)
-
-        valid_Cf = Cf > self.cfg["C_conf"]
-        valid_Ck = Ck > self.cfg["C_conf"]
-        valid_Q = Qk > self.cfg["Q_conf"]
-        valid_opt = valid_match_k & valid_Cf & valid_Ck & valid_Q
-        valid_kf = valid_match_k & valid_Q
+        Xf_all, Xk, T_WCf, T_WCk, Cf_all, Ck = self._points_poses_full(
+            frame, keyframe, img_size, use_calib, keyframe.K)
+        # gathers by idx_f2k, Qk = sqrt(Qff[idx] * Qkf), the valid_opt /
+        # valid_kf masks and the decision counts (incl. unique(idx[valid]))
+        # in one HIP pass, without a host sync
+        Xf, Qk, valid_opt, stats = track_prep(idx_f2k, valid_match_k, Xf_all, Cf_all, Ck, Qff,
+                                              Qkf, self.cfg["C_conf"], self.cfg["Q_conf"])
         n = valid_opt.numel()
-        # unique(idx_f2k[valid_match_k]) counted without a host sync: mark
-        # the hit keyframe pixels (invalid matches mark a spare slot n; every
-        # write stores the same 1, so duplicates need no atomics), then the
-        # three counts in one reduction
-        vm = valid_match_k[:, 0]
-        hit = torch.zeros(n + 1, dtype=torch.bool, device=idx_f2k.device)
-        hit.index_fill_(0, torch.where(vm, idx_f2k, n), True)
-        stats = torch.stack([valid_opt.view(-1), valid_kf.view(-1), hit[:n]]).sum(1)
         stats_host = torch.empty(3, dtype=torch.int64, pin_memory=True)
         stats_host.copy_(stats, non_blocking=True)
         # queue the first GN chunk at the device-side relative pose, then one
@@ -279,6 +293,16 @@ class FrameTracker:
             self._K_key = key
             self._K9 = np.ascontiguousarray(K.detach().float().cpu().numpy().reshape(9))
         return self._K9
+
+    def _points_poses_full(self, frame, keyframe, img_size=None, use_calib=False, K=None):
+        """get_points_poses before the gather by idx_f2k (track_prep gathers)."""
+        Xf = frame.X_canon
+        Xk = keyframe.X_canon
+        if use_calib:
+            from splatt3r_amd.geometry import constrain_points_to_ray
+            Xf = constrain_points_to_ray(img_size, Xf[None], K).squeeze(0)
+            Xk = constrain_points_to_ray(img_size, Xk[None], K).squeeze(0)
+        return Xf, Xk, frame.T_WC, keyframe.T_WC, frame.get_average_conf(), keyframe.get_average_conf()
 
     def get_points_poses(self, frame, keyframe, idx_f2k, img_size=None, use_calib=False, K=None):
         """tracker.py:129-154.  With use_calib both pointmaps are first

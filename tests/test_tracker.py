@@ -291,3 +291,31 @@ def test_calib_device_gn_matches_oracle_loop():
                                       _dev(K), (h, w))
     assert tr.last_iters == 3
     np.testing.assert_allclose(T_dev.data.cpu().numpy().reshape(8), T, atol=5e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,seed", [(196608, 0), (1000, 1), (63, 2)])
+def test_track_prep_matches_torch_reference_expressions(n, seed):
+    """s3t_track_prep == the reference's torch expressions (tracker.py:
+    28-91): gathers and masks exact, Qk = sqrt(Qff[idx] * Qkf) within one
+    ulp (device sqrt), the three decision counts exact (incl. the unique
+    count of hit keyframe pixels, with many duplicate matches)."""
+    from splatt3r_amd.tracker import track_prep
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    r = lambda *s: torch.rand(*s, device="cuda", generator=g)
+    idx = torch.randint(0, n, (n,), device="cuda", generator=g)
+    idx[: n // 3] = idx[0]                                   # duplicate hits
+    vm = r(n, 1) > 0.3
+    Xf = torch.randn(n, 3, device="cuda", generator=g)
+    Cf, Ck = r(n, 1) * 3, r(n, 1) * 3
+    Qff, Qkf = r(n, 1) * 4, r(n, 1) * 4
+    C_conf, Q_conf = 1.0, 1.5
+    Xo, Qo, vo, cnt = track_prep(idx, vm, Xf, Cf, Ck, Qff, Qkf, C_conf, Q_conf)
+    Qk = torch.sqrt(Qff[idx] * Qkf)
+    torch.testing.assert_close(Qo, Qk, rtol=2e-7, atol=0)
+    assert torch.equal(Xo, Xf[idx])
+    vq = Qo > Q_conf                                        # masks from the kernel's own Qk
+    vopt = vm & (Cf[idx] > C_conf) & (Ck > C_conf) & vq
+    assert torch.equal(vo, vopt)
+    ref = [int(vopt.sum()), int((vm & vq).sum()), int(torch.unique(idx[vm[:, 0]]).numel())]
+    assert cnt.cpu().tolist() == ref
