@@ -177,7 +177,7 @@ def load_prng(model, cfg, seed):
     man = W.manifest(cfg)
     assert [n for n, _ in man] == list(sd.keys()), "manifest order differs from the reference"
     assert all(tuple(sd[n].shape) == tuple(s) for n, s in man), "manifest shapes differ"
-    new = {n: torch.from_numpy(W.prng_tensor_numpy(seed, n, s)) for n, s in man}
+    new = {n: torch.from_numpy(W.prng_tensor_numpy(seed, n, s, cfg)) for n, s in man}
     model.load_state_dict(new)
     return man
 
@@ -546,6 +546,31 @@ N1_POSES = {
     "moved": ([0.1, -0.05, 0.2, 0.0499792, 0.0, 0.0, 0.99875026, 1.2],
               [0.13, -0.04, 0.15, 0.0499792, 0.0399893, 0.0, 0.99795, 1.2]),
 }
+# (tag, config, scale bias of weights.n1_init, H, W): the small config and
+# the full architecture at the C2 (384x512) and C4 (320x512) sizes
+N1_CASES = (("small_off", "small_off", -1.2, 48, 64), ("small_nooff", "small_nooff", -1.2, 48, 64),
+            ("full_384x512", "full", -2.5, 384, 512), ("full_320x512", "full", -2.5, 320, 512))
+N1_CONTRAST = 0.08
+N1_LOOKAT_BACK = 0.3
+N1_Q16 = 65535.0          # fp32 image -> uint16 quantum (mean error 3.8e-6)
+N1_DQ = float(2 ** 20)    # TF32-minus-fp32 image delta -> int16 quantum ~1e-6
+
+
+def n1_image(H, W, phase):
+    """The N1 input image: a smooth colour field of amplitude N1_CONTRAST
+    around mid-grey, as uint8 HxWx3 (a camera frame's type).  Low spatial
+    frequency, so splats that land next to each other carry similar
+    colours."""
+    yy, xx = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
+    ch = [0.5 + N1_CONTRAST * np.sin(5 * xx + 3 * yy + 2.1 * k + phase) * np.cos(2 * yy - xx + k)
+          for k in range(3)]
+    return np.round(np.stack(ch, -1) * 255).astype(np.uint8)
+
+
+def n1_normalise(u8):
+    """uint8 HxWx3 -> ImgNorm [1,3,H,W] float32 in [-1, 1] (dust3r/utils/image.py:23)."""
+    a = torch.from_numpy(u8.astype(np.float32) / np.float32(255.0)).permute(2, 0, 1)[None]
+    return ((a - 0.5) / 0.5).contiguous()
 
 
 def _look_at(means, back=1.0):
@@ -563,14 +588,21 @@ def _look_at(means, back=1.0):
 def gen_n1():
     """North-star N1 fixture: the reference pipeline's rendered RGB.
 
-    Reference head outputs (the committed net_small_* goldens, and the full
-    architecture at 384x512 re-run here with the net_full_384x512 inputs) go
-    through the reference glue exactly as splatt3r_render drives it
-    (splatt3r_utils.py:332-432: build_covariance, RGB2SH residual,
-    DecoderSplattingCUDA with default intrinsics f = max(h, w)), with a stub
-    rasterizer capturing what the glue hands GaussianRasterizer; the captured
-    inputs are rasterized by oracle.raster (the canonical graphdeco forward,
-    oracle/raster_ref.c).  Saved: the rendered [3,H,W] images + the poses."""
+    The reference network (imported modules, portable-PRNG weights with the
+    conditioned init of weights.n1_init: multi-pixel splats of varying scale,
+    the colour from the image) is run on smooth uint8 frames (n1_image), in
+    fp32 and with TF32-emulated matrix products (the reference CUDA path's
+    arithmetic, main.py:195); its head outputs go through the reference glue
+    exactly as splatt3r_render drives it (splatt3r_utils.py:332-432:
+    build_covariance, RGB2SH residual, DecoderSplattingCUDA with default
+    intrinsics f = max(h, w)), a stub rasterizer captures what the glue hands
+    GaussianRasterizer and oracle.raster (oracle/raster_ref.c) renders it.
+    Views: self, moved, look-at.  Saved: the frames, poses, images (fp32 as
+    uint16, the TF32 image as an int16 delta), subsampled head outputs of the
+    conditioned init (the scales check) and, for the small configs, the full
+    head outputs (the glue check).  Also kept: the default-init small
+    matching on TF32 outputs (tests/test_net.py)."""
+    import dataclasses
     import types
     sys.path.insert(0, os.path.dirname(HERE))
     import oracle
@@ -635,63 +667,374 @@ def gen_n1():
     keys = ("means", "scales", "rotations", "sh", "opacities")
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "splatt3r-slam_amd"))
     from splatt3r_amd import weights as W
-    import dataclasses
-    out = {}
-    cases = []
-    for tag, use_off in (("small_off", True), ("small_nooff", False)):
-        g = np.load(os.path.join(GOLDEN, f"net_{tag}.npz"))
-        im1, im2 = torch.from_numpy(g["img1"]), torch.from_numpy(g["img2"])
-        r1 = {k: torch.from_numpy(g["res1_" + k]) for k in keys}
-        r2 = {k: torch.from_numpy(g["res2_" + k]) for k in keys}
-        cfg = dataclasses.replace(W.SMALL, use_offsets=use_off)
+    out = {"contrast": np.float32(N1_CONTRAST), "lookat_back": np.float32(N1_LOOKAT_BACK),
+           "q16": np.float32(N1_Q16), "dq": np.float32(N1_DQ)}
+    # default-init small model: matching on the TF32 outputs (test_net.py)
+    g = np.load(os.path.join(GOLDEN, "net_small_off.npz"))
+    torch.manual_seed(0)
+    model = build_reference_model(dataclasses.replace(W.SMALL, use_offsets=True))
+    load_prng(model, dataclasses.replace(W.SMALL, use_offsets=True), seed=1234)
+    with tf32_mode():
+        _, _, _, _, _, t1, t2 = run_reference(model, torch.from_numpy(g["img1"]),
+                                              torch.from_numpy(g["img2"]))
+    idx_t, valid_t = oracle.match(t1["pts3d"].numpy(), t2["pts3d"].numpy(),
+                                  t1["desc"].numpy(), t2["desc"].numpy())
+    out["small_off_match_tf32_idx"] = idx_t
+    out["small_off_match_tf32_valid"] = valid_t
+    only = os.environ.get("N1_ONLY")          # experiments: a subset of the cases
+    sb_over = os.environ.get("N1_SMALL_BIAS")
+    for tag, kind, scale_bias, H, Wd in N1_CASES:
+        if only and tag not in only.split(","):
+            continue
+        if sb_over and kind != "full":
+            scale_bias = float(sb_over)
+        base = W.FULL if kind == "full" else dataclasses.replace(
+            W.SMALL, use_offsets=(kind == "small_off"))
+        cfg = W.n1_init(base, scale_bias)
         torch.manual_seed(0)
         model = build_reference_model(cfg)
         load_prng(model, cfg, seed=1234)
+        u1, u2 = n1_image(H, Wd, 0.0), n1_image(H, Wd, 0.4)
+        im1, im2 = n1_normalise(u1), n1_normalise(u2)
+        _, _, _, _, _, r1, r2 = run_reference(model, im1, im2)
         with tf32_mode():
             _, _, _, _, _, t1, t2 = run_reference(model, im1, im2)
-        cases.append((tag, r1, r2, t1, t2, im1, im2))
-        # matching on the TF32 reference outputs (splatt3r_match_asymmetric's
-        # idx/valid as the reference CUDA path would produce them)
-        idx_t, valid_t = oracle.match(t1["pts3d"].numpy(), t2["pts3d"].numpy(),
-                                      t1["desc"].numpy(), t2["desc"].numpy())
-        out[f"{tag}_match_tf32_idx"] = idx_t
-        out[f"{tag}_match_tf32_valid"] = valid_t
-    # full architecture at 384x512 (same inputs as net_full_384x512.npz)
-    torch.manual_seed(0)
-    model = build_reference_model(W.FULL)
-    load_prng(model, W.FULL, seed=1234)
-    g = torch.Generator().manual_seed(6)
-    img1 = torch.rand(1, 3, 384, 512, generator=g) * 2 - 1
-    img2 = torch.rand(1, 3, 384, 512, generator=g) * 2 - 1
-    full = np.load(os.path.join(GOLDEN, "net_full_384x512.npz"))
-    assert np.array_equal(full["img1"], img1.numpy())
-    _, _, _, _, _, r1, r2 = run_reference(model, img1, img2)
-    with tf32_mode():
-        _, _, _, _, _, t1, t2 = run_reference(model, img1, img2)
-    del model
-    cases.append(("full_384x512", r1, r2, t1, t2, img1, img2))
-    for tag, r1, r2, t1, t2, im1, im2 in cases:
+        del model
+        out[f"{tag}_u8img1"], out[f"{tag}_u8img2"] = u1, u2
+        out[f"{tag}_scale_bias"] = np.float32(scale_bias)
+        sub = (slice(None), slice(None, None, 8), slice(None, None, 8)) if kind == "full" \
+            else (slice(None),)
+        for i, r in ((1, r1), (2, r2)):
+            for k in keys + ("pts3d", "conf"):
+                out[f"{tag}_res{i}_{k}"] = r[k][sub].contiguous().numpy()
         poses = dict(N1_POSES)
-        # a target looking at view 1's point cloud from behind the origin
-        # (portable-PRNG weights put the full model's points outside the
-        # default frustum)
-        poses["lookat"] = ([0.0, 0, 0, 0, 0, 0, 1, 1], _look_at(r1["means"]))
+        poses["lookat"] = ([0.0, 0, 0, 0, 0, 0, 1, 1], _look_at(r1["means"], N1_LOOKAT_BACK))
         for pname, (Tc, Tt) in poses.items():
             img, nr = render(r1, r2, im1, im2, Tc, Tt)
             img_t, _ = render(t1, t2, im1, im2, Tc, Tt)
-            out[f"{tag}_{pname}_image"] = img
-            out[f"{tag}_{pname}_image_tf32"] = img_t
+            q = np.round(np.clip(img, 0, 1) * N1_Q16)
+            assert np.array_equal(np.clip(img, 0, 1), img), "bg 0 + alpha <= 1: image in [0, 1]"
+            out[f"{tag}_{pname}_image_u16"] = q.astype(np.uint16)
+            d = np.round((img_t.astype(np.float64) - q / N1_Q16) * N1_DQ)
+            out[f"{tag}_{pname}_tf32_delta"] = np.clip(d, -32767, 32767).astype(np.int16)
             out[f"{tag}_{pname}_ctx"] = np.float32(Tc)
             out[f"{tag}_{pname}_tgt"] = np.float32(Tt)
-            print(tag, pname, "num_rendered", nr, "mean", float(img.mean()),
-                  "covered", float((img.sum(0) > 0).mean()),
-                  "tf32-vs-fp32 mean-L1", float(np.abs(img - img_t).mean()))
-    np.savez_compressed(os.path.join(GOLDEN, "n1_render.npz"), **out)
+            dref = float(np.abs(img - img_t).mean())
+            print(tag, pname, "num_rendered", nr, "mean %.4f" % float(img.mean()),
+                  "covered %.3f" % float((img.sum(0) > 0).mean()),
+                  "tf32-vs-fp32 mean-L1 %.3e" % dref,
+                  "delta clipped", int((np.abs(d) > 32767).sum()), flush=True)
+    np.savez_compressed(os.environ.get("N1_OUT", os.path.join(GOLDEN, "n1_render.npz")), **out)
     del sys.modules["diff_gaussian_rasterization"]
     print("wrote n1_render.npz")
 
 
-SECTIONS = {"matching": gen_matching, "render": gen_render, "net": gen_net, "net_c4": gen_net_c4, "n1": gen_n1, "mono": gen_mono, "resize": gen_resize, "viz": gen_viz, "portrait": gen_portrait}
+# ------------------------------------------------------- host glue (AST) ---
+def _ast_defs(path, names, ns, cls=None):
+    """Compile the reference's own function (or, with `cls`, method) text
+    from `path` into namespace `ns` (the module itself does not import here:
+    lietorch / mast3r_slam_backends / cv2 are absent).  Decorators are
+    dropped (torch.inference_mode only)."""
+    import ast
+    tree = ast.parse(open(path).read())
+    body = tree.body
+    if cls is not None:
+        body = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == cls).body
+    fns = [n for n in body if isinstance(n, ast.FunctionDef) and n.name in names]
+    assert sorted(f.name for f in fns) == sorted(names), (path, names)
+    for f in fns:
+        f.decorator_list = []
+    exec(compile(ast.Module(body=fns, type_ignores=[]), path, "exec"), ns)
+    return ns
+
+
+def _reference_config():
+    """config/base.yaml through the reference's own loader
+    (splatt3r_slam/config.py, importable: yaml + re)."""
+    cfgmod = _load_file("ref_config", os.path.join(REF, "splatt3r_slam", "config.py"))
+    cwd = os.getcwd()
+    try:
+        os.chdir(REF)
+        cfgmod.load_config("config/base.yaml")
+    finally:
+        os.chdir(cwd)
+    return cfgmod.config
+
+
+class MatSim3:
+    """lietorch.Sim3 in matrix form (float64 4x4 [sR | t]) for driving the
+    reference's tracker / geometry text: act, inv, compose, matrix.  `retr`
+    records the GN step and keeps the pose (one normal-equation step is
+    what the fixture pins; lietorch's Exp is not importable)."""
+
+    def __init__(self, M):
+        self.M = M
+
+    @staticmethod
+    def from_data(T):
+        return MatSim3(_sim3_matrix(T)[0].double())
+
+    def act(self, p):
+        return p @ self.M[:3, :3].T + self.M[:3, 3]
+
+    def inv(self):
+        return MatSim3(torch.linalg.inv(self.M))
+
+    def __mul__(self, o):
+        return MatSim3(self.M @ o.M)
+
+    def retr(self, tau):
+        self.tau = tau
+        return self
+
+
+def gen_host():
+    """Fixtures for the host-side Python of the path, produced by running
+    the reference's own function text (AST-extracted) on synthetic inputs:
+
+      gaussians_to_world     splatt3r_utils.py:180-328 (+ _get_original_img_hwc
+                             :140-150; build_covariance / RGB2SH imported from
+                             splatt3r_core/utils; _sim3_to_4x4 -> MatSim3
+                             matrix, i.e. numpy in place of lietorch)
+      geometry               geometry.py:5-128 (point_to_ray_dist, act_Sim3,
+                             project_calib, constrain_points_to_ray, ...)
+      tracker GN step        tracker.py:129-270 (get_points_poses, solve,
+                             opt_pose_ray_dist_sim3, opt_pose_calib_sim3 with
+                             max_iters 1; H captured at the Cholesky)
+      add_factors            global_opt.py:30-99 with splatt3r_match_symmetric
+                             stubbed to fixed match tensors
+      match_iterative_proj   matching.py:8-90 with mast3r_slam_backends stubbed
+                             by the oracle kernels (oracle.iter_proj /
+                             refine_matches; the CUDA kernels do not compile)
+    -> tests/golden/host_glue.npz."""
+    import types
+    import einops
+    sys.path.insert(0, os.path.dirname(HERE))
+    import oracle
+    core = os.path.join(REF, "splatt3r_core")
+    geo_core = _load_file("ref_geometry_core", os.path.join(core, "utils", "geometry.py"))
+    shu = _load_file("ref_sh_utils", os.path.join(core, "utils", "sh_utils.py"))
+    nlo = _load_file("ref_nlo", os.path.join(REF, "splatt3r_slam", "nonlinear_optimizer.py"))
+    rimg = _load_file("ref_image", os.path.join(REF, "splatt3r_slam", "image.py"))
+    cfg = _reference_config()
+    out = {}
+
+    # ---- gaussians_to_world
+    ns = {"torch": torch, "einops": einops, "RGB2SH": shu.RGB2SH,
+          "build_covariance": geo_core.build_covariance,
+          "_sim3_to_4x4": lambda T: _sim3_matrix(T.data.reshape(-1)[:8].numpy())}
+    _ast_defs(os.path.join(REF, "splatt3r_slam", "splatt3r_utils.py"),
+              ["gaussians_to_world", "_get_original_img_hwc"], ns)
+    g2w = ns["gaussians_to_world"]
+
+    def pred(H, W, seed):
+        g = torch.Generator().manual_seed(seed)
+        q = torch.randn(1, H, W, 4, generator=g)
+        q = q / q.norm(dim=-1, keepdim=True)
+        means = torch.randn(1, H, W, 3, generator=g) * 0.5
+        means[..., 2] = torch.rand(1, H, W, generator=g) * 4 - 0.5
+        return dict(means=means, scales=torch.exp(torch.randn(1, H, W, 3, generator=g) - 2.5),
+                    rotations=q, sh=torch.randn(1, H, W, 3, 1, generator=g) * 0.3,
+                    opacities=torch.rand(1, H, W, 1, generator=g),
+                    conf=1 + torch.rand(1, H, W, generator=g) * 2)
+
+    G2W_CASES = ((48, 64, 4, True, 0.98, 1.0, 1.5), (48, 64, 1, False, 0.98, 0.5, 1.5),
+                 (37, 50, 3, True, 0.9, 0.3, 2.0), (40, 56, 2, False, 1.0, 10.0, 0.0))
+    for c, (H, W, stride, cross, q, maxs, minc) in enumerate(G2W_CASES):
+        p1, p2 = pred(H, W, 100 + c), pred(H, W, 200 + c)
+        img = torch.rand(1, 3, H, W, generator=torch.Generator().manual_seed(300 + c)) * 2.2 - 1.1
+        T = np.array([0.2, -0.1, 0.5, 0.0, np.sin(0.15), 0.0, np.cos(0.15), 1.3], np.float32)
+        fr = types.SimpleNamespace(gaussian_pred=p1, gaussian_pred_cross=p2, img=img,
+                                   T_WC=types.SimpleNamespace(data=torch.from_numpy(T)[None]))
+        res = g2w(fr, include_cross=cross, spatial_stride=stride, depth_max_percentile=q,
+                  max_scale=maxs, min_confidence=minc)
+        pre = f"g2w{c}_"
+        out[pre + "args"] = np.float64([H, W, stride, cross, q, maxs, minc])
+        out[pre + "T"] = T
+        out[pre + "img"] = img.numpy()
+        for k in p1:
+            out[pre + "p1_" + k] = p1[k].numpy()
+            out[pre + "p2_" + k] = p2[k].numpy()
+        for k, v in zip(("means", "cov", "colors", "opacities"), res):
+            out[pre + "out_" + k] = v.numpy()
+        print("gaussians_to_world case", c, "kept", res[0].shape[0])
+
+    # ---- geometry (float64)
+    gns = {"torch": torch, "lietorch": None}
+    _ast_defs(os.path.join(REF, "splatt3r_slam", "geometry.py"),
+              ["skew_sym", "point_to_dist", "point_to_ray_dist", "act_Sim3", "decompose_K",
+               "project_calib", "backproject", "get_pixel_coords", "constrain_points_to_ray"], gns)
+    rng = np.random.default_rng(7)
+    X = torch.from_numpy(np.concatenate([rng.uniform(-1, 1, (512, 2)),
+                                         rng.uniform(0.5, 4, (512, 1))], 1))
+    rd, J = gns["point_to_ray_dist"](X, jacobian=True)
+    out["geo_X"], out["geo_rd"], out["geo_rd_J"] = X.numpy(), rd.numpy(), J.numpy()
+    Td = np.array([0.1, -0.2, 0.3, 0.1, -0.05, 0.2, 0.0, 1.1])
+    Td[6] = np.sqrt(1 - np.sum(Td[3:6] ** 2))
+    pW, Ja = gns["act_Sim3"](MatSim3.from_data(Td), X, jacobian=True)
+    out["geo_T"], out["geo_act"], out["geo_act_J"] = np.float32(Td), pW.numpy(), Ja.numpy()
+    K = torch.tensor([[300.0, 0, 160.0], [0, 310.0, 120.0], [0, 0, 1]], dtype=torch.float64)
+    P = X.clone()
+    P[::17, 2] = -0.5                                     # behind the camera
+    pz, D, valid = gns["project_calib"](P, K, (240, 320), jacobian=True, border=-10, z_eps=1e-6)
+    out["geo_K"], out["geo_P"] = K.numpy(), P.numpy()
+    out["geo_pz"], out["geo_pz_J"], out["geo_pz_valid"] = pz.numpy(), D.numpy(), valid.numpy()
+
+    # ---- tracker: one normal-equation step, ray/dist and calibrated
+    tcfg = dict(cfg["tracking"], max_iters=1)
+    captured = {}
+
+    class TorchProxy(types.ModuleType):
+        def __getattr__(self, k):
+            return getattr(torch, k)
+
+    tp = TorchProxy("torch")
+    tp.linalg = types.SimpleNamespace(
+        cholesky=lambda H, upper=False: captured.setdefault("H", [H.clone()]) and
+        torch.linalg.cholesky(H, upper=upper), norm=torch.linalg.norm)
+    tns = dict(gns, torch=tp, huber=nlo.huber, check_convergence=nlo.check_convergence,
+               config={"tracking": tcfg})
+    _ast_defs(os.path.join(REF, "splatt3r_slam", "tracker.py"),
+              ["solve", "opt_pose_ray_dist_sim3", "opt_pose_calib_sim3", "get_points_poses"],
+              tns, cls="FrameTracker")
+    tracker = types.SimpleNamespace(cfg=tcfg)
+    for k in ("solve", "opt_pose_ray_dist_sim3", "opt_pose_calib_sim3", "get_points_poses"):
+        setattr(tracker, k, types.MethodType(tns[k], tracker))
+
+    def scene(n, seed, calib_hw=None):
+        r = np.random.default_rng(seed)
+        if calib_hw is None:
+            Xk = np.concatenate([r.uniform(-1, 1, (n, 2)), r.uniform(1, 4, (n, 1))], 1)
+        else:
+            h, w = calib_hw
+            v, u = np.divmod(np.arange(h * w), w)
+            z = r.uniform(1, 4, h * w)
+            Xk = np.stack([(u - w / 2) / (0.9 * max(h, w)) * z, (v - h / 2) / (0.9 * max(h, w)) * z,
+                           z], 1) + r.normal(size=(h * w, 3)) * 0.02
+            n = h * w
+        T_true = np.array([0.05, -0.02, 0.03, 0.02, -0.01, 0.015, 0.0, 1.02])
+        T_true[6] = np.sqrt(1 - np.sum(T_true[3:6] ** 2))
+        Xf = MatSim3.from_data(T_true).inv().act(torch.from_numpy(Xk)).numpy() \
+            + r.normal(size=(n, 3)) * 0.02
+        Q = r.uniform(0.5, 3.0, (n, 1))
+        valid = r.uniform(size=(n, 1)) > 0.1
+        return Xf, Xk, Q, valid
+
+    Ttr = np.array([0.01, 0.02, -0.01, 0.01, 0.0, -0.01, 0.0, 0.98])
+    Ttr[6] = np.sqrt(1 - np.sum(Ttr[3:6] ** 2))
+    Xf, Xk, Q, valid = scene(4096, 11)
+    captured.clear()
+    I = MatSim3.from_data(np.array([0, 0, 0, 0, 0, 0, 1, 1.0]))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    _, Tc = tracker.opt_pose_ray_dist_sim3(t(Xf), t(Xk), MatSim3.from_data(Ttr), I, t(Q),
+                                           t(valid))
+    H = captured["H"][0].numpy()
+    tau = Tc.tau.numpy().reshape(-1)
+    out.update(trk_ray_Xf=Xf, trk_ray_Xk=Xk, trk_ray_Q=Q, trk_ray_valid=valid,
+               trk_ray_T=np.float32(Ttr), trk_ray_H=H, trk_ray_g=H @ tau, trk_ray_tau=tau)
+    # calibrated: get_points_poses (constrain to rays, pixel grid + log z)
+    h, w = 24, 32
+    Xf, Xk, Q, valid = scene(0, 12, (h, w))
+    Kc = torch.tensor([[0.9 * 32, 0, 16.0], [0, 0.9 * 32, 12.0], [0, 0, 1]], dtype=torch.float64)
+    idx = np.random.default_rng(13).permutation(h * w)
+    frame = types.SimpleNamespace(X_canon=t(Xf), T_WC=MatSim3.from_data(Ttr),
+                                  get_average_conf=lambda: torch.ones(h * w, 1, dtype=torch.float64))
+    kf = types.SimpleNamespace(X_canon=t(Xk), T_WC=I,
+                               get_average_conf=lambda: torch.ones(h * w, 1, dtype=torch.float64))
+    Xf_c, Xk_c, T_WCf, T_WCk, _, _, meas, vmeas = tracker.get_points_poses(
+        frame, kf, t(idx), (h, w), True, Kc)
+    captured.clear()
+    _, Tc = tracker.opt_pose_calib_sim3(Xf_c, Xk_c, T_WCf, T_WCk, t(Q), t(valid), meas, vmeas, Kc,
+                                        (h, w))
+    H = captured["H"][0].numpy()
+    tau = Tc.tau.numpy().reshape(-1)
+    out.update(trk_cal_Xf=Xf, trk_cal_Xk=Xk, trk_cal_idx=idx, trk_cal_K=Kc.numpy(),
+               trk_cal_hw=np.int64([h, w]), trk_cal_Q=Q, trk_cal_valid=valid,
+               trk_cal_T=np.float32(Ttr), trk_cal_Xf_c=Xf_c.numpy(), trk_cal_Xk_c=Xk_c.numpy(),
+               trk_cal_meas=meas.numpy(), trk_cal_vmeas=vmeas.numpy(), trk_cal_H=H,
+               trk_cal_g=H @ tau)
+    print("tracker steps: |g| ray", np.abs(out["trk_ray_g"]).max(), "calib", np.abs(H @ tau).max())
+
+    # ---- add_factors (global_opt.py:30-99)
+    fns = {"torch": torch}
+    _ast_defs(os.path.join(REF, "splatt3r_slam", "global_opt.py"), ["add_factors"], fns,
+              cls="FactorGraph")
+    hh, ww, b = 12, 16, 4
+    r = np.random.default_rng(21)
+    dens = np.array([0.05, 0.6, 0.05, 0.3])          # pair 0 consecutive, pair 2 rejected
+    m = dict(idx_i2j=r.integers(0, hh * ww, (b, hh * ww)), idx_j2i=r.integers(0, hh * ww, (b, hh * ww)),
+             valid_j=r.uniform(size=(b, hh * ww, 1)) < dens[:, None, None],
+             valid_i=r.uniform(size=(b, hh * ww, 1)) < dens[:, None, None] + 0.05,
+             Qii=r.uniform(0.5, 3.5, (b, hh * ww, 1)), Qjj=r.uniform(0.5, 3.5, (b, hh * ww, 1)),
+             Qji=r.uniform(0.5, 3.5, (b, hh * ww, 1)), Qij=r.uniform(0.5, 3.5, (b, hh * ww, 1)))
+    m = {k: torch.from_numpy(v.astype(np.float32) if v.dtype == np.float64 else v)
+         for k, v in m.items()}
+    fns["splatt3r_match_symmetric"] = lambda *a: (m["idx_i2j"], m["idx_j2i"], m["valid_j"],
+                                                  m["valid_i"], m["Qii"], m["Qjj"], m["Qji"],
+                                                  m["Qij"])
+    ii, jj = [0, 0, 1, 2], [1, 2, 3, 4]
+    for k, v in m.items():
+        out["af_m_" + k] = v.numpy()
+    out["af_ii"], out["af_jj"] = np.int64(ii), np.int64(jj)
+    for case, reloc in (("add", False), ("reloc", True)):
+        L = lambda dt: torch.as_tensor([], dtype=dt)
+        fg = types.SimpleNamespace(
+            model=None, device="cpu", cfg=cfg["local_opt"],
+            frames=[types.SimpleNamespace(feat=torch.zeros(1, 2, 4), pos=torch.zeros(1, 2, 2),
+                                          img_true_shape=torch.tensor([[hh, ww]]))] * 5,
+            ii=L(torch.long), jj=L(torch.long), idx_ii2jj=L(torch.long), idx_jj2ii=L(torch.long),
+            valid_match_j=L(torch.bool), valid_match_i=L(torch.bool),
+            Q_ii2jj=L(torch.float32), Q_jj2ii=L(torch.float32))
+        ret = fns["add_factors"](fg, ii, jj, cfg["local_opt"]["min_match_frac"], is_reloc=reloc)
+        out[f"af_{case}_ret"] = np.bool_(bool(ret))
+        for k in ("ii", "jj", "idx_ii2jj", "idx_jj2ii", "valid_match_j", "valid_match_i",
+                  "Q_ii2jj", "Q_jj2ii"):
+            out[f"af_{case}_{k}"] = getattr(fg, k).numpy()
+        print("add_factors", case, "->", bool(ret), "edges", getattr(fg, "ii").tolist())
+
+    # ---- match_iterative_proj glue (matching.py:8-90)
+    def iter_proj(rays, pts, p_init, max_iter, lam, thr):
+        p, c = oracle.iter_proj(rays.numpy(), pts.numpy(), p_init.numpy(), max_iter, lam, thr)
+        return [torch.from_numpy(p), torch.from_numpy(c)]
+
+    def refine(D11, D21, p1, radius, dil):
+        return [torch.from_numpy(oracle.refine_matches(D11.numpy(), D21.numpy(), p1.numpy(),
+                                                       radius, dil))]
+
+    mns = {"torch": torch, "F": F, "img_utils": rimg, "config": cfg,
+           "mast3r_slam_backends": types.SimpleNamespace(iter_proj=iter_proj,
+                                                         refine_matches=refine)}
+    _ast_defs(os.path.join(REF, "splatt3r_slam", "matching.py"),
+              ["match", "pixel_to_lin", "lin_to_pixel", "prep_for_iter_proj",
+               "match_iterative_proj"], mns)
+    for c, (b, h, w, init) in enumerate(((2, 48, 64, False), (1, 40, 56, True))):
+        r = np.random.default_rng(40 + c)
+        v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+        X11 = np.stack([(u - w / 2) / w * 2, (v - h / 2) / w * 2, 2 + 0.3 * np.sin(u / 7.0)], -1)
+        X11 = np.repeat(X11[None], b, 0) + r.normal(size=(b, h, w, 3)) * 0.002
+        X21 = np.roll(X11, (1, 2), axis=(1, 2)) + r.normal(size=(b, h, w, 3)) * 0.002
+        D11 = r.normal(size=(b, h, w, 24))
+        D11 /= np.linalg.norm(D11, axis=-1, keepdims=True)
+        D21 = np.roll(D11, (1, 2), axis=(1, 2)) + r.normal(size=(b, h, w, 24)) * 0.3
+        D21 /= np.linalg.norm(D21, axis=-1, keepdims=True)
+        X11, X21, D11, D21 = (a.astype(np.float32) for a in (X11, X21, D11, D21))
+        idx0 = None
+        if init:
+            idx0 = torch.from_numpy(np.clip(np.arange(h * w) + r.integers(-3, 4, h * w), 0,
+                                            h * w - 1)[None].repeat(b, 0))
+        idx, valid = mns["match"](t(X11), t(X21), t(D11), t(D21), idx0)
+        pre = f"mt{c}_"
+        out.update({pre + "X11": X11, pre + "X21": X21, pre + "D11": D11, pre + "D21": D21,
+                    pre + "idx": idx.numpy(), pre + "valid": valid.numpy()})
+        if idx0 is not None:
+            out[pre + "idx_init"] = idx0.numpy()
+        print("match case", c, "valid frac", float(valid.float().mean()),
+              "identity frac", float((idx.numpy() == np.arange(h * w)).mean()))
+    np.savez_compressed(os.path.join(GOLDEN, "host_glue.npz"), **out)
+    print("wrote host_glue.npz")
+
+
+SECTIONS = {"host": gen_host, "matching": gen_matching, "render": gen_render, "net": gen_net, "net_c4": gen_net_c4, "n1": gen_n1, "mono": gen_mono, "resize": gen_resize, "viz": gen_viz, "portrait": gen_portrait}
 
 
 def main(argv):

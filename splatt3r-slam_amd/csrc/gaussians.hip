@@ -249,12 +249,17 @@ k_map_flags(int64_t n_max, const float* __restrict__ rec, const int64_t* __restr
   flags[i] = (i < *count && rec[i * 13 + 12] > thr) ? 1u : 0u;
 }
 
-// grid-stride: every block copies a slice of the newest half when full
+// grid-stride: every block copies a slice of the newest half when full.
+// A batch with no record left after the opacity filter (or a device count
+// of 0) leaves the map untouched: frame.py:414-416 returns before the
+// eviction when n_new == 0.
 __global__ void __launch_bounds__(kThreads)
-k_map_evict(s3w_map m, int64_t* __restrict__ n0) {
+k_map_evict(s3w_map m, int64_t n_max, const uint32_t* __restrict__ flags,
+            const uint32_t* __restrict__ offsets, int64_t* __restrict__ n0) {
   const int64_t n = *m.n;
   const int64_t half = m.cap / 2;
-  const bool full = n >= m.cap;
+  const int64_t kept = (int64_t)offsets[n_max - 1] + flags[n_max - 1];
+  const bool full = n >= m.cap && kept > 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *n0 = full ? half : n;
   if (!full) return;
   const int64_t src = m.cap - half;
@@ -335,7 +340,7 @@ extern "C" int s3w_map_append(const s3w_map* map, const float* records, const in
   S3_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, sb, w.flags, w.offsets, (int)n_max, st));
   const int64_t half = map->cap / 2;
   const int eb = (int)std::max<int64_t>(1, std::min<int64_t>(s3::cdiv(half, kThreads), 2048));
-  k_map_evict<<<eb, kThreads, 0, st>>>(*map, w.n0);
+  k_map_evict<<<eb, kThreads, 0, st>>>(*map, n_max, w.flags, w.offsets, w.n0);
   S3_LAUNCH_CHECK();
   k_map_emit<<<blocks, kThreads, 0, st>>>(n_max, *map, records, w.flags, w.offsets, w.n0,
                                           kf_idx);

@@ -125,6 +125,11 @@ class Backend:
                 self._q.task_done()
                 return
             idx, ready = item
+            # keyframe reads on this thread are stream-safe snapshots and pose
+            # writes are handed to the frontend's stream (frame.Keyframes);
+            # registered per task: the frontend may attach its keyframe list
+            # after the worker started
+            self.keyframes.register_reader(self._stream)
             try:
                 with torch.cuda.stream(self._stream), torch.inference_mode():
                     self._stream.wait_event(ready)
@@ -147,6 +152,7 @@ class Backend:
         if self._q is not None:
             self._q.join()
             torch.cuda.current_stream(self.device).wait_stream(self._stream)
+            self.keyframes.apply_pending(wait=True)
         if self._err is not None:
             e, self._err = self._err, None
             raise e

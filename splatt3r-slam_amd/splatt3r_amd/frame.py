@@ -9,7 +9,9 @@ cross-GPU exchange is an explicit RCCL collective (splatt3r_amd/pairs.py).
 """
 from __future__ import annotations
 
+import copy
 import dataclasses
+import threading
 from enum import Enum
 from typing import Optional
 
@@ -136,20 +138,128 @@ def create_frame(i, img, T_WC=None, img_size=512, device="cuda:0"):
 
 
 class Keyframes:
-    """List-backed stand-in for SharedKeyframes (frame.py:240-330)."""
+    """List-backed stand-in for SharedKeyframes (frame.py:240-330).
+
+    The reference shares keyframes between the frontend and the backend
+    process through shared-memory buffers guarded by a lock
+    (frame.py:269-330): a reader copies out a consistent keyframe, the
+    backend writes optimised poses back in place.  Here both sides are
+    threads of one process issuing HIP work on different streams, so the
+    same contract is kept with stream-ordered handoffs:
+
+      * the owner (frontend) mutates a keyframe under `lock` and publishes
+        it (`append` / `__setitem__`), which records a ready event on its
+        stream after the producing kernels;
+      * a registered reader thread (the backend worker, `register_reader`)
+        gets a shallow snapshot from `__getitem__`, taken under the lock: its
+        stream waits on the keyframe's ready event, and every tensor it can
+        read is `record_stream`-ed onto the reader's stream, so the caching
+        allocator cannot hand a block the frontend has since replaced to new
+        work while the reader's kernels still read it;
+      * poses written by the reader (`set_poses`) are queued with an event on
+        the reader's stream and applied by the owner in `apply_pending`
+        (start of each frontend step, and `Backend.wait`): the owner's
+        stream waits on that event and the new pose tensors are
+        `record_stream`-ed onto the owner's stream.
+    Single-thread use (no reader registered) is a plain list.
+    """
+
+    _SNAP_FIELDS = ("img", "X_canon", "C", "feat", "pos")
 
     def __init__(self):
         self._kf: list = []
         self.K: Optional[torch.Tensor] = None
+        self.lock = threading.RLock()
+        self._readers: dict = {}       # thread id -> reader stream
+        self._pending: list = []       # [(indices, pose rows [n,8], event)]
 
     def __len__(self):
         return len(self._kf)
 
+    # ------------------------------------------------ stream handoffs ----
+    def register_reader(self, stream):
+        """Called on the reader (backend worker) thread with its stream."""
+        self._readers[threading.get_ident()] = stream
+
+    def _reader_stream(self):
+        return self._readers.get(threading.get_ident()) if self._readers else None
+
+    @staticmethod
+    def _ready_event(frame):
+        if frame.img is not None and frame.img.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(frame.img.device))
+            frame._kf_ready = ev
+
+    def _snapshot(self, kf, stream):
+        with self.lock:
+            snap = copy.copy(kf)
+            ev = getattr(kf, "_kf_ready", None)
+        if ev is not None:
+            stream.wait_event(ev)
+        for name in self._SNAP_FIELDS:
+            t = getattr(snap, name)
+            if torch.is_tensor(t) and t.is_cuda:
+                t.record_stream(stream)
+        if snap.T_WC is not None and snap.T_WC.data.is_cuda:
+            snap.T_WC.data.record_stream(stream)
+        return snap
+
+    def set_poses(self, indices, poses: torch.Tensor):
+        """Write keyframe poses [n, 8] (lietorch layout).  From a reader
+        thread the write is deferred to the owner's `apply_pending`."""
+        stream = self._reader_stream()
+        if stream is None:
+            with self.lock:
+                for r, i in enumerate(indices):
+                    self._kf[int(i)].T_WC = lietorch.Sim3(poses[r:r + 1].clone())
+            return
+        rows = poses.clone()
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        with self.lock:
+            self._pending.append(([int(i) for i in indices], rows, ev))
+
+    def apply_pending(self, wait: bool = False) -> int:
+        """Owner side: install the reader's finished pose writes (all of them
+        when `wait`, else those whose event has completed, in order)."""
+        if not self._pending:
+            return 0
+        done = 0
+        with self.lock:
+            while self._pending:
+                idx, rows, ev = self._pending[0]
+                if not wait and not ev.query():
+                    break
+                self._pending.pop(0)
+                cur = torch.cuda.current_stream(rows.device)
+                cur.wait_event(ev)
+                rows.record_stream(cur)
+                for r, i in enumerate(idx):
+                    if i < len(self._kf):
+                        self._kf[i].T_WC = lietorch.Sim3(rows[r:r + 1])
+                        self._ready_event(self._kf[i])
+                done += 1
+        return done
+
+    # ------------------------------------------------------- accessors ----
     def __getitem__(self, i) -> Frame:
         kf = self._kf[i]
         if self.K is not None:
             kf.K = self.K      # frame.py:295 (SharedKeyframes.__getitem__)
-        return kf
+        stream = self._reader_stream()
+        if stream is None:
+            return kf
+        snap = self._snapshot(kf, stream)
+        # the reader's own pose writes not yet installed by the owner are
+        # what it sees (the reference backend reads back what it wrote)
+        i = i % len(self._kf) if isinstance(i, int) else int(i)
+        with self.lock:
+            for idx, rows, _ in reversed(self._pending):
+                if i in idx:
+                    snap.T_WC = lietorch.Sim3(rows[idx.index(i):idx.index(i) + 1])
+                    break
+        return snap
 
     def set_intrinsics(self, K: torch.Tensor):
         """frame.py:346-349 (use_calib only)."""
@@ -159,16 +269,22 @@ class Keyframes:
         return self.K
 
     def __setitem__(self, i, frame: Frame):
-        self._kf[i] = frame
+        with self.lock:
+            self._kf[i] = frame
+            self._ready_event(frame)
 
     def append(self, frame: Frame):
-        self._kf.append(frame)
+        with self.lock:
+            self._kf.append(frame)
+            self._ready_event(frame)
 
     def pop_last(self):
-        self._kf.pop()
+        with self.lock:
+            self._kf.pop()
 
     def last_keyframe(self) -> Optional[Frame]:
         return self[len(self._kf) - 1] if self._kf else None
 
     def get_poses(self) -> lietorch.Sim3:
-        return lietorch.Sim3(torch.cat([k.T_WC.data.reshape(1, 8) for k in self._kf]))
+        return lietorch.Sim3(torch.cat([self[i].T_WC.data.reshape(1, 8)
+                                        for i in range(len(self._kf))]))

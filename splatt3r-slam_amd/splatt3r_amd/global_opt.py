@@ -100,6 +100,18 @@ class FactorGraph:
         Cs = torch.stack([k.get_average_conf() for k in kfs])
         return Xs, T_WCs, Cs
 
+    def _publish(self, unique, pose_data, pin):
+        """global_opt.py:155-158 / :211-215: write the optimised poses back
+        (through Keyframes.set_poses: deferred to the frontend's stream when
+        this runs on the backend worker thread)."""
+        idx = unique[pin:].tolist()
+        rows = pose_data[pin:]
+        if hasattr(self.frames, "set_poses"):
+            self.frames.set_poses(idx, rows)
+            return
+        for r, i in enumerate(idx):
+            self.frames[i].T_WC = lietorch.Sim3(rows[r:r + 1].clone())
+
     def solve_GN_rays(self):
         """global_opt.py:121-158."""
         pin = self.cfg["pin"]
@@ -114,8 +126,7 @@ class FactorGraph:
             jj.contiguous(), idx.contiguous(), valid.contiguous(), Q.contiguous().float(),
             self.cfg["sigma_ray"], self.cfg["sigma_dist"], self.cfg["C_conf"],
             self.cfg["Q_conf"], self.cfg["max_iters"], self.cfg["delta_norm"])
-        for k in range(pin, unique.numel()):
-            self.frames[int(unique[k])].T_WC = lietorch.Sim3(pose_data[k:k + 1].clone())
+        self._publish(unique, pose_data, pin)
         return dx
 
     def solve_GN_calib(self):
@@ -139,6 +150,5 @@ class FactorGraph:
             self.cfg["depth_eps"], self.cfg["sigma_pixel"], self.cfg["sigma_depth"],
             self.cfg["C_conf"], self.cfg["Q_conf"], self.cfg["max_iters"],
             self.cfg["delta_norm"])
-        for k in range(pin, unique.numel()):
-            self.frames[int(unique[k])].T_WC = lietorch.Sim3(pose_data[k:k + 1].clone())
+        self._publish(unique, pose_data, pin)
         return dx

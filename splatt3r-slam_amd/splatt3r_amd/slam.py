@@ -199,6 +199,7 @@ class Frontend:
             a = self.gs_args
             T = _sim3_to_4x4(frame.T_WC)[0].to(frame.img.device)
             pred = frame.gaussian_pred
+            total = None
             for b in range(pred["means"].shape[0]):
                 view = {k: v[b] for k, v in pred.items()}
                 rec, cnt = world_records(view, frame.img[min(b, frame.img.shape[0] - 1)], T,
@@ -206,7 +207,12 @@ class Frontend:
                                          a["depth_max_percentile"], a["max_scale"],
                                          a["min_confidence"])
                 self.gmap.append_records(rec, cnt, kf_idx, self.map_opacity_threshold)
-            return True
+                total = cnt if total is None else total + cnt
+            # gaussians_to_world returns None when every view's records were
+            # filtered out (splatt3r_utils.py:318-319); the caller then does
+            # not record the append (main.py:424-435).  One host read of the
+            # device count, in viz mode only.
+            return True if total is not None and int(total.item()) > 0 else None
         # viz off: the reference computes gaussians_to_world and drops the
         # result (main.py:467-488); the same records are computed here and
         # kept on the device with their device count (frame.gs_world), so
@@ -279,6 +285,9 @@ class Frontend:
     def _step(self, i: int, img, next_img=None, e0=None) -> Frame:
         if self.fps_timer is None:
             self.fps_timer = time.time()
+        # keyframe poses the backend worker has finished optimising
+        # (SharedKeyframes' in-place writes, frame.py:269-330)
+        self.keyframes.apply_pending()
         T_WC = (lietorch.Sim3.Identity(1, device=self.device) if self.last_T_WC is None
                 else self.last_T_WC)
         frame = self._take_prefetched(i, T_WC)
@@ -306,6 +315,7 @@ class Frontend:
             e0[0] = self._event()
         self._stats["frames"] += 1
         add_new_kf = False
+        T_state = frame.T_WC
         if self.mode == Mode.INIT:
             X, C = splatt3r_inference_mono(self.model, frame)
             frame.update_pointmap(X, C)
@@ -323,6 +333,10 @@ class Frontend:
             hook = self._speculate(frame, self.keyframes.last_keyframe()) if self.gmap is None \
                 else None
             add_new_kf, _, try_reloc = self.tracker.track(frame, before_sync=hook)
+            # states.set_frame(frame) (main.py:455): the next frame starts from
+            # the tracked pose, not from what the backend later writes into
+            # the keyframe (the same object here, a shared-memory copy there)
+            T_state = frame.T_WC
             spec = self.tracker.spec if (self.tracker.spec_valid and not try_reloc) else None
             if pending is not None:
                 self._prefetch(*pending)
@@ -350,6 +364,7 @@ class Frontend:
             # from an unverified pose)
             X, C = splatt3r_inference_mono(self.model, frame)
             frame.update_pointmap(X, C)
+            T_state = frame.T_WC                  # states.set_frame (main.py:511)
             self._stats["reloc"] += 1
             if self.backend is not None:
                 self.backend.wait()
@@ -364,5 +379,5 @@ class Frontend:
             self._stats["keyframes"] += 1
             self.tracker.reset_idx_f2k()
             self._kf_added(frame)
-        self.last_T_WC = frame.T_WC
+        self.last_T_WC = T_state
         return frame

@@ -274,8 +274,11 @@ class FrameTracker:
         frame.T_WC = T_WCf
 
         Xkk = T_CkCf.act(Xkf)
-        keyframe.update_pointmap(Xkk, Ckf)
-        self.keyframes[len(self.keyframes) - 1] = keyframe
+        # under the keyframe lock: a backend reader snapshots either the old
+        # or the new (X_canon, C, N), with a ready event covering the fusion
+        with self.keyframes.lock:
+            keyframe.update_pointmap(Xkk, Ckf)
+            self.keyframes[len(self.keyframes) - 1] = keyframe
 
         match_frac_k = n_kf / n
         unique_frac_f = n_unique / n

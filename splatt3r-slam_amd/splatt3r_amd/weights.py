@@ -43,6 +43,14 @@ class NetConfig:
     layer_dims: tuple = (96, 192, 384, 768)
     rope_base: float = 100.0
     ln_eps: float = 1e-6
+    # portable-PRNG init of the two final 1x1 convs (not architecture):
+    # (channels, xavier gain, bias) per split of the Gaussian head's final
+    # conv, and an optional constant added to the pts head's x, y, z bias.
+    # The defaults are the reference init (catmlp_dpt_head.py:222-238);
+    # N1_INIT is the conditioned variant of the N1 render fixture.
+    gauss_splits: tuple = ((3, 0.001, 0.001), (3, 0.00003, -7.0), (4, 1.0, 0.0),
+                           (3, 1.0, 0.0), (1, 1.0, -2.0))
+    pts_bias: tuple = None
 
     @property
     def hooks(self):  # catmlp_dpt_head.py:317
@@ -58,6 +66,21 @@ FULL = NetConfig()
 # The reduced configuration the golden fixtures use (dec_depth > 9 is
 # asserted by the reference head factory; head_dim stays 64).
 SMALL = NetConfig(enc_dim=128, enc_depth=2, enc_heads=2, dec_dim=128, dec_depth=12, dec_heads=2)
+
+
+def n1_init(cfg: NetConfig, scale_bias: float) -> NetConfig:
+    """The N1 render fixture's init (oracle/gen_golden.py `n1`):
+    with the reference init the Gaussian head's scales are a constant e^-7
+    (xavier gain 3e-5, bias -7: sub-pixel splats, opacity sigmoid(-2)) and
+    the rendered image is a step function of the means.  Trained weights
+    give multi-pixel, varying splats; this init gets there with the same
+    PRNG streams: scale gain 0.2 and bias `scale_bias` (per resolution:
+    splats of ~10-30 px), SH residual gain 0.05 (the colour comes from the
+    image, as after training), opacity bias 0, and +0.3 on the pts head's
+    z bias (points in front of the camera)."""
+    return dataclasses.replace(
+        cfg, gauss_splits=((3, 0.001, 0.001), (3, 0.2, scale_bias), (4, 1.0, 0.0),
+                           (3, 0.05, 0.0), (1, 1.0, 0.0)), pts_bias=(0.0, 0.0, 0.3))
 
 
 # ------------------------------------------------------------ manifest ----
@@ -191,16 +214,22 @@ def _fans(shape):
 
 # final Gaussian conv: (channels, xavier gain, bias) per split,
 # catmlp_dpt_head.py:222-238
-GAUSS_SPLITS = ((3, 0.001, 0.001), (3, 0.00003, -7.0), (4, 1.0, 0.0), (3, 1.0, 0.0), (1, 1.0, -2.0))
+GAUSS_SPLITS = FULL.gauss_splits
 
 
-def init_spec(name: str, shape: tuple) -> list[tuple[str, int, float, float]]:
+def init_spec(name: str, shape: tuple, cfg: NetConfig = FULL) -> list[tuple[str, int, float, float]]:
     """List of (stream name, numel, a, c) chunks that fill the tensor in order."""
     n = int(np.prod(shape))
+    if cfg.pts_bias is not None and name.endswith(".dpt.head.4.bias") \
+            and ".gaussian_dpt." not in name:
+        # the same stream and scale as the default; chunk k = one channel
+        # with its constant (pts x, y, z, conf)
+        off = tuple(cfg.pts_bias) + (0.0,) * (n - len(cfg.pts_bias))
+        return [(f"{name}#{k}", 1, 0.02, off[k]) for k in range(n)]
     if name.endswith("gaussian_dpt.dpt.head.4.weight") or name.endswith("gaussian_dpt.dpt.head.4.bias"):
         chunks = []
         per = int(np.prod(shape[1:])) if len(shape) > 1 else 1
-        for k, (nc, gain, bias) in enumerate(GAUSS_SPLITS):
+        for k, (nc, gain, bias) in enumerate(cfg.gauss_splits):
             if name.endswith("weight"):
                 fi, fo = per, nc * int(np.prod(shape[2:]))
                 a = gain * math.sqrt(6.0 / (fi + fo))
@@ -246,9 +275,9 @@ def prng_numpy(seed: int, n: int, a: float, c: float) -> np.ndarray:
     return y + np.float32(c)
 
 
-def prng_tensor_numpy(global_seed: int, name: str, shape: tuple) -> np.ndarray:
+def prng_tensor_numpy(global_seed: int, name: str, shape: tuple, cfg: NetConfig = FULL) -> np.ndarray:
     parts = [prng_numpy(tensor_seed(global_seed, s), n, a, c)
-             for s, n, a, c in init_spec(canonical(name), shape)]
+             for s, n, a, c in init_spec(canonical(name), shape, cfg)]
     return np.concatenate(parts).reshape(shape)
 
 
@@ -263,7 +292,7 @@ def prng_state_dict(cfg: NetConfig, seed: int, device) -> dict[str, torch.Tensor
             continue
         t = torch.empty(int(np.prod(shape)), device=device, dtype=torch.float32)
         off = 0
-        for s, n, a, c in init_spec(cname, shape):
+        for s, n, a, c in init_spec(cname, shape, cfg):
             ops.prng_fill(t[off:off + n], tensor_seed(seed, s), a, c)
             off += n
         sd[name] = t.view(shape)

@@ -87,6 +87,45 @@ def test_hip_map_append_from_world_records_respects_device_count():
     np.testing.assert_array_equal(gm.opacities[:ref.n].cpu().numpy(), ref.opac[:ref.n])
 
 
+@pytest.mark.gpu
+def test_hip_map_empty_batch_on_full_map_is_a_noop():
+    """frame.py:414-416: an append whose batch is empty after the opacity
+    filter returns before the FIFO eviction.  Full map + (a) every record
+    below the threshold, (b) a device count of 0, (c) then a real batch
+    (evicts once, exactly like MapRef)."""
+    from splatt3r_amd.gaussian_map import SharedGaussians
+    rng = np.random.default_rng(17)
+    cap = 600
+    gm = SharedGaussians(max_gaussians=cap, device="cuda")
+    ref = MapRef(cap)
+    b = _batch(rng, cap)
+    ref.append(*b, kf_idx=0, thr=-1.0)
+    gm.append(*(torch.from_numpy(x).cuda() for x in b), kf_idx=0, opacity_threshold=-1.0)
+    assert gm.n_gaussians == ref.n == cap
+
+    def check():
+        k = ref.n
+        assert gm.n_gaussians == k
+        np.testing.assert_array_equal(gm.means[:k].cpu().numpy(), ref.means[:k])
+        np.testing.assert_array_equal(gm.opacities[:k].cpu().numpy(), ref.opac[:k])
+        np.testing.assert_array_equal(gm.kf_id[:k].cpu().numpy(), ref.kf[:k])
+
+    low = _batch(rng, 50)
+    low = low[:3] + (low[3] * 0.2,)                    # all opacities < 0.3
+    ref.append(*low, kf_idx=1, thr=0.3)
+    gm.append(*(torch.from_numpy(x).cuda() for x in low), kf_idx=1, opacity_threshold=0.3)
+    check()
+    rec = torch.from_numpy(rng.uniform(0.5, 1, (40, 13)).astype(np.float32)).cuda()
+    gm.append_records(rec, torch.zeros(1, dtype=torch.int64, device="cuda"), kf_idx=2,
+                      opacity_threshold=0.3)          # device count 0
+    check()
+    c = _batch(rng, 70)
+    ref.append(*c, kf_idx=3, thr=0.3)
+    gm.append(*(torch.from_numpy(x).cuda() for x in c), kf_idx=3, opacity_threshold=0.3)
+    check()
+    assert ref.n < cap
+
+
 def test_viz_camera_matches_reference_capture():
     """Camera math of _render_gs_interactive (CPU): settings vs the capture."""
     from splatt3r_amd.gaussian_map import gl_to_cv_T_WC, viz_camera

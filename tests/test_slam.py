@@ -196,27 +196,63 @@ def test_frontend_with_backend_single_thread():
         assert torch.isfinite(fe.keyframes[k].T_WC.data).all()
 
 
-@pytest.mark.gpu
-def test_frontend_with_backend_worker_thread():
-    """single_thread: False -- keyframe tasks run on the backend worker's
-    own HIP stream while the frontend keeps tracking."""
+def _backend_run(model, frames, dev, mode, n=20):
+    """The frontend + backend over `n` frames.  mode: 'single' (single_thread:
+    the keyframe task runs inside the step), 'lockstep' (worker thread +
+    stream, the frontend waits for each task after its step: the same
+    schedule as 'single', through the stream handoffs), 'async' (worker
+    thread, no waiting: the frontend tracks against whatever keyframe poses
+    the worker has finished, like the reference's backend process)."""
     from splatt3r_amd.backend import Backend
     from splatt3r_amd.frame import Keyframes
     from splatt3r_amd.slam import Frontend
-    dev, model, frames = _model_and_frames(10, step_px=4.0)
     be = Backend(model, Keyframes(), device=dev)
-    be.start_worker()
+    if mode != "single":
+        be.start_worker()
     fe = Frontend(model, device=dev, spatial_stride=4, render=True, backend=be)
     try:
-        for i in range(10):
+        for i in range(n):
             fe.step(i, frames[i])
+            if mode == "lockstep":
+                be.wait()
         be.wait()
     finally:
         be.stop()
-    assert be.stats["optimized"] == len(fe.keyframes) >= 3
-    assert fe.stats["tracked"] == 9
-    for k in range(len(fe.keyframes)):
-        assert torch.isfinite(fe.keyframes[k].T_WC.data).all()
+    torch.cuda.synchronize()
+    fg = be.factor_graph
+    poses = torch.cat([fe.keyframes[k].T_WC.data.reshape(1, 8) for k in range(len(fe.keyframes))])
+    return dict(kf=list(fe.new_kf_frames), ii=fg.ii.tolist(), jj=fg.jj.tolist(),
+                poses=poses.cpu(), stats=dict(fe.stats), optimized=be.stats["optimized"])
+
+
+@pytest.mark.gpu
+def test_frontend_with_backend_worker_thread(parity):
+    """single_thread: False -- keyframe tasks run on the backend worker's own
+    HIP stream while the frontend keeps tracking (stream-safe
+    handoffs through frame.Keyframes).  A fixed 20-frame sequence:
+      * lockstep worker == single_thread: same keyframes, factor-graph edges
+        and keyframe poses within 1e-5 (every handoff goes through the
+        snapshot / deferred-pose path, on another stream);
+      * async worker: same keyframes and edges (tracking decisions and pair
+        matches do not depend on the keyframe poses), poses within 1e-2 of
+        single_thread (the frontend sees backend poses one or more frames
+        late, as the reference's frontend process does)."""
+    dev, model, frames = _model_and_frames(20, step_px=4.0)
+    ref = _backend_run(model, frames, dev, "single")
+    lock = _backend_run(model, frames, dev, "lockstep")
+    asy = _backend_run(model, frames, dev, "async")
+    assert len(ref["kf"]) >= 3 and ref["stats"]["tracked"] == 19
+    for r in (lock, asy):
+        assert r["kf"] == ref["kf"]
+        assert (r["ii"], r["jj"]) == (ref["ii"], ref["jj"])
+        assert r["optimized"] == ref["optimized"] == len(ref["kf"])
+        assert torch.isfinite(r["poses"]).all()
+    d_lock = float((lock["poses"] - ref["poses"]).abs().max())
+    d_async = float((asy["poses"] - ref["poses"]).abs().max())
+    parity("backend_worker_lockstep_vs_single_thread", max_abs=d_lock, tol=1e-5)
+    parity("backend_worker_async_vs_single_thread", max_abs=d_async, tol=1e-2)
+    assert d_lock <= 1e-5
+    assert d_async <= 1e-2
 
 
 @pytest.mark.gpu
