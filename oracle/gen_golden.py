@@ -256,6 +256,12 @@ def gen_net_c4():
     gen_full(320, 512, seed=7)
 
 
+def gen_net_c5():
+    """Full architecture at 304x512 (C5 ETH3D shape by the resize_img rule;
+    N = 608 tokens, a ragged tile tail for the 64-row attention tiles)."""
+    gen_full(304, 512, seed=8)
+
+
 def gen_full(H, Wd, seed, write_manifest=False):
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "splatt3r-slam_amd"))
     from splatt3r_amd import weights as W
@@ -1034,7 +1040,7 @@ def gen_host():
     print("wrote host_glue.npz")
 
 
-SECTIONS = {"host": gen_host, "matching": gen_matching, "render": gen_render, "net": gen_net, "net_c4": gen_net_c4, "n1": gen_n1, "mono": gen_mono, "resize": gen_resize, "viz": gen_viz, "portrait": gen_portrait}
+SECTIONS = {"host": gen_host, "matching": gen_matching, "render": gen_render, "net": gen_net, "net_c4": gen_net_c4, "net_c5": gen_net_c5, "n1": gen_n1, "mono": gen_mono, "resize": gen_resize, "viz": gen_viz, "portrait": gen_portrait}
 
 
 def main(argv):

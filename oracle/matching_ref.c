@@ -105,9 +105,11 @@ static float lerp_ch(const taps_t* t, int c) {
 void oracle_iter_proj(const float* rays_img, const float* pts, const float* p_init,
                       float* p_new, uint8_t* converged_out, int b, int h, int w, int n,
                       int max_iter, float lambda_init, float cost_thresh) {
+  /* pixels are independent: OpenMP over them changes no result */
+#pragma omp parallel for collapse(2) schedule(static)
   for (int bi = 0; bi < b; ++bi) {
-    const float* img = rays_img + (int64_t)bi * h * w * 9;
     for (int i = 0; i < n; ++i) {
+      const float* img = rays_img + (int64_t)bi * h * w * 9;
       int64_t pi = (int64_t)bi * n + i;
       float u = p_init[pi * 2 + 0], v = p_init[pi * 2 + 1];
       u = clampf(u, 1, w - 2);
@@ -168,6 +170,7 @@ void oracle_iter_proj(const float* rays_img, const float* pts, const float* p_in
 void oracle_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
                            int64_t* p1_new, int b, int h, int w, int n, int fdim,
                            int radius, int dilation_max) {
+#pragma omp parallel for collapse(2) schedule(dynamic, 256)
   for (int bi = 0; bi < b; ++bi) {
     for (int i = 0; i < n; ++i) {
       int64_t pi = (int64_t)bi * n + i;

@@ -170,6 +170,56 @@ def test_hip_match_end_to_end_vs_oracle():
         np.testing.assert_array_equal(valid.cpu().numpy(), valid_ref)
 
 
+def _tracker_like_init(h, w, rng, shift=(1, 2), jitter=2):
+    """The tracker's idx_f2k init (the previous frame's match, tracker.py:
+    31-36): a near-identity map, shifted by the inter-frame motion, with a
+    few pixels of disagreement (matching_kernels.cu:24-80 starts each
+    refine window there)."""
+    v, u = np.divmod(np.arange(h * w), w)
+    u2 = np.clip(u + shift[1] + rng.integers(-jitter, jitter + 1, h * w), 0, w - 1)
+    v2 = np.clip(v + shift[0] + rng.integers(-jitter, jitter + 1, h * w), 0, h - 1)
+    return (v2 * w + u2).astype(np.int64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h,w", [(384, 512), (320, 512)])
+def test_hip_refine_full_size_tracker_init_vs_oracle(h, w):
+    """refine_matches at the C2 / C4 frame sizes the tracker runs every
+    frame, from tracker-like starting pixels (f = 24, radius 3, dilation 5)."""
+    import mast3r_slam_backends as be
+    rng = np.random.default_rng(h + w)
+    D11 = unit_desc(1, h, w, 24, rng)
+    D21 = np.roll(D11, (1, 2), axis=(1, 2)) + rng.normal(size=D11.shape).astype(np.float32) * 0.3
+    D21 /= np.linalg.norm(D21, axis=-1, keepdims=True)
+    D11h, D21h = D11.astype(np.float16), D21.astype(np.float16).reshape(1, h * w, 24)
+    idx0 = _tracker_like_init(h, w, rng)
+    p1 = np.stack([idx0 % w, idx0 // w], -1)[None].astype(np.int64)
+    ref = oracle.refine_matches(D11h, D21h, p1, 3, 5)
+    (out,) = be.refine_matches(_to(D11h), _to(D21h), _to(p1), 3, 5)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h,w", [(384, 512), (320, 512)])
+def test_hip_match_full_size_tracker_init_vs_oracle(h, w):
+    """The end-to-end match (prep, iter_proj, occlusion, refine, pixel_to_lin)
+    at C2 / C4 size, with and without the tracker-like idx init."""
+    from splatt3r_amd.matching import match
+    rng = np.random.default_rng(3 * h + w)
+    X11 = smooth_pointmap(1, h, w, rng)
+    X21 = np.roll(X11, (1, 2), axis=(1, 2)) + rng.normal(size=X11.shape).astype(np.float32) * 1e-3
+    D11 = unit_desc(1, h, w, 24, rng)
+    D21 = np.roll(D11, (1, 2), axis=(1, 2)) + rng.normal(size=D11.shape).astype(np.float32) * 0.3
+    D21 /= np.linalg.norm(D21, axis=-1, keepdims=True)
+    for idx_init in (None, _tracker_like_init(h, w, rng)[None]):
+        idx_ref, valid_ref = oracle.match(X11, X21, D11, D21, idx_init)
+        idx, valid = match(_to(X11), _to(X21), _to(D11), _to(D21),
+                           None if idx_init is None else _to(idx_init))
+        np.testing.assert_array_equal(idx.cpu().numpy(), idx_ref)
+        np.testing.assert_array_equal(valid.cpu().numpy(), valid_ref)
+        assert valid_ref.mean() > 0.5
+
+
 @pytest.mark.gpu
 def test_backends_reject_non_contiguous():
     import mast3r_slam_backends as be

@@ -183,6 +183,14 @@ def test_full_model_320x512_vs_reference_golden(parity):
 
 
 @pytest.mark.gpu
+def test_full_model_304x512_vs_reference_golden(parity):
+    """C5 ETH3D shape: 512x304 by the resize_img rule, 19 x 32 = 608 tokens
+    -- not a multiple of the 64-row Q/K tiles or of the GEMM row tiles, so
+    the attention and GEMM M-tails run at full size."""
+    _full_size(parity, 304, 512, "net_full_304x512.npz")
+
+
+@pytest.mark.gpu
 def test_pair_batch_bp2_matches_bp1_and_golden(parity):
     """The DP shard unit: one Bp = 2 grouped pair plan over (1,2) and (2,1)
     equals two Bp = 1 runs (splatt3r_utils.py:466-499 loops pairs one at a
