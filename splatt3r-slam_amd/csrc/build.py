@@ -39,6 +39,11 @@ SOURCES = {
     "splat_pack.hip": STRICT,
     "gaussians.hip": STRICT,
     "net_gemm.hip": FAST,
+    "net_gemm_t1.hip": FAST,
+    "net_gemm_t2.hip": FAST,
+    "net_gemm_t3.hip": FAST,
+    "net_gemm_t4.hip": FAST,
+    "net_gemm_t5.hip": FAST,
     "net_attn.hip": FAST,
     "net_ops.hip": STRICT,
     "gn_backend.hip": STRICT,

@@ -186,7 +186,11 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
                 12: (128, 128), 14: (256, 256),
                 # in-workgroup K-groups (net_gemm.hip KG > 1)
                 15: (64, 64), 16: (64, 64), 17: (64, 128), 18: (128, 128), 19: (64, 64),
-                20: (64, 128)}
+                20: (64, 128),
+                # v_mfma_f32_16x16x32 tiles, 4 waves (net_gemm_t4/t5.hip)
+                21: (64, 160), 22: (96, 64), 23: (128, 96), 24: (160, 128), 25: (256, 128),
+                26: (64, 64), 27: (128, 128), 28: (64, 128), 29: (96, 128), 30: (64, 192),
+                31: (64, 64)}
 _TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14}   # the fused tail runs with one K-group
 
 

@@ -50,7 +50,15 @@ def test_gemm_dense_bias_residual(M, N, K, groups):
     (768, 1024, 1024, 1, 1, 15), (768, 1024, 4096, 1, 1, 16), (300, 200, 1000, 2, 1, 16),
     (768, 768, 768, 2, 1, 17), (700, 256, 2304, 1, 1, 18), (130, 300, 968, 1, 1, 19),
     (768, 1024, 1088, 1, 1, 20), (64, 64, 64, 1, 1, 16), (520, 384, 640, 2, 2, 16),
-    (300, 256, 200, 1, 1, 20)])
+    (300, 256, 200, 1, 1, 20),
+    # v_mfma_f32_16x16x32 tiles (21-31): ragged M / N / K tails, global split-K
+    (768, 3072, 1024, 1, 1, 21), (130, 300, 968, 2, 1, 21), (768, 768, 768, 2, 1, 22),
+    (300, 200, 1000, 1, 3, 22), (768, 4096, 1024, 1, 1, 23), (520, 300, 640, 2, 2, 23),
+    (768, 3072, 768, 2, 1, 24), (700, 256, 2304, 1, 1, 24), (768, 1600, 1792, 2, 1, 25),
+    (300, 136, 520, 1, 1, 25), (768, 1024, 1024, 1, 1, 26), (64, 64, 136, 1, 2, 26),
+    (768, 2304, 768, 2, 1, 27), (130, 96, 2000, 2, 1, 27), (600, 256, 200, 1, 1, 28),
+    (768, 768, 3072, 2, 3, 29), (300, 500, 1000, 1, 1, 29), (768, 3072, 1024, 1, 1, 30),
+    (200, 96, 200, 2, 5, 30), (768, 1024, 4096, 1, 2, 31), (130, 300, 968, 1, 1, 31)])
 def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
     """Split-K partials + ordered reduce + the full epilogue (bias, GELU,
     fp32 residual, fp16 out + fp16 copy) for every tile shape."""
@@ -73,7 +81,9 @@ def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
                                             (1, 5, 768), (1, 9, 768), (2, 10, 768), (1, 11, 96),
                                             (1, 12, 768), (1, 9, 96), (2, 9, 136), (1, 15, 768),
                                             (1, 16, 96), (1, 17, 768), (2, 18, 256), (1, 19, 136),
-                                            (1, 20, 768)])
+                                            (1, 20, 768), (1, 21, 768), (2, 23, 256),
+                                            (1, 24, 96), (1, 25, 136), (1, 27, 768),
+                                            (1, 29, 256), (1, 31, 768)])
 def test_gemm_implicit_conv_split_k(split, tile, Cin):
     from splatt3r_amd import ops, _lib
     B, H, W, Cout, k, stride, pad = 1, 12, 16, 256, 3, 1, 1
@@ -189,9 +199,11 @@ def rope_ref(t, pos, cos, sin):
     return torch.cat((r1d(y, pos[:, :, 0]), r1d(xx, pos[:, :, 1])), -1)
 
 
-@pytest.mark.parametrize("B,ht,wt,heads,ncol_heads,groups", [(1, 24, 32, 16, 32, 1), (2, 6, 8, 12, 12, 2),
-                                                            (1, 5, 7, 2, 4, 2)])
-def test_gemm_rope_epilogue_vs_torch(B, ht, wt, heads, ncol_heads, groups):
+@pytest.mark.parametrize("B,ht,wt,heads,ncol_heads,groups,tile", [
+    (1, 24, 32, 16, 32, 1, 0), (2, 6, 8, 12, 12, 2, 0), (1, 5, 7, 2, 4, 2, 0),
+    (1, 24, 32, 16, 32, 1, 21), (1, 24, 32, 12, 12, 2, 24), (2, 6, 8, 12, 12, 2, 30),
+    (1, 24, 32, 16, 32, 1, 23)])
+def test_gemm_rope_epilogue_vs_torch(B, ht, wt, heads, ncol_heads, groups, tile):
     """QKV projection with RoPE2D fused into the epilogue == linear then
     pos_embed.py's rope on each head of the first rope_ncols columns."""
     from splatt3r_amd import ops, _lib
@@ -210,7 +222,7 @@ def test_gemm_rope_epilogue_vs_torch(B, ht, wt, heads, ncol_heads, groups):
     b = [_rand(Nout, dtype=torch.float32, seed=60 + g) for g in range(groups)]
     C = [torch.empty(M, Nout, device="cuda") for _ in range(groups)]
     ops.gemm(A, W, C, M, Nout, K, lda=K, bias=b, rope=(cos, sin), rope_pos=pos,
-             rope_ncols=ncols)(_lib.stream())
+             rope_ncols=ncols, tile=tile)(_lib.stream())
     for g in range(groups):
         lin = A[g].float() @ W[g].float().T + b[g]
         ref = lin.clone()

@@ -54,7 +54,7 @@ def main():
                       oW=conv[1])
         fl = 2 * M * N * K * g
         res = []
-        for tile in (1, 2, 3, 5, 6, 7, 8):
+        for tile in (1, 2, 3, 5, 6, 7, 8, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31):
             for sk in (1, 2, 3, 4):
                 if conv is not None and sk > 1:
                     continue
