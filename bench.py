@@ -69,6 +69,8 @@ def _args():
                     help="skip the frontend + concurrent backend leg")
     ap.add_argument("--backend-steps", type=int, default=60)
     ap.add_argument("--no-map", action="store_true", help="skip the C5 full-map render leg")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end leg (dataset PNG read + resize + H2D + PNG write)")
     ap.add_argument("--pairs-per-rank", type=int, default=4)
     ap.add_argument("--no-kprof", action="store_true",
                     help="skip the per-launch network profile (roofline object)")
@@ -289,6 +291,57 @@ def bench_backend(model, dev, steps, rank):
             "mode": "single_thread: False (worker thread + HIP stream, same GPU)"}
 
 
+def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, writers=3):
+    """The reference's FPS definition (main.py:363-535): frames / wall time of
+    the whole loop, with the host work inside it -- the dataset read (PNG
+    decode of 640x480 TUM-layout frames), create_frame's resize_img (PIL
+    LANCZOS -> 512x384) + ImgNorm + H2D (dataio.FrameLoader, worker
+    threads), the tracking step, and the per-frame gs_init_* / gs_track_*
+    PNG write (dataio.RenderWriter, writer threads).  The frames are written
+    to a scratch TUM layout before the timed region; the timed region ends
+    when every PNG is on disk."""
+    import shutil
+    import tempfile
+    from splatt3r_amd.dataio import FrameLoader, RenderWriter, TUMDataset, write_synthetic_tum
+    from splatt3r_amd.slam import Frontend
+    root = tempfile.mkdtemp(prefix="s3_tum_")
+    try:
+        n = warmup + steps + 2
+        write_synthetic_tum(os.path.join(root, "seq"), n, seed=7)
+        ds = TUMDataset(os.path.join(root, "seq"))
+        writer = RenderWriter(os.path.join(root, "renders"), workers=writers)
+        fe = Frontend(model, device=dev, spatial_stride=4, render=True, render_writer=writer,
+                      main_priority=main_priority)
+        loader = FrameLoader(ds, dev, workers=workers, depth=2 * workers)
+        cur = next(loader)
+        t0 = None
+        for i in range(n - 1):
+            if i == warmup + 1:                  # frame 0 = INIT, W warm-up frames
+                writer.flush()
+                torch.cuda.synchronize()
+                s0 = dict(fe.stats)
+                t0 = time.perf_counter()
+            nxt = next(loader)
+            fe.step(i, cur.consume(), next_img=[nxt.consume()])
+            cur = nxt
+        torch.cuda.synchronize()
+        writer.flush()
+        t = time.perf_counter() - t0
+        st = {k: fe.stats[k] - s0[k] for k in fe.stats}
+        loader.close()
+        writer.close()
+        written = len(os.listdir(os.path.join(root, "renders")))
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return {"frames_per_s": steps / t, "steps": steps, "tracked": st["tracked"],
+            "reloc": st["reloc"], "keyframes": st["keyframes"],
+            "keyframe_rate": st["keyframes"] / steps, "pngs_written": written,
+            "loader_threads": workers, "png_writer_threads": writers,
+            "input": "640x480 PNG frames, TUM layout (rgb.txt), synthetic panning texture",
+            "includes": "PNG decode + resize_img (PIL LANCZOS) + ImgNorm + H2D, tracking step, "
+                        "render D2H + uint8 + PNG encode/write (compress_level 1)"}
+
+
 def bench_map(dev, n=8_388_608, iters=5, warmup=2, seed=0):
     """C5 full-map render: an n-Gaussian world map (SharedGaussians, filled
     through s3w_map_append in 1M-record batches) rasterized with
@@ -383,8 +436,14 @@ def main():
                             "keyframes": st["keyframes"],
                             "keyframe_rate": st["keyframes"] / max(1, a.steps),
                             "reloc": st["reloc"],
-                            "rendered": st["rendered"], "tracked": st["tracked"]},
+                            "rendered": st["rendered"], "tracked": st["tracked"],
+                            # a lost frame (RELOC) in this frontend-only loop would
+                            # turn later frames into untracked mono inferences
+                            "tracking_complete": st["tracked"] == a.steps and st["reloc"] == 0},
     }
+    if not result["frame_breakdown"]["tracking_complete"]:
+        print(f"[bench] WARNING: tracked {st['tracked']} of {a.steps} frames, reloc {st['reloc']}: "
+              "the frame rate is not a tracking frame rate", file=sys.stderr, flush=True)
     if rank == 0 and not a.no_kprof:
         # after the timed region: kernel durations of the plans' graph
         # replays (roctracer trace) and a per-launch eager profile
@@ -423,6 +482,11 @@ def main():
                              "mfma_util_in_kernels": net_tflops / PEAK_F16_TFLOPS,
                              "gflop_per_frame": flops_frame / 1e9,
                              "tflops_wall": flops_frame / (net_ms * 1e-3) / 1e12}
+    result["device_path_fps"] = value
+    if rank == 0 and not a.no_e2e:
+        e2e = bench_end_to_end(model, dev, a.steps, a.warmup, a.main_priority)
+        result["end_to_end_fps"] = e2e["frames_per_s"]
+        result["end_to_end"] = e2e
     if not a.no_pairs:
         from splatt3r_amd.pairs import bench_pairs
         result["pairs"] = bench_pairs(model, frames, ws, rank, dev, a.pairs_per_rank)

@@ -108,6 +108,41 @@ class Backend:
             self._solve()
         return success
 
+    # ------------------------------------------------------------ map -----
+    def refresh_map(self, gmap, spatial_stride: int = 4, depth_max_percentile: float = 0.98,
+                    max_scale: float = 1.0, min_confidence: float = 1.5,
+                    opacity_threshold: float = 0.3):
+        """The global-map refresh after optimisation (north star C5: batched
+        re-inference + full-map render): every keyframe of the factor graph
+        is re-inferred against its first edge partner -- sharded over the
+        ranks (pair p on rank p mod W) -- and its self-prediction becomes
+        world Gaussians at its optimised pose with gaussians_to_world's
+        filters (splatt3r_utils.py:180-328; the defaults are main.py's map
+        arguments); one all-gather rebuilds `gmap` (and every worker's map)
+        in keyframe order, the SharedGaussians.append semantics
+        (frame.py:388-443, opacity > 0.3).  Call from the frontend thread
+        after wait().  Returns the per-keyframe record tensors."""
+        from splatt3r_amd.pairs import PairShard
+        ii, jj = self.factor_graph.ii.tolist(), self.factor_graph.jj.tolist()
+        partner: dict = {}
+        for i, j in zip(ii, jj):
+            partner.setdefault(i, j)
+            partner.setdefault(j, i)
+        ks = sorted(partner)
+        if not ks:
+            gmap.clear()
+            return []
+        poses = self.keyframes.get_poses().data.reshape(-1, 8)
+        if self.shard is not None and self.shard.ws > 1:
+            sh = self.shard
+        else:
+            sh = PairShard(self.model, self.device)
+            for k in ks:
+                sh.register_local(k, self.keyframes[k])
+        sh.gmap = gmap
+        return sh.refresh_map(ks, [partner[k] for k in ks], poses, spatial_stride,
+                              depth_max_percentile, max_scale, min_confidence, opacity_threshold)
+
     # --------------------------------------------------------- worker ----
     def start_worker(self):
         """single_thread: False -- keyframe tasks run on a worker thread and

@@ -14,8 +14,15 @@ keyframe pair in both orders and matches both directions
     reference's Q-weighting into its results (Qj, Qi), and rank 0 gathers
     idx / valid / Q (26 B per pixel per pair) with three all-gathers and
     restores the pair order; the GN solve stays on rank 0 (global_opt.py);
-  * the world Gaussians of a rank's pairs reach every rank's map buffer with
-    one all-gather (`gather_map`, 52 B per Gaussian).
+  * the global-map refresh after an optimisation (`PairShard.refresh_map`,
+    the C5 path "batched ViT re-inference + full-map render"): every rank
+    re-infers its share of the factor-graph edges, turns keyframe i's
+    prediction of edge (i, j) into world Gaussians with gaussians_to_world's
+    filters at the optimised pose (splatt3r_utils.py:180-328, one HIP pass),
+    and one all-gather (`gather_map`, 52 B per Gaussian) gives every rank
+    the whole map in edge order; each rank rebuilds its SharedGaussians
+    (frame.py:388-443) from it, so any rank can render the full map
+    (gaussian_map.render_map, visualization.py:467-600).
 
 Ranks other than 0 sit in `PairShard.serve()` and execute the tasks rank 0
 broadcasts (keyframe, pair batch, stop).  With gloo (CPU tests) the
@@ -33,7 +40,7 @@ from splatt3r_amd.splatt3r_utils import splatt3r_match_symmetric, world_records
 
 GAUSS_FLOATS = 13   # means 3 + cov_triu 6 + colour 3 + opacity 1 (52 B)
 
-OP_STOP, OP_KEYFRAME, OP_PAIRS = 0, 1, 2
+OP_STOP, OP_KEYFRAME, OP_PAIRS, OP_MAP = 0, 1, 2, 3
 
 
 def shard(pairs, ws: int, rank: int):
@@ -104,9 +111,17 @@ class PairShard:
     of splatt3r_match_symmetric; injectable so the collective protocol is
     testable without the network (tests/test_pairs.py)."""
 
-    def __init__(self, model, device, match_fn: Optional[Callable] = None, Q_conf=None):
+    def __init__(self, model, device, match_fn: Optional[Callable] = None, Q_conf=None,
+                 map_fn: Optional[Callable] = None, gmap=None):
         from splatt3r_amd.config import config
         self.model = model
+        # map_fn(pairs, poses [n_kf, 8], params [4]) -> list of [n_p, 13] world
+        # records per pair (default: re-inference + gaussians_to_world on the
+        # device); injectable like match_fn.  gmap: this rank's map buffer,
+        # rebuilt on every refresh_map (workers too).
+        self.map_fn = map_fn or self._map_records
+        self.gmap = gmap
+        self.last_map = None
         self.device = torch.device(device)
         self.ws = dist.get_world_size() if _backend() else 1
         self.rank = dist.get_rank() if _backend() else 0
@@ -139,9 +154,13 @@ class PairShard:
             feat = frame.feat.reshape(1, N, C).float().contiguous()
             self._bcast(feat)
             pos = frame.pos.reshape(1, N, 2).contiguous()
+            # the image too: the map's colours are RGB2SH(image) + the
+            # predicted residual (splatt3r_utils.py:250-257)
+            img = frame.img.reshape(1, 3, H, W).float().contiguous()
+            self._bcast(img)
         else:
             raise RuntimeError("broadcast_keyframe is called on rank 0; workers use serve()")
-        self.kf[idx] = (feat, pos, torch.tensor([[H, W]], dtype=torch.int32))
+        self.kf[idx] = (feat, pos, torch.tensor([[H, W]], dtype=torch.int32), img)
         self.stats["keyframes"] += 1
 
     def _recv_keyframe(self, idx, nc):
@@ -153,12 +172,13 @@ class PairShard:
         # croco/models/blocks.py:193-205): rebuilt, not sent
         from splatt3r_amd.net import positions
         pos = positions(1, H // 16, W // 16, self.device)
-        self.kf[idx] = (feat, pos, torch.tensor([[H, W]], dtype=torch.int32))
+        img = self._bcast(torch.empty(1, 3, H, W, device=self.device))
+        self.kf[idx] = (feat, pos, torch.tensor([[H, W]], dtype=torch.int32), img)
         self.stats["keyframes"] += 1
 
     def register_local(self, idx: int, frame):
         """Single-rank use: cache a keyframe without a broadcast."""
-        self.kf[idx] = (frame.feat, frame.pos, frame.img_true_shape)
+        self.kf[idx] = (frame.feat, frame.pos, frame.img_true_shape, frame.img)
 
     # ----------------------------------------------------------- pairs ----
     def _run_local(self, pairs):
@@ -191,7 +211,7 @@ class PairShard:
         mine = shard(pairs, ws, rank)
         res = self._run_local(mine)
         per = -(-n // ws)
-        (feat, _, shp) = self.kf[pairs[0][0]]
+        feat, _, shp = self.kf[pairs[0][0]][:3]
         hw = int(shp.reshape(-1)[0]) * int(shp.reshape(-1)[1])
         dev = self.device
         idx = torch.zeros(per, 2, hw, dtype=torch.int64, device=dev)
@@ -215,6 +235,79 @@ class PairShard:
         return I[:, 0], I[:, 1], V[:, 0, :, None], V[:, 1, :, None], Qt[:, 0, :, None], \
             Qt[:, 1, :, None]
 
+    # ------------------------------------------------------------- map ----
+    def refresh_map(self, ii, jj, poses: torch.Tensor, spatial_stride: int = 1,
+                    depth_max_percentile: float = 0.98, max_scale: float = 1.0,
+                    min_confidence: float = 1.5, opacity_threshold: float = 0.3):
+        """Rank 0: re-infer the edges (ii[p], jj[p]) across the ranks and
+        rebuild every rank's map from keyframe ii[p]'s world Gaussians at
+        poses[ii[p]] (lietorch layout [n_kf, 8]), in edge order.  Returns
+        the per-edge [n_p, 13] records (on every rank)."""
+        pairs = list(zip((int(i) for i in ii), (int(j) for j in jj)))
+        poses = poses.reshape(-1, 8).float().contiguous()
+        params = torch.tensor([spatial_stride, depth_max_percentile, max_scale, min_confidence,
+                               opacity_threshold], dtype=torch.float64, device=self.device)
+        if self.ws > 1:
+            self._header(OP_MAP, len(pairs), poses.shape[0])
+            self._bcast(torch.tensor(pairs, dtype=torch.int64, device=self.device).reshape(-1, 2))
+            self._bcast(poses)
+            self._bcast(params)
+        return self._map_collective(pairs, poses, params)
+
+    def _map_collective(self, pairs, poses, params):
+        ws, rank, n = self.ws, self.rank, len(pairs)
+        mine = shard(pairs, ws, rank)
+        local = self.map_fn(mine, poses, params) if mine else []
+        if ws == 1:
+            recs = local
+        else:
+            # per-pair counts (padded to the largest shard), then one all-gather
+            # of the records; both in rank order, re-cut into edge order
+            per = -(-n // ws)
+            cnt = torch.zeros(per, dtype=torch.int64, device=self.device)
+            for s_, r in enumerate(local):
+                cnt[s_] = r.shape[0]
+            cnts = [c.tolist() for c in _all_gather_equal(cnt, ws)]
+            flat = (torch.cat(local) if local else
+                    torch.zeros(0, GAUSS_FLOATS, device=self.device))
+            gathered = gather_map(flat, ws)
+            recs, off = [None] * n, 0
+            for r in range(ws):
+                for s_, p in enumerate(range(r, n, ws)):
+                    recs[p] = gathered[off:off + cnts[r][s_]]
+                    off += cnts[r][s_]
+        self.last_map = recs
+        if self.gmap is not None:
+            thr = float(params[4])
+            self.gmap.clear()
+            for (i, _), r in zip(pairs, recs):
+                if r.shape[0]:
+                    self.gmap.append_records(r, torch.tensor([r.shape[0]], device=r.device), i, thr)
+        return recs
+
+    def _map_records(self, pairs, poses, params):
+        """This rank's edges: one batched pair decode (the backend's pair
+        plans), keyframe i's self-prediction -> gaussians_to_world filters +
+        world transform at poses[i] (one HIP pass per edge)."""
+        from lietorch import Sim3
+        stride, q, max_scale, min_conf = (float(v) for v in params[:4].tolist())
+        fi = torch.cat([self.kf[i][0] for i, _ in pairs])
+        pi = torch.cat([self.kf[i][1] for i, _ in pairs])
+        fj = torch.cat([self.kf[j][0] for _, j in pairs])
+        pj = torch.cat([self.kf[j][1] for _, j in pairs])
+        H, W = (int(v) for v in self.kf[pairs[0][0]][2].reshape(-1)[:2].tolist())
+        r11, _, _ = self.model.encoder.infer_pair(fi, pi, fj, pj, (H, W), tag="backend")
+        out = []
+        for b, (i, _) in enumerate(pairs):
+            view = {k: v[b] for k, v in r11.items()
+                    if k in ("means", "scales", "rotations", "sh", "opacities", "conf")}
+            M = Sim3(poses[i].reshape(1, 8).to(self.device)).matrix()[0]
+            rec, cnt = world_records(view, self.kf[i][3][0], M, max(1, int(stride)), 0.05, q,
+                                     max_scale, min_conf)
+            out.append(rec[:int(cnt.item())])
+        self.stats["map_pairs"] = self.stats.get("map_pairs", 0) + len(pairs)
+        return out
+
     # ---------------------------------------------------------- workers ---
     def serve(self):
         """Ranks > 0: execute rank 0's tasks until OP_STOP."""
@@ -228,23 +321,16 @@ class PairShard:
             elif op == OP_PAIRS:
                 pl = self._bcast(torch.empty(a, 2, dtype=torch.int64, device=self.device))
                 self._pairs_collective([tuple(int(v) for v in p) for p in pl.tolist()])
+            elif op == OP_MAP:
+                pl = self._bcast(torch.empty(a, 2, dtype=torch.int64, device=self.device))
+                poses = self._bcast(torch.empty(b, 8, device=self.device))
+                params = self._bcast(torch.empty(5, dtype=torch.float64, device=self.device))
+                self._map_collective([tuple(int(v) for v in p) for p in pl.tolist()], poses,
+                                     params)
 
     def stop(self):
         if self.rank == 0 and self.ws > 1:
             self._header(OP_STOP)
-
-
-def world_gaussians(res, T_WC: torch.Tensor, img: torch.Tensor) -> torch.Tensor:
-    """Per-pixel Gaussians of one predicted view ([H,W,...] dict) -> [h*w, 13]
-    world records (means, cov triu, RGB colour, opacity): the transform of
-    gaussians_to_world (splatt3r_utils.py:290-318) at stride 1 with its
-    filters off, as one HIP pass (include/s3w.h).  Labelled unfiltered in
-    the bench: the map records of the pair shard, not the reference's
-    per-frame gaussians_to_world output."""
-    from lietorch import Sim3
-    M = Sim3(T_WC.reshape(1, 8)).matrix()[0]
-    out, _ = world_records(res, img[0] if img.dim() == 4 else img, M)
-    return out
 
 
 @torch.inference_mode()
@@ -253,16 +339,17 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
     creates n_kf keyframes (encoder + broadcast to every rank), then issues
     add_factors over consecutive keyframes plus 3 retrieval-like earlier
     partners per keyframe (main.py:153-173, k = 3), ws * pairs_per_rank pairs
-    per batch; ranks > 0 serve.  After each batch the jj self-predictions
-    of every rank's pairs become world records and are all-gathered into
-    every rank's map buffer (unfiltered, stride 1)."""
+    per batch; ranks > 0 serve.  Then the global-map refresh on the same
+    keyframes (refresh_map: each keyframe re-inferred against a partner on
+    rank k mod W, gaussians_to_world filters at stride 4, all-gather into
+    every rank's SharedGaussians), timed on its own."""
     from splatt3r_amd.frame import Keyframes, create_frame
     from splatt3r_amd.gaussian_map import SharedGaussians
     from splatt3r_amd.global_opt import FactorGraph
     H, W = frames.shape[-2:]
     torch.cuda.synchronize()
     n_kf = max(2, min(n_kf, frames.shape[0]))
-    sh = PairShard(model, dev)
+    sh = PairShard(model, dev, gmap=SharedGaussians(max_gaussians=n_kf * H * W, device=dev))
     kfs = Keyframes()
     allp = []
     for k in range(1, n_kf):
@@ -272,6 +359,11 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
                 allp.append((k - d, k))
     total = ws * pairs_per_rank
     allp = (allp * (total // len(allp) + 1))[:total]
+    map_i = list(range(n_kf))
+    map_j = [k + 1 if k + 1 < n_kf else k - 1 for k in map_i]
+    poses = torch.zeros(n_kf, 8, device=dev)
+    poses[:, 6] = poses[:, 7] = 1.0
+    poses[:, 0] = torch.arange(n_kf, device=dev) * 0.02
     t_bc = 0.0
     if rank == 0:
         for k in range(n_kf):
@@ -293,51 +385,57 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
         jj = [p[1] for p in allp]
     else:
         sh.serve()              # receive the keyframes
-    gmap = SharedGaussians(max_gaussians=max(1, 2 * total * H * W), device=dev)
-    pp = model.encoder.pair_plan(len(shard(allp, ws, rank)), H, W, tag="backend")
+    model.encoder.pair_plan(len(shard(allp, ws, rank)), H, W, tag="backend")
 
-    def one_batch():
+    def pair_batch():
         if rank == 0:
             fg.add_factors(ii, jj, 0.0)
             if ws > 1:
                 sh.stop()
         else:
             sh.serve()
-        # the jj self-predictions of this rank's pairs -> world records ->
-        # every rank's map (the last decoded order is (jj, ii): res[0] = jj)
-        mine = shard(allp, ws, rank)
-        recs = [world_gaussians({k: v[b] for k, v in pp.res[0].items()},
-                                torch.tensor([0, 0, 0, 0, 0, 0, 1, 1.0], device=dev),
-                                frames[j]) for b, (_, j) in enumerate(mine)]
-        gathered = gather_map(torch.cat(recs, 0), ws)
-        gmap.clear()
-        gmap.append_records(gathered, torch.tensor([gathered.shape[0]], device=dev), 0, -1.0)
-        return gathered
 
-    one_batch()                 # build + capture plans
-    torch.cuda.synchronize()
-    times = []
-    for _ in range(reps):
-        if ws > 1:
-            dist.barrier()
+    def map_refresh():
+        if rank == 0:
+            sh.refresh_map(map_i, map_j, poses, spatial_stride=4)
+            if ws > 1:
+                sh.stop()
+        else:
+            sh.serve()
+
+    def timed(fn):
+        fn()                    # build + capture plans
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        gathered = one_batch()
-        torch.cuda.synchronize()
+        times = []
+        for _ in range(reps):
+            if ws > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            if ws > 1:
+                dist.barrier()
+            times.append(time.perf_counter() - t0)
+        t = sorted(times)[len(times) // 2]
         if ws > 1:
-            dist.barrier()
-        times.append(time.perf_counter() - t0)
-    t = sorted(times)[len(times) // 2]
-    if ws > 1:
-        tt = torch.tensor([t], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt)
+            tt = torch.tensor([t], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = float(tt)
+        return t
+
+    t = timed(pair_batch)
+    t_map = timed(map_refresh)
     out = dict(kf_pairs_per_s=total / t, pairs=total, pairs_per_rank=len(shard(allp, ws, rank)),
-               ms_per_batch=t * 1e3, map_gaussians=int(gathered.shape[0]),
-               map_records="unfiltered stride-1 jj self-predictions (52 B each)",
+               ms_per_batch=t * 1e3,
                path="FactorGraph.add_factors -> PairShard (pair p on rank p mod W) -> "
-                    "gather to rank 0; map all-gather")
+                    "gather to rank 0",
+               map_refresh={"ms": t_map * 1e3, "keyframes": n_kf,
+                            "map_gaussians": sh.gmap.n_gaussians,
+                            "path": "PairShard.refresh_map: keyframe k re-inferred on rank k mod "
+                                    "W, gaussians_to_world filters (stride 4, q 0.98, max scale "
+                                    "1, conf 1.5) -> all-gather -> SharedGaussians (opacity > "
+                                    "0.3)"})
     if ws > 1:
         out["keyframe_broadcast_ms"] = t_bc / n_kf * 1e3
-        out["allgather_MB_per_rank"] = len(shard(allp, ws, rank)) * H * W * GAUSS_FLOATS * 4 / 1e6
     return out

@@ -47,8 +47,11 @@ class Frontend:
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
                  readback=True, enc_batch=1, main_priority=None, late_prefetch=False,
-                 viz=False, max_gaussians=4 * 1024 * 1024, backend=None):
+                 viz=False, max_gaussians=4 * 1024 * 1024, backend=None, render_writer=None):
         self.model = model
+        # dataio.RenderWriter: the per-frame gs_init_* / gs_track_* PNG export
+        # (main.py:436-446, 490-506), written off the tracking thread
+        self.render_writer = render_writer
         # viz: the reference's enable_gs_viz (main.py:357, `not --no-viz`).
         # Only then does it record the last append (main.py:434-435,488-489);
         # under --no-viz last_gs_append_T_WC stays None, so should_append is
@@ -147,10 +150,11 @@ class Frontend:
             self._rb_event.synchronize()
         return self._last_render
 
-    def _render(self, frame, ref, target):
+    def _render(self, frame, ref, target, prefix="gs_track"):
         if not self.render:
             return
-        self._finish_render(splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=target))
+        self._finish_render(splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=target),
+                            frame.frame_id, prefix)
 
     def _speculate(self, frame, ref):
         """Hook for FrameTracker.track: with the map off, the tracked frame's
@@ -170,9 +174,13 @@ class Frontend:
             return recs, img
         return hook
 
-    def _finish_render(self, img):
+    def _finish_render(self, img, index=0, prefix="gs_track"):
         if img is not None:
             self._stats["rendered"] += 1
+            if self.render_writer is not None:
+                self.render_writer.submit(index, img, prefix)
+                self._last_render, self._rb_event = None, None
+                return
             out = img[0, 0].clamp(0, 1).permute(1, 2, 0)
             if not self.readback:
                 self._last_render, self._rb_event = out, None
@@ -326,7 +334,7 @@ class Frontend:
             self.mode = Mode.TRACKING
             if self._to_world(frame, len(self.keyframes) - 1) is not None and self.viz:
                 self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
-            self._render(frame, frame, None)
+            self._render(frame, frame, None, prefix="gs_init")
             self.last_T_WC = frame.T_WC
             return frame
         if self.mode == Mode.TRACKING:
@@ -353,7 +361,7 @@ class Frontend:
                     self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
             if not try_reloc:
                 if spec is not None:
-                    self._finish_render(spec[1])
+                    self._finish_render(spec[1], i, "gs_track")
                 else:
                     self._render(frame, self.keyframes.last_keyframe(), frame.T_WC)
         elif self.mode == Mode.RELOC:

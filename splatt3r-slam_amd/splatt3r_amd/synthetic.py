@@ -84,16 +84,10 @@ def settings_to_dict(rs) -> dict:
                 sh_degree=rs.sh_degree, campos=t(rs.campos))
 
 
-def tum_like_sequence(n: int, H: int = 384, W: int = 512, seed: int = 0, step_px: float = 3.0,
-                      device="cuda") -> torch.Tensor:
-    """C2 stand-in when the TUM fr1_desk frames are absent: n frames of a
-    slowly panning camera over a smooth multi-scale noise texture (numpy
-    PCG64 `seed`), already resized/cropped to the 512x384 the reference's
-    resize_img produces from 640x480, normalised like ImgNorm.
-    Returns [n, 1, 3, H, W] float32 on `device`."""
+def smooth_texture(TH: int, TW: int, seed: int) -> np.ndarray:
+    """[3, TH, TW] float32 in [0, 1]: three octaves of bicubically upsampled
+    uniform noise (cells 64 / 16 / 4 px), numpy PCG64 `seed`."""
     rng = np.random.default_rng(seed)
-    pad = int(np.ceil(step_px * n)) + 8
-    TH, TW = H + pad, W + pad
     tex = np.zeros((3, TH, TW), np.float32)
     for cell, amp in ((64, 0.5), (16, 0.3), (4, 0.2)):
         g = rng.random((3, TH // cell + 2, TW // cell + 2)).astype(np.float32)
@@ -101,7 +95,18 @@ def tum_like_sequence(n: int, H: int = 384, W: int = 512, seed: int = 0, step_px
         up = torch.nn.functional.interpolate(t, scale_factor=cell, mode="bicubic",
                                              align_corners=False)[0, :, :TH, :TW]
         tex += amp * up.numpy()
-    tex = np.clip(tex, 0.0, 1.0)
+    return np.clip(tex, 0.0, 1.0)
+
+
+def tum_like_sequence(n: int, H: int = 384, W: int = 512, seed: int = 0, step_px: float = 3.0,
+                      device="cuda") -> torch.Tensor:
+    """C2 stand-in when the TUM fr1_desk frames are absent: n frames of a
+    slowly panning camera over a smooth multi-scale noise texture (numpy
+    PCG64 `seed`), already resized/cropped to the 512x384 the reference's
+    resize_img produces from 640x480, normalised like ImgNorm.
+    Returns [n, 1, 3, H, W] float32 on `device`."""
+    pad = int(np.ceil(step_px * n)) + 8
+    tex = smooth_texture(H + pad, W + pad, seed)
     texd = torch.from_numpy(tex).to(device)
     out = torch.empty(n, 1, 3, H, W, device=device)
     for i in range(n):

@@ -147,8 +147,11 @@ def test_sharded_add_factors_matches_single_rank_gloo(ws):
 
 
 @pytest.mark.gpu
-def test_world_gaussians_matches_numpy():
-    from splatt3r_amd.pairs import world_gaussians
+def test_world_records_matches_numpy():
+    """world_records (the map records of refresh_map, include/s3w.h) with its
+    filters off: the world transform of gaussians_to_world vs numpy."""
+    import lietorch
+    from splatt3r_amd.splatt3r_utils import world_records
     rng = np.random.default_rng(0)
     h, w = 4, 6
     q = rng.normal(size=(1, h, w, 4)).astype(np.float32)
@@ -160,7 +163,9 @@ def test_world_gaussians_matches_numpy():
                opacities=torch.from_numpy(rng.uniform(size=(1, h, w, 1)).astype(np.float32)))
     T = torch.tensor([0.1, -0.2, 0.3, 0.0, 0.0, np.sin(0.2), np.cos(0.2), 1.5])
     img = torch.from_numpy(rng.uniform(-1, 1, (1, 3, h, w)).astype(np.float32))
-    out = world_gaussians({k: v[0].cuda() for k, v in res.items()}, T.cuda(), img.cuda())
+    M = lietorch.Sim3(T.cuda().reshape(1, 8)).matrix()[0]
+    out, cnt = world_records({k: v[0].cuda() for k, v in res.items()}, img.cuda()[0], M)
+    assert int(cnt) == h * w
     out = out.cpu().numpy()
     # numpy restatement of splatt3r_utils.py:290-312
     c, s_ = np.cos(0.4), np.sin(0.4)
@@ -238,11 +243,39 @@ def _gpu_shard_worker(rank, ws, port, q):
                     want[p] = [t[s_] for t in res]
             ok = all(torch.equal(got[k][p], want[p][k]) for p in range(len(pairs))
                      for k in range(6))
-            q.put((rank, ok))
+            # the global-map refresh: keyframe k re-inferred against partner
+            # k+1 (k-1 for the last) on rank k mod 2, world records at its
+            # pose, all-gathered into both ranks' maps
+            from splatt3r_amd.gaussian_map import SharedGaussians, render_map
+            import lietorch
+            poses = torch.stack([lietorch.Sim3.Identity(1, device=dev).data.reshape(8)] * 4)
+            poses[:, 0] = torch.arange(4, device=dev) * 0.05
+            edges_i, edges_j = [0, 1, 2, 3], [1, 2, 3, 2]
+            sh.gmap = SharedGaussians(max_gaussians=1 << 20, device=dev)
+            sh.refresh_map(edges_i, edges_j, poses, spatial_stride=4)
+            _beat(rank, "map refreshed")
+            sh.stop()
+            local = PairShard(model, dev, gmap=SharedGaussians(max_gaussians=1 << 20, device=dev))
+            for k in range(4):
+                local.register_local(k, kfs[k])
+            local.refresh_map(edges_i, edges_j, poses, spatial_stride=4)
+            n = sh.gmap.n_gaussians
+            map_ok = n == local.gmap.n_gaussians and n > 0 and all(
+                torch.equal(getattr(sh.gmap, a)[:n], getattr(local.gmap, a)[:n])
+                for a in ("means", "cov_triu", "colors", "opacities", "kf_id"))
+            T = np.eye(4, dtype=np.float32)
+            T[2, 3] = -1.0
+            img0 = render_map(sh.gmap, T, 256, 192, 60.0)
+            img1 = render_map(local.gmap, T, 256, 192, 60.0)
+            q.put((rank, (ok, map_ok, bool(torch.equal(img0, img1)), n,
+                          sh.gmap.means[:n].double().sum().item())))
         else:
+            from splatt3r_amd.gaussian_map import SharedGaussians
+            sh.gmap = SharedGaussians(max_gaussians=1 << 20, device=dev)
             sh.serve()
             _beat(rank, "served")
-            q.put((rank, sh.stats["pairs"]))
+            n = sh.gmap.n_gaussians
+            q.put((rank, (sh.stats["pairs"], n, sh.gmap.means[:n].double().sum().item())))
     except Exception as e:           # report instead of leaving the peer blocked
         q.put((rank, f"error: {e!r}"))
         raise
@@ -255,7 +288,10 @@ def test_sharded_pairs_two_ranks_on_gpu_match_local_decode():
     """Two ranks on the GPU (gloo transport staged through the host): keyframe
     features broadcast from rank 0, pairs decoded on rank p mod 2 with the
     real network, idx/valid/Q gathered back in pair order -- identical to
-    decoding the same per-rank batches locally."""
+    decoding the same per-rank batches locally.  Then the global-map refresh
+    (PairShard.refresh_map): edges re-inferred across the ranks, filtered
+    world records all-gathered into both ranks' SharedGaussians -- both maps
+    equal the single-rank map and render_map of it is bit-identical."""
     ws, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -275,5 +311,71 @@ def test_sharded_pairs_two_ranks_on_gpu_match_local_decode():
                 p.kill()
     for p in procs:
         assert p.exitcode == 0
-    assert res[0] is True
-    assert res[1] == 2          # pairs 1 and 3 ran on rank 1
+    ok, map_ok, render_ok, n0, sum0 = res[0]
+    pairs1, n1, sum1 = res[1]
+    assert ok is True
+    assert pairs1 == 2          # pairs 1 and 3 ran on rank 1
+    # refresh_map: both ranks hold the same map, equal to the single-rank map,
+    # and its render is bit-identical
+    assert map_ok and render_ok
+    assert n0 == n1 and sum0 == sum1
+
+
+def fake_map(pairs, poses, params):
+    """Deterministic stand-in for PairShard._map_records (no network on the
+    CPU): a variable number of records per edge, valued from the edge, the
+    keyframe pose and the filter parameters."""
+    out = []
+    for i, j in pairs:
+        n = 3 + (5 * i + j) % 7
+        base = poses[i].sum() + float(params[1]) + 10 * i + j
+        out.append(base + torch.arange(n * 13, dtype=torch.float32).reshape(n, 13) * 0.5)
+    return out
+
+
+MAP_EDGES = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (0, 2), (1, 3)]
+
+
+def _map_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from splatt3r_amd.pairs import PairShard
+    sh = PairShard(None, "cpu", match_fn=fake_match, map_fn=fake_map)
+    poses = torch.arange(6 * 8, dtype=torch.float32).reshape(6, 8) * 0.1
+    if rank == 0:
+        for k, f in enumerate(_kf_frames(6)):
+            sh.broadcast_keyframe(k, f)
+        recs = sh.refresh_map([e[0] for e in MAP_EDGES], [e[1] for e in MAP_EDGES], poses,
+                              spatial_stride=4, depth_max_percentile=0.9)
+        sh.stop()
+    else:
+        sh.serve()
+        recs = sh.last_map
+    q.put((rank, [r.numpy() for r in recs]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_sharded_map_refresh_matches_single_rank_gloo(ws):
+    """refresh_map over ws gloo ranks: edge e re-inferred on rank e mod ws,
+    variable-length record sets all-gathered -- every rank holds exactly the
+    single-rank records, in edge order."""
+    from splatt3r_amd.pairs import PairShard
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_map_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sh = PairShard(None, "cpu", map_fn=fake_map)
+    poses = torch.arange(6 * 8, dtype=torch.float32).reshape(6, 8) * 0.1
+    want = sh.refresh_map([e[0] for e in MAP_EDGES], [e[1] for e in MAP_EDGES], poses,
+                          spatial_stride=4, depth_max_percentile=0.9)
+    for r in range(ws):
+        assert len(res[r]) == len(MAP_EDGES)
+        for got, w in zip(res[r], want):
+            np.testing.assert_array_equal(got, w.numpy())

@@ -1,5 +1,7 @@
 """Frontend (main.py:395-535 loop body) on the GPU: the side-stream encoder
 pipelining must not change a single output bit."""
+import os
+
 import pytest
 import torch
 
@@ -194,6 +196,18 @@ def test_frontend_with_backend_single_thread():
     assert be.factor_graph.ii.numel() >= 1
     for k in range(n_kf):
         assert torch.isfinite(fe.keyframes[k].T_WC.data).all()
+    # global-map refresh (C5): every keyframe re-inferred, filtered world
+    # Gaussians at its optimised pose, appended with opacity > 0.3
+    import numpy as np
+    from splatt3r_amd.gaussian_map import SharedGaussians, render_map
+    gm = SharedGaussians(max_gaussians=1 << 21, device=dev)
+    recs = be.refresh_map(gm)
+    assert len(recs) == n_kf
+    kept = sum(int((r[:, 12] > 0.3).sum()) for r in recs)
+    assert gm.n_gaussians == kept > 0
+    assert all(r.shape[0] <= (384 // 4) * (512 // 4) for r in recs)   # stride 4
+    img = render_map(gm, np.eye(4, dtype=np.float32), 256, 192, 60.0)
+    assert torch.isfinite(img).all() and float(img.mean()) > 0
 
 
 def _backend_run(model, frames, dev, mode, n=20):
@@ -305,3 +319,29 @@ def _reloc_cases(dev, model, frames, Backend, Keyframes, Mode, Frontend):
             assert torch.isfinite(fe.keyframes[n_kf].T_WC.data).all()
         else:
             assert fe.mode == Mode.RELOC and len(fe.keyframes) == n_kf
+
+
+@pytest.mark.gpu
+def test_frontend_writes_render_pngs(tmp_path):
+    """The per-frame render export (main.py:436-446 gs_init_*, 490-506
+    gs_track_*) through dataio.RenderWriter: one PNG per rendered frame,
+    holding uint8(clamp(render) * 255) of the same frame rendered without
+    the writer."""
+    import numpy as np
+    from PIL import Image
+    from splatt3r_amd.dataio import RenderWriter, render_to_uint8
+    from splatt3r_amd.slam import Frontend
+    dev, model, frames = _model_and_frames(5)
+    w = RenderWriter(tmp_path / "renders", workers=2)
+    fe = Frontend(model, device=dev, spatial_stride=4, render=True, render_writer=w)
+    for i in range(5):
+        fe.step(i, frames[i])
+    w.close()
+    names = sorted(os.listdir(tmp_path / "renders"))
+    assert names == ["gs_init_000000.png"] + [f"gs_track_{i:06d}.png" for i in range(1, 5)]
+    fe2 = Frontend(model, device=dev, spatial_stride=4, render=True)
+    for i in range(5):
+        fe2.step(i, frames[i])
+        want = render_to_uint8(fe2.last_render.cpu().numpy())
+        got = np.asarray(Image.open(tmp_path / "renders" / names[i]))
+        np.testing.assert_array_equal(got, want)
