@@ -136,7 +136,7 @@ class Backend:
         if self.shard is not None and self.shard.ws > 1:
             sh = self.shard
         else:
-            sh = PairShard(self.model, self.device)
+            sh = PairShard(self.model, self.device, local=True)
             for k in ks:
                 sh.register_local(k, self.keyframes[k])
         sh.gmap = gmap

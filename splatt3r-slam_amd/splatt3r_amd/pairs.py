@@ -112,7 +112,7 @@ class PairShard:
     testable without the network (tests/test_pairs.py)."""
 
     def __init__(self, model, device, match_fn: Optional[Callable] = None, Q_conf=None,
-                 map_fn: Optional[Callable] = None, gmap=None):
+                 map_fn: Optional[Callable] = None, gmap=None, local: bool = False):
         from splatt3r_amd.config import config
         self.model = model
         # map_fn(pairs, poses [n_kf, 8], params [4]) -> list of [n_p, 13] world
@@ -123,8 +123,9 @@ class PairShard:
         self.gmap = gmap
         self.last_map = None
         self.device = torch.device(device)
-        self.ws = dist.get_world_size() if _backend() else 1
-        self.rank = dist.get_rank() if _backend() else 0
+        # local: this rank alone, even inside a process group
+        self.ws = dist.get_world_size() if _backend() and not local else 1
+        self.rank = dist.get_rank() if _backend() and not local else 0
         self.match_fn = match_fn or (lambda *a: splatt3r_match_symmetric(model, *a))
         self.Q_conf = config["local_opt"]["Q_conf"] if Q_conf is None else Q_conf
         self.kf: dict[int, tuple] = {}   # keyframe index -> (feat, pos, true_shape)

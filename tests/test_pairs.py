@@ -226,7 +226,6 @@ def _gpu_shard_worker(rank, ws, port, q):
             _beat(rank, "keyframes broadcast")
             got = sh.match_pairs([p[0] for p in pairs], [p[1] for p in pairs])
             _beat(rank, "pairs gathered")
-            sh.stop()
             # the same per-rank batches decoded locally, reassembled in order
             want = [None] * len(pairs)
             for r in range(ws):
@@ -252,13 +251,15 @@ def _gpu_shard_worker(rank, ws, port, q):
             poses[:, 0] = torch.arange(4, device=dev) * 0.05
             edges_i, edges_j = [0, 1, 2, 3], [1, 2, 3, 2]
             sh.gmap = SharedGaussians(max_gaussians=1 << 20, device=dev)
-            sh.refresh_map(edges_i, edges_j, poses, spatial_stride=4)
+            # (portable-PRNG opacities sit near 0.12: threshold 0 keeps them)
+            sh.refresh_map(edges_i, edges_j, poses, spatial_stride=4, opacity_threshold=0.0)
             _beat(rank, "map refreshed")
             sh.stop()
-            local = PairShard(model, dev, gmap=SharedGaussians(max_gaussians=1 << 20, device=dev))
+            local = PairShard(model, dev, gmap=SharedGaussians(max_gaussians=1 << 20, device=dev),
+                              local=True)
             for k in range(4):
                 local.register_local(k, kfs[k])
-            local.refresh_map(edges_i, edges_j, poses, spatial_stride=4)
+            local.refresh_map(edges_i, edges_j, poses, spatial_stride=4, opacity_threshold=0.0)
             n = sh.gmap.n_gaussians
             map_ok = n == local.gmap.n_gaussians and n > 0 and all(
                 torch.equal(getattr(sh.gmap, a)[:n], getattr(local.gmap, a)[:n])

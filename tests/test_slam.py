@@ -201,9 +201,12 @@ def test_frontend_with_backend_single_thread():
     import numpy as np
     from splatt3r_amd.gaussian_map import SharedGaussians, render_map
     gm = SharedGaussians(max_gaussians=1 << 21, device=dev)
-    recs = be.refresh_map(gm)
+    # the portable-PRNG head puts opacities near sigmoid(-2) = 0.12: the
+    # reference's 0.3 map threshold would keep none, so append everything
+    # that survives gaussians_to_world's filters
+    recs = be.refresh_map(gm, opacity_threshold=0.0)
     assert len(recs) == n_kf
-    kept = sum(int((r[:, 12] > 0.3).sum()) for r in recs)
+    kept = sum(int((r[:, 12] > 0.0).sum()) for r in recs)
     assert gm.n_gaussians == kept > 0
     assert all(r.shape[0] <= (384 // 4) * (512 // 4) for r in recs)   # stride 4
     img = render_map(gm, np.eye(4, dtype=np.float32), 256, 192, 60.0)
