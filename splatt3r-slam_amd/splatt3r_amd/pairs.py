@@ -398,7 +398,9 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
 
     def map_refresh():
         if rank == 0:
-            sh.refresh_map(map_i, map_j, poses, spatial_stride=4)
+            # opacity threshold 0: the portable-PRNG head's opacities sit near
+            # 0.12, under the reference's 0.3, which would leave the map empty
+            sh.refresh_map(map_i, map_j, poses, spatial_stride=4, opacity_threshold=0.0)
             if ws > 1:
                 sh.stop()
         else:
@@ -435,8 +437,8 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
                             "map_gaussians": sh.gmap.n_gaussians,
                             "path": "PairShard.refresh_map: keyframe k re-inferred on rank k mod "
                                     "W, gaussians_to_world filters (stride 4, q 0.98, max scale "
-                                    "1, conf 1.5) -> all-gather -> SharedGaussians (opacity > "
-                                    "0.3)"})
+                                    "1, conf 1.5) -> all-gather -> SharedGaussians (opacity "
+                                    "threshold 0 with PRNG weights; reference 0.3)"})
     if ws > 1:
         out["keyframe_broadcast_ms"] = t_bc / n_kf * 1e3
     return out
