@@ -67,10 +67,9 @@ constexpr int kDupRanks = 512;  // depth ranks per duplication wave
 inline int64_t nsegs(int64_t n) { return std::max<int64_t>(1, s3::cdiv(n, kSegItems)); }
 
 struct GeomState {
-  float* depth;
   float4* rec0;  // x, y, conic.a, conic.b
   float4* rec1;  // conic.c, opacity, rgb.r, rgb.g (the blend's staged record)
-  float* rgb;    // [P,3]
+  float* blue;   // [P] rgb.b (r, g ride in rec1)
   float* cov3D;  // [P,6] (scale/rotation path)
   uint8_t* clamped;  // [P,3]
   // duplication record per Gaussian: x = x0 | y0 << 16, y = rect w | h << 16,
@@ -91,10 +90,9 @@ struct GeomState {
 GeomState carve_geom(void* base, int64_t P, size_t* total = nullptr) {
   Carver c{static_cast<char*>(base)};
   GeomState g;
-  g.depth = c.take<float>(P);
   g.rec0 = c.take<float4>(P);
   g.rec1 = c.take<float4>(P);
-  g.rgb = c.take<float>(P * 3);
+  g.blue = c.take<float>(P);
   g.cov3D = c.take<float>(P * 6);
   g.clamped = c.take<uint8_t>(P * 3);
   g.dup = c.take<uint4>(P);
@@ -194,10 +192,10 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
              const float* __restrict__ vm, const float* __restrict__ pm,
              const float* __restrict__ campos, int32_t* __restrict__ radii, GeomState g,
              uint32_t* key_out) {
-  // depth-sort key/value (fused here instead of a separate pass): culled
-  // Gaussians sort last and emit nothing.  Every per-Gaussian output is
-  // stored once: a culled Gaussian's here, a kept one's at the end.
-  g.dval[0][i] = (uint32_t)i;
+  // depth-sort key (fused here instead of a separate pass; the first sort
+  // pass takes the index as its value): culled Gaussians sort last and emit
+  // nothing.  Every per-Gaussian output is stored once: a culled Gaussian's
+  // here, a kept one's at the end.
   auto cull = [&]() -> uint32_t {
     radii[i] = 0;
     g.dup[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -255,8 +253,7 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
       rgb[ch] = fmaxf(acc, 0.0f);
     }
   }
-  g.rgb[i * 3 + 0] = rgb[0]; g.rgb[i * 3 + 1] = rgb[1]; g.rgb[i * 3 + 2] = rgb[2];
-  g.depth[i] = pv[2];
+  g.blue[i] = rgb[2];
   radii[i] = r;
   g.rec0[i] = make_float4(px, py, c * det_inv, -b * det_inv);
   g.rec1[i] = make_float4(a * det_inv, opac[i], rgb[0], rgb[1]);
@@ -469,8 +466,9 @@ struct Digit {
   }
 };
 
+template <typename K>
 __global__ void __launch_bounds__(kSortThreads)
-k_rs_hist(int64_t n, const uint32_t* __restrict__ keys, Digit dg, int64_t nseg,
+k_rs_hist(int64_t n, const K* __restrict__ keys, Digit dg, int64_t nseg,
           uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[kMaxBins];
   const int bins = 1 << dg.bits;
@@ -483,7 +481,7 @@ k_rs_hist(int64_t n, const uint32_t* __restrict__ keys, Digit dg, int64_t nseg,
 #pragma unroll
   for (int j = 0; j < kSortPerLane; ++j) {
     const int64_t i = i0 + j * kSortThreads + threadIdx.x;
-    key[j] = i < n ? keys[i] : 0u;
+    key[j] = i < n ? (uint32_t)keys[i] : 0u;
   }
 #pragma unroll
   for (int j = 0; j < kSortPerLane; ++j) {
@@ -499,16 +497,16 @@ k_rs_hist(int64_t n, const uint32_t* __restrict__ keys, Digit dg, int64_t nseg,
 
 // One segment of kSegItems items: wave w owns items [w * 512, (w + 1) *
 // 512) of it, in 8 windows of 64.
-template <typename V>
+template <typename K, typename V>
 __global__ void __launch_bounds__(kSortThreads)
-k_rs_scatter(int64_t n, const uint32_t* __restrict__ kin, const V* __restrict__ vin,
-             uint32_t* __restrict__ kout, V* __restrict__ vout, Digit dg, int64_t nseg,
+k_rs_scatter(int64_t n, const K* __restrict__ kin, const V* __restrict__ vin,
+             K* __restrict__ kout, V* __restrict__ vout, Digit dg, int64_t nseg,
              const uint32_t* __restrict__ hist, const uint32_t* __restrict__ tot) {
   constexpr int NW = kSortThreads / 64;
   __shared__ uint32_t cnt[NW][kMaxBins];  // per-wave counts -> local slots
   __shared__ uint32_t gdelta[kMaxBins];   // global slot - local slot, per digit
   __shared__ uint32_t s_w[NW];
-  __shared__ uint32_t sk[kSegItems];
+  __shared__ K sk[kSegItems];
   __shared__ V sv[kSegItems];
   const int bins = 1 << dg.bits;
   for (int d = threadIdx.x; d < NW * kMaxBins; d += kSortThreads) (&cnt[0][0])[d] = 0u;
@@ -524,8 +522,9 @@ k_rs_scatter(int64_t n, const uint32_t* __restrict__ kin, const V* __restrict__ 
 #pragma unroll
   for (int j = 0; j < kSortPerLane; ++j) {
     const int64_t i = base_w + j * 64 + lane;
-    key[j] = i < n ? kin[i] : 0u;
-    val[j] = i < n ? vin[i] : V(0);
+    key[j] = i < n ? (uint32_t)kin[i] : 0u;
+    // vin == nullptr: the item's own index (first pass of the depth sort)
+    val[j] = i < n ? (vin ? vin[i] : (V)i) : V(0);
   }
 #pragma unroll
   for (int j = 0; j < kSortPerLane; ++j) {
@@ -584,7 +583,7 @@ k_rs_scatter(int64_t n, const uint32_t* __restrict__ kin, const V* __restrict__ 
       const uint32_t b = cnt[w][d];
       const uint32_t lp = b + (uint32_t)__popcll(peers & lanemask_lt(lane));
       if ((peers >> lane) == 1ull) cnt[w][d] = b + (uint32_t)__popcll(peers);
-      sk[lp] = key[j];
+      sk[lp] = (K)key[j];
       sv[lp] = val[j];
     }
     wave_lds_sync();
@@ -596,8 +595,8 @@ k_rs_scatter(int64_t n, const uint32_t* __restrict__ kin, const V* __restrict__ 
   for (int j = 0; j < kSortPerLane; ++j) {
     const int lp = j * kSortThreads + threadIdx.x;
     if (lp < m) {
-      const uint32_t k = sk[lp];
-      const uint32_t gp = (uint32_t)lp + gdelta[dg(k)];
+      const K k = sk[lp];
+      const uint32_t gp = (uint32_t)lp + gdelta[dg((uint32_t)k)];
       if (kout) kout[gp] = k;
       vout[gp] = sv[lp];
     }
@@ -662,17 +661,18 @@ __global__ void __launch_bounds__(1024) k_seg_scan(uint32_t* __restrict__ cnt_se
 // stores.  Waves are independent (no workgroup barriers).
 constexpr int DCH = 512;
 
+template <typename K>
 __global__ void __launch_bounds__(kThreads)
 k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ order,
             const uint4* __restrict__ dsorted,
-            const uint32_t* __restrict__ seg_off, int64_t nwseg, uint32_t* __restrict__ keys,
+            const uint32_t* __restrict__ seg_off, int64_t nwseg, K* __restrict__ keys,
             uint32_t* __restrict__ vals) {
-  __shared__ uint32_t s_key[kThreads / 64][DCH];
+  __shared__ K s_key[kThreads / 64][DCH];
   __shared__ uint32_t s_val[kThreads / 64][DCH];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t ws = (int64_t)blockIdx.x * (kThreads / 64) + w;
   if (ws >= nwseg) return;
-  uint32_t* sk = s_key[w];
+  K* sk = s_key[w];
   uint32_t* sv = s_val[w];
   uint32_t running = seg_off[ws];
   const int64_t k_base = ws * kDupRanks + lane;
@@ -715,14 +715,14 @@ k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ order,
             const int pos = __builtin_ctzll(m);
             m &= m - 1;
             if (q >= c0) {
-              sk[q - c0] = (uint32_t)((y0 + pos / rw) * gx + x0 + pos % rw);
+              sk[q - c0] = (K)((y0 + pos / rw) * gx + x0 + pos % rw);
               sv[q - c0] = i;
             }
           }
         } else {
           const uint32_t j0 = max(c0, start) - start, j1 = min(c1, start + cnt) - start;
           for (uint32_t j = j0; j < j1; ++j) {
-            sk[start + j - c0] = (uint32_t)((y0 + (int)j / rw) * gx + x0 + (int)j % rw);
+            sk[start + j - c0] = (K)((y0 + (int)j / rw) * gx + x0 + (int)j % rw);
             sv[start + j - c0] = i;
           }
         }
@@ -737,8 +737,9 @@ k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ order,
   }
 }
 
+template <typename K>
 __global__ void __launch_bounds__(kThreads)
-k_ranges(int64_t R, const uint32_t* __restrict__ keys, uint2* __restrict__ ranges) {
+k_ranges(int64_t R, const K* __restrict__ keys, uint2* __restrict__ ranges) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R) return;
   const uint32_t cur = keys[i];
@@ -763,9 +764,10 @@ inline int tile_sort_buffer(int ntiles) {
   return sort_passes(bit_length((uint64_t)(ntiles - 1))) & 1;
 }
 
-template <typename V>
-int radix_sort(int64_t n, uint32_t* keys[2], V* vals[2], uint32_t kmin, uint32_t span, int bits,
-               bool keep_keys, uint32_t* hist, uint32_t* tot, hipStream_t st) {
+template <typename K, typename V>
+int radix_sort(int64_t n, K* keys[2], V* vals[2], uint32_t kmin, uint32_t span, int bits,
+               bool keep_keys, uint32_t* hist, uint32_t* tot, hipStream_t st,
+               bool index_vals = false) {
   const int passes = sort_passes(bits);
   const int width = (bits + passes - 1) / passes;
   const int64_t nseg = nsegs(n);
@@ -773,11 +775,11 @@ int radix_sort(int64_t n, uint32_t* keys[2], V* vals[2], uint32_t kmin, uint32_t
   for (int p = 0; p < passes; ++p) {
     const int hi = std::min(bits, (p + 1) * width);
     const Digit dg{kmin, span, p * width, std::max(1, hi - p * width)};
-    k_rs_hist<<<(unsigned)nseg, kSortThreads, 0, st>>>(n, keys[src], dg, nseg, hist);
+    k_rs_hist<K><<<(unsigned)nseg, kSortThreads, 0, st>>>(n, keys[src], dg, nseg, hist);
     k_row_scan<<<1u << dg.bits, kThreads, 0, st>>>(hist, nseg, tot);
     const bool last = p == passes - 1;
-    k_rs_scatter<V><<<(unsigned)nseg, kSortThreads, 0, st>>>(
-        n, keys[src], vals[src], (!last || keep_keys) ? keys[src ^ 1] : nullptr, vals[src ^ 1],
+    k_rs_scatter<K, V><<<(unsigned)nseg, kSortThreads, 0, st>>>(
+        n, keys[src], (p == 0 && index_vals) ? nullptr : vals[src], (!last || keep_keys) ? keys[src ^ 1] : nullptr, vals[src ^ 1],
         dg, nseg, hist, tot);
     src ^= 1;
   }
@@ -814,7 +816,7 @@ k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
       const uint32_t id = point_list[range.x + prog];
       s_r0[threadIdx.x] = g.rec0[id];
       s_r1[threadIdx.x] = g.rec1[id];
-      s_b[threadIdx.x] = g.rgb[id * 3 + 2];
+      s_b[threadIdx.x] = g.blue[id];
     }
     __syncthreads();
     const int n = todo < BS ? todo : BS;
@@ -991,7 +993,7 @@ k_blend_backward(int W, int H, int gx, int ntiles, const uint2* __restrict__ ran
       s_id[threadIdx.x] = id;
       s_r0[threadIdx.x] = g.rec0[id];
       s_r1[threadIdx.x] = g.rec1[id];
-      s_b[threadIdx.x] = g.rgb[id * 3 + 2];
+      s_b[threadIdx.x] = g.blue[id];
     }
 #pragma unroll
     for (int k = 0; k < kGS; ++k) s_acc[threadIdx.x * kGS + k] = 0.f;
@@ -1362,8 +1364,9 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
     }
     // visible keys map to [0, kmax - kmin], culled ones (~0u) to span
     const uint32_t span = kmax - kmin + 1u;
-    const int dsrc = radix_sort<uint32_t>(P, g.dkey, g.dval, kmin, span, bit_length(span), false,
-                                          g.dhist, g.dtot, st);
+    const int dsrc = radix_sort<uint32_t, uint32_t>(P, g.dkey, g.dval, kmin, span,
+                                                    bit_length(span), false, g.dhist, g.dtot, st,
+                                                    true);
     const uint32_t* order = g.dval[dsrc];
     tmark(4, st);
     const int64_t nwseg = s3::cdiv(P, kDupRanks);
@@ -1371,14 +1374,29 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
     k_order_gather<<<dup_blocks, kThreads, 0, st>>>(P, order, g.dup, nwseg, g.dup_sorted,
                                                     g.cnt_seg);
     k_seg_scan<<<1, 1024, 0, st>>>(g.cnt_seg, nwseg);
-    k_duplicate<<<dup_blocks, kThreads, 0, st>>>(P, gx, order, g.dup_sorted, g.cnt_seg, nwseg,
-                                                 b.keys[0], b.vals[0]);
-    const int tsrc = radix_sort<uint32_t>(R, b.keys, b.vals, 0u, 0xFFFFFFFFu,
-                                          bit_length((uint64_t)(ntiles - 1)), true, b.hist, b.tot,
-                                          st);
+    // tile ids as 16-bit keys up to 65536 tiles: the two tile passes and the
+    // ranges pass move 6 B per instance instead of 8
+    const int tbits = bit_length((uint64_t)(ntiles - 1));
+    int tsrc;
+    if (ntiles <= 65536) {
+      uint16_t* k16[2] = {reinterpret_cast<uint16_t*>(b.keys[0]),
+                          reinterpret_cast<uint16_t*>(b.keys[1])};
+      k_duplicate<uint16_t><<<dup_blocks, kThreads, 0, st>>>(P, gx, order, g.dup_sorted,
+                                                             g.cnt_seg, nwseg, k16[0], b.vals[0]);
+      tsrc = radix_sort<uint16_t, uint32_t>(R, k16, b.vals, 0u, 0xFFFFFFFFu, tbits, true, b.hist,
+                                            b.tot, st);
+      k_ranges<uint16_t><<<(unsigned)s3::cdiv(R, kThreads), kThreads, 0, st>>>(R, k16[tsrc],
+                                                                             im.ranges);
+    } else {
+      k_duplicate<uint32_t><<<dup_blocks, kThreads, 0, st>>>(P, gx, order, g.dup_sorted,
+                                                             g.cnt_seg, nwseg, b.keys[0], b.vals[0]);
+      tsrc = radix_sort<uint32_t, uint32_t>(R, b.keys, b.vals, 0u, 0xFFFFFFFFu, tbits, true,
+                                            b.hist, b.tot, st);
+      k_ranges<uint32_t><<<(unsigned)s3::cdiv(R, kThreads), kThreads, 0, st>>>(R, b.keys[tsrc],
+                                                                             im.ranges);
+    }
     S3_REQUIRE(tsrc == tile_sort_buffer(ntiles), "gsr_render: tile sort buffer mismatch");
     point_list = b.vals[tsrc];
-    k_ranges<<<(unsigned)s3::cdiv(R, kThreads), kThreads, 0, st>>>(R, b.keys[tsrc], im.ranges);
     S3_LAUNCH_CHECK();
   } else {
     tmark(4, st);

@@ -164,21 +164,36 @@ def _restage(sc, z):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["plane", "two_depths", "wide_range", "all_culled", "tail_4097",
-                                  "tiles_3600", "tiles_8160"])
+                                  "tail_8193", "tiles_3600", "tiles_8160", "tiles_8832",
+                                  "big_splats", "ragged_1x1"])
 def test_hip_binning_edge_cases_bitexact_vs_oracle(case):
     """The hand-written depth / tile sorts (raster.hip "sorting"): equal
     depths (stability by index), a 1-2 pass key width, a 4-pass key width,
-    nothing visible (R = 0), a segment tail, and tile ids of 12 and 13 bits
-    (two 6/7-bit tile passes) -- bit-exact against the oracle."""
+    nothing visible (R = 0), segment tails (4096 and 8192 items), tile ids
+    of 12, 13 and 14 bits, splats whose rect exceeds the 64-tile mask (plain
+    rect enumeration), and a ragged 1-tile image -- bit-exact against the
+    oracle."""
     rng = np.random.default_rng(7)
     P, H, W, fx = 3000, 48, 64, 60.0
     if case == "tail_4097":
         P = 4097
+    if case == "tail_8193":
+        P = 8193
     if case == "tiles_3600":
         H, W, fx = 720, 1280, 900.0
     if case == "tiles_8160":
         H, W, fx = 1088, 1920, 1300.0
+    if case == "tiles_8832":
+        H, W, fx = 1104, 2048, 1400.0
+    if case == "big_splats":
+        P, H, W, fx = 2000, 540, 960, 700.0
+    if case == "ragged_1x1":
+        H, W, fx = 13, 9, 12.0
     sc = small_scene(P, 11, H=H, W=W, fx=fx)
+    if case == "big_splats":
+        # sigma x 12: rects of ~10 x 10 tiles and more (> 64: no tile mask)
+        sc = dict(sc)
+        sc["cov6"] = (sc["cov6"] * 144.0).astype(np.float32)
     if case == "plane":
         sc = _restage(sc, np.full(P, 3.0, np.float32))
     elif case == "two_depths":
