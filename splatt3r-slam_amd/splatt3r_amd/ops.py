@@ -192,6 +192,8 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
                 26: (64, 64), 27: (128, 128), 28: (64, 128), 29: (96, 128), 30: (64, 192),
                 31: (64, 64)}
 _TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14}   # the fused tail runs with one K-group
+# S3_GEMM_MF16=0: leave the 16x16x32 tile family out of the tuner (A/B)
+_EXCLUDED = set(range(21, 32)) if os.environ.get("S3_GEMM_MF16", "1") == "0" else set()
 
 
 def _tune_key(a):
@@ -206,6 +208,8 @@ def _tune_candidates(a, split_ok):
     kt = -(-a.K // 64)
     out = []
     for tile, (bm, bn) in _TILE_SHAPES.items():
+        if tile in _EXCLUDED:
+            continue
         if a.tail_n and (bn != a.N or tile not in _TAIL_OK):
             continue
         tiles = a.groups * -(-a.M // bm) * -(-a.N // bn)
