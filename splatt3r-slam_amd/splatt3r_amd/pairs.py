@@ -19,8 +19,10 @@ keyframe pair in both orders and matches both directions
     re-infers its share of the factor-graph edges, turns keyframe i's
     prediction of edge (i, j) into world Gaussians with gaussians_to_world's
     filters at the optimised pose (splatt3r_utils.py:180-328, one HIP pass),
-    and one all-gather (`gather_map`, 52 B per Gaussian) gives every rank
-    the whole map in edge order; each rank rebuilds its SharedGaussians
+    and two all-gathers of fixed size (each pair's records padded to the
+    stride-subsampled pixel count, 52 B per row, plus the device counts)
+    give every rank the whole map in edge order without a host round trip;
+    each rank rebuilds its SharedGaussians
     (frame.py:388-443) from it, so any rank can render the full map
     (gaussian_map.render_map, visualization.py:467-600).
 
@@ -76,20 +78,31 @@ def _all_gather_equal(t: torch.Tensor, ws: int) -> list[torch.Tensor]:
     return [p.to(t.device) for p in parts]
 
 
-def gather_map(recs: torch.Tensor, ws: int) -> torch.Tensor:
-    """The map exchange: every rank contributes its [n_r, 13] world records,
-    every rank receives all of them in rank order (one all-gather; shards
-    of unequal size are padded to the largest and trimmed after)."""
-    if ws == 1:
-        return recs
-    dev = recs.device
-    n = torch.tensor([recs.shape[0]], device=dev, dtype=torch.int64)
-    ns = [int(x) for x in _all_gather_equal(n, ws)]
-    nmax = max(ns)
-    buf = torch.zeros(nmax, recs.shape[1], device=dev, dtype=recs.dtype)
-    buf[:recs.shape[0]] = recs
-    parts = _all_gather_equal(buf, ws)
-    return torch.cat([p[:k] for p, k in zip(parts, ns)])
+class MapRecords:
+    """Per-edge world records of a map refresh, kept on the device in edge
+    order: buffers [n, cap, 13] (rows past counts[p] are padding) and
+    counts [n] int64.  The map rebuild consumes them with device counts (no
+    host read); iterating / indexing gives the compacted [n_p, 13] tensors
+    (one host read of the counts)."""
+
+    def __init__(self, buffers: torch.Tensor, counts: torch.Tensor):
+        self.buffers, self.counts = buffers, counts
+        self._list = None
+
+    def __len__(self):
+        return self.buffers.shape[0]
+
+    def _compact(self):
+        if self._list is None:
+            ns = self.counts.tolist()
+            self._list = [self.buffers[p, :k] for p, k in enumerate(ns)]
+        return self._list
+
+    def __iter__(self):
+        return iter(self._compact())
+
+    def __getitem__(self, p):
+        return self._compact()[p]
 
 
 def q_weighted(m, Q_conf):
@@ -112,14 +125,18 @@ class PairShard:
     testable without the network (tests/test_pairs.py)."""
 
     def __init__(self, model, device, match_fn: Optional[Callable] = None, Q_conf=None,
-                 map_fn: Optional[Callable] = None, gmap=None, local: bool = False):
+                 map_fn: Optional[Callable] = None, gmap=None, local: bool = False,
+                 map_cap: Optional[Callable] = None):
         from splatt3r_amd.config import config
         self.model = model
-        # map_fn(pairs, poses [n_kf, 8], params [4]) -> list of [n_p, 13] world
-        # records per pair (default: re-inference + gaussians_to_world on the
-        # device); injectable like match_fn.  gmap: this rank's map buffer,
-        # rebuilt on every refresh_map (workers too).
+        # map_fn(pairs, poses [n_kf, 8], params (stride, q, max_scale, conf,
+        # opacity)) -> (records [k, cap', 13], counts [k] int64) for this
+        # rank's pairs, cap' <= map_cap(pairs, params) rows per pair, counts
+        # on the device (default: re-inference + gaussians_to_world on the
+        # device); injectable like match_fn, with its map_cap.  gmap: this
+        # rank's map buffer, rebuilt on every refresh_map (workers too).
         self.map_fn = map_fn or self._map_records
+        self.map_cap = map_cap or self._map_capacity
         self.gmap = gmap
         self.last_map = None
         self.device = torch.device(device)
@@ -239,75 +256,84 @@ class PairShard:
     # ------------------------------------------------------------- map ----
     def refresh_map(self, ii, jj, poses: torch.Tensor, spatial_stride: int = 1,
                     depth_max_percentile: float = 0.98, max_scale: float = 1.0,
-                    min_confidence: float = 1.5, opacity_threshold: float = 0.3):
+                    min_confidence: float = 1.5, opacity_threshold: float = 0.3) -> MapRecords:
         """Rank 0: re-infer the edges (ii[p], jj[p]) across the ranks and
         rebuild every rank's map from keyframe ii[p]'s world Gaussians at
         poses[ii[p]] (lietorch layout [n_kf, 8]), in edge order.  Returns
-        the per-edge [n_p, 13] records (on every rank)."""
+        the per-edge records (on every rank: `last_map`)."""
         pairs = list(zip((int(i) for i in ii), (int(j) for j in jj)))
         poses = poses.reshape(-1, 8).float().contiguous()
-        params = torch.tensor([spatial_stride, depth_max_percentile, max_scale, min_confidence,
-                               opacity_threshold], dtype=torch.float64, device=self.device)
+        hp = (float(spatial_stride), float(depth_max_percentile), float(max_scale),
+              float(min_confidence), float(opacity_threshold))
         if self.ws > 1:
             self._header(OP_MAP, len(pairs), poses.shape[0])
             self._bcast(torch.tensor(pairs, dtype=torch.int64, device=self.device).reshape(-1, 2))
             self._bcast(poses)
-            self._bcast(params)
-        return self._map_collective(pairs, poses, params)
+            self._bcast(torch.tensor(hp, dtype=torch.float64, device=self.device))
+        return self._map_collective(pairs, poses, hp)
 
-    def _map_collective(self, pairs, poses, params):
+    def _map_collective(self, pairs, poses, hp) -> MapRecords:
+        """Fixed-capacity exchange: every rank pads its pairs' records to
+        map_cap rows and sends them with their device counts in two
+        all-gathers of known size (no count round trip, no host read on the
+        NCCL path); re-cut into edge order on the device."""
         ws, rank, n = self.ws, self.rank, len(pairs)
+        dev = self.device
+        cap = int(self.map_cap(pairs, hp)) if n else 0
         mine = shard(pairs, ws, rank)
-        local = self.map_fn(mine, poses, params) if mine else []
+        per = -(-n // ws)
+        buf = torch.zeros(per, cap, GAUSS_FLOATS, device=dev)
+        cnt = torch.zeros(per, dtype=torch.int64, device=dev)
+        if mine:
+            rec, c = self.map_fn(mine, poses, hp)
+            k = len(mine)
+            buf[:k, :rec.shape[1]] = rec
+            cnt[:k] = c.reshape(k)
         if ws == 1:
-            recs = local
+            B, C = buf[:n], cnt[:n]
         else:
-            # per-pair counts (padded to the largest shard), then one all-gather
-            # of the records; both in rank order, re-cut into edge order
-            per = -(-n // ws)
-            cnt = torch.zeros(per, dtype=torch.int64, device=self.device)
-            for s_, r in enumerate(local):
-                cnt[s_] = r.shape[0]
-            cnts = [c.tolist() for c in _all_gather_equal(cnt, ws)]
-            flat = (torch.cat(local) if local else
-                    torch.zeros(0, GAUSS_FLOATS, device=self.device))
-            gathered = gather_map(flat, ws)
-            recs, off = [None] * n, 0
-            for r in range(ws):
-                for s_, p in enumerate(range(r, n, ws)):
-                    recs[p] = gathered[off:off + cnts[r][s_]]
-                    off += cnts[r][s_]
+            Gb = _all_gather_equal(buf, ws)
+            Gc = _all_gather_equal(cnt, ws)
+            # pair p sits on rank p % ws at local slot p // ws
+            B = torch.stack([Gb[p % ws][p // ws] for p in range(n)]) if n else buf[:0]
+            C = torch.stack([Gc[p % ws][p // ws] for p in range(n)]) if n else cnt[:0]
+        recs = MapRecords(B, C)
         self.last_map = recs
         if self.gmap is not None:
-            thr = float(params[4])
             self.gmap.clear()
-            for (i, _), r in zip(pairs, recs):
-                if r.shape[0]:
-                    self.gmap.append_records(r, torch.tensor([r.shape[0]], device=r.device), i, thr)
+            for p, (i, _) in enumerate(pairs):
+                self.gmap.append_records(B[p], C[p:p + 1], i, hp[4])
         return recs
 
-    def _map_records(self, pairs, poses, params):
+    def _map_capacity(self, pairs, hp):
+        """Records per pair at most: the stride-subsampled pixel grid."""
+        H, W = (int(v) for v in self.kf[pairs[0][0]][2].reshape(-1)[:2].tolist())
+        s = max(1, int(hp[0]))
+        return -(-H // s) * -(-W // s)
+
+    def _map_records(self, pairs, poses, hp):
         """This rank's edges: one batched pair decode (the backend's pair
         plans), keyframe i's self-prediction -> gaussians_to_world filters +
-        world transform at poses[i] (one HIP pass per edge)."""
+        world transform at poses[i] (one HIP pass per edge, device counts)."""
         from lietorch import Sim3
-        stride, q, max_scale, min_conf = (float(v) for v in params[:4].tolist())
+        stride, q, max_scale, min_conf = hp[:4]
         fi = torch.cat([self.kf[i][0] for i, _ in pairs])
         pi = torch.cat([self.kf[i][1] for i, _ in pairs])
         fj = torch.cat([self.kf[j][0] for _, j in pairs])
         pj = torch.cat([self.kf[j][1] for _, j in pairs])
         H, W = (int(v) for v in self.kf[pairs[0][0]][2].reshape(-1)[:2].tolist())
         r11, _, _ = self.model.encoder.infer_pair(fi, pi, fj, pj, (H, W), tag="backend")
-        out = []
+        recs, cnts = [], []
         for b, (i, _) in enumerate(pairs):
             view = {k: v[b] for k, v in r11.items()
                     if k in ("means", "scales", "rotations", "sh", "opacities", "conf")}
             M = Sim3(poses[i].reshape(1, 8).to(self.device)).matrix()[0]
             rec, cnt = world_records(view, self.kf[i][3][0], M, max(1, int(stride)), 0.05, q,
                                      max_scale, min_conf)
-            out.append(rec[:int(cnt.item())])
+            recs.append(rec)
+            cnts.append(cnt.reshape(1))
         self.stats["map_pairs"] = self.stats.get("map_pairs", 0) + len(pairs)
-        return out
+        return torch.stack(recs), torch.cat(cnts)
 
     # ---------------------------------------------------------- workers ---
     def serve(self):
@@ -325,9 +351,9 @@ class PairShard:
             elif op == OP_MAP:
                 pl = self._bcast(torch.empty(a, 2, dtype=torch.int64, device=self.device))
                 poses = self._bcast(torch.empty(b, 8, device=self.device))
-                params = self._bcast(torch.empty(5, dtype=torch.float64, device=self.device))
+                hp = self._bcast(torch.empty(5, dtype=torch.float64, device=self.device))
                 self._map_collective([tuple(int(v) for v in p) for p in pl.tolist()], poses,
-                                     params)
+                                     tuple(hp.tolist()))
 
     def stop(self):
         if self.rank == 0 and self.ws > 1:

@@ -28,34 +28,6 @@ def _free_port():
     return p
 
 
-def _worker(rank, ws, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=ws)
-    from splatt3r_amd.pairs import GAUSS_FLOATS, gather_map
-    n = 5 + 3 * rank                       # unequal shards
-    recs = torch.full((n, GAUSS_FLOATS), float(rank)) + torch.arange(n)[:, None] * 0.01
-    out = gather_map(recs, ws)
-    q.put((rank, out.numpy()))
-    dist.destroy_process_group()
-
-
-def test_gather_map_world_size_2_gloo():
-    ws, port = 2, _free_port()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, q)) for r in range(ws)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=120) for _ in range(ws))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    want = np.concatenate([np.full((5 + 3 * r, 13), float(r)) + np.arange(5 + 3 * r)[:, None] * 0.01
-                           for r in range(ws)]).astype(np.float32)
-    for r in range(ws):
-        np.testing.assert_array_equal(res[r], want)
-
-
 def fake_match(feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
     """Deterministic stand-in for splatt3r_match_symmetric (no network on the
     CPU): the 8-tuple's shapes and dtypes, values derived from the keyframe
@@ -322,16 +294,28 @@ def test_sharded_pairs_two_ranks_on_gpu_match_local_decode():
     assert n0 == n1 and sum0 == sum1
 
 
+FAKE_CAP = 10
+
+
 def fake_map(pairs, poses, params):
     """Deterministic stand-in for PairShard._map_records (no network on the
-    CPU): a variable number of records per edge, valued from the edge, the
+    CPU): a variable number of records per edge (3..9 of FAKE_CAP rows, the
+    rest garbage that must never reach the map), valued from the edge, the
     keyframe pose and the filter parameters."""
-    out = []
-    for i, j in pairs:
+    buf = torch.full((len(pairs), FAKE_CAP, 13), -7.0)
+    cnt = torch.zeros(len(pairs), dtype=torch.int64)
+    for p, (i, j) in enumerate(pairs):
         n = 3 + (5 * i + j) % 7
         base = poses[i].sum() + float(params[1]) + 10 * i + j
-        out.append(base + torch.arange(n * 13, dtype=torch.float32).reshape(n, 13) * 0.5)
-    return out
+        buf[p, :n] = base + torch.arange(n * 13, dtype=torch.float32).reshape(n, 13) * 0.5
+        cnt[p] = n
+    return buf, cnt
+
+
+def fake_records(pairs, poses, params):
+    """fake_map's records, compacted (the single-rank expectation)."""
+    buf, cnt = fake_map(pairs, poses, params)
+    return [buf[p, :int(cnt[p])] for p in range(len(pairs))]
 
 
 MAP_EDGES = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (0, 2), (1, 3)]
@@ -341,7 +325,8 @@ def _map_worker(rank, ws, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     from splatt3r_amd.pairs import PairShard
-    sh = PairShard(None, "cpu", match_fn=fake_match, map_fn=fake_map)
+    sh = PairShard(None, "cpu", match_fn=fake_match, map_fn=fake_map,
+                   map_cap=lambda pairs, hp: FAKE_CAP)
     poses = torch.arange(6 * 8, dtype=torch.float32).reshape(6, 8) * 0.1
     if rank == 0:
         for k, f in enumerate(_kf_frames(6)):
@@ -359,8 +344,9 @@ def _map_worker(rank, ws, port, q):
 @pytest.mark.parametrize("ws", [2, 3])
 def test_sharded_map_refresh_matches_single_rank_gloo(ws):
     """refresh_map over ws gloo ranks: edge e re-inferred on rank e mod ws,
-    variable-length record sets all-gathered -- every rank holds exactly the
-    single-rank records, in edge order."""
+    variable-length record sets padded to a fixed capacity and all-gathered
+    with their counts -- every rank holds exactly the single-rank records,
+    in edge order, and no padding row leaks."""
     from splatt3r_amd.pairs import PairShard
     port = _free_port()
     ctx = mp.get_context("spawn")
@@ -372,10 +358,14 @@ def test_sharded_map_refresh_matches_single_rank_gloo(ws):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    sh = PairShard(None, "cpu", map_fn=fake_map)
+    sh = PairShard(None, "cpu", map_fn=fake_map, map_cap=lambda pairs, hp: FAKE_CAP)
     poses = torch.arange(6 * 8, dtype=torch.float32).reshape(6, 8) * 0.1
-    want = sh.refresh_map([e[0] for e in MAP_EDGES], [e[1] for e in MAP_EDGES], poses,
-                          spatial_stride=4, depth_max_percentile=0.9)
+    single = sh.refresh_map([e[0] for e in MAP_EDGES], [e[1] for e in MAP_EDGES], poses,
+                            spatial_stride=4, depth_max_percentile=0.9)
+    want = fake_records(MAP_EDGES, poses, (4.0, 0.9, 1.0, 1.5, 0.3))
+    assert [w.shape[0] for w in want] == [int(c) for c in single.counts]
+    for got, w in zip(single, want):
+        np.testing.assert_array_equal(got.numpy(), w.numpy())
     for r in range(ws):
         assert len(res[r]) == len(MAP_EDGES)
         for got, w in zip(res[r], want):

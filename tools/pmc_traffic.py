@@ -13,6 +13,10 @@ warms them, then replays one frame's network (encoder plan + pair plan)
 `--reps` times eagerly, each replay bracketed by a GPU sleep (`spin`)
 kernel so the summary can cut the dispatch stream into frames.
 
+`run --workload raster` replays the C3 rasterizer microbench instead
+(4,194,304 splats at 960x540, forward + backward through
+GaussianRasterizer), one replay per frame marker.
+
 `summarize` applies the gfx950 corrections of
 /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE reports
 half the bytes of wide coalesced reads -> x2; WRITE_SIZE is exact for
@@ -36,6 +40,32 @@ def _family(name: str) -> str:
         return "gemm_dense" if m.group(3) == "0" else "gemm_conv"
     m = re.search(r"\b(k_\w+)", name)
     return m.group(1) if m else name[:40]
+
+
+def run_raster(reps: int) -> None:
+    import torch
+    from tools.bench_raster import prepare
+    from diff_gaussian_rasterization import GaussianRasterizer
+    sc, rs, inputs, grad = prepare(4_194_304)
+    rast = GaussianRasterizer(rs)
+    leaf = {k: v.clone().requires_grad_(True) for k, v in inputs.items()}
+
+    def step():
+        for v in leaf.values():
+            v.grad = None
+        m2 = torch.zeros_like(leaf["means3D"], requires_grad=True)
+        img, _ = rast(means3D=leaf["means3D"], means2D=m2, opacities=leaf["opacities"],
+                      shs=leaf["shs"], cov3D_precomp=leaf["cov3D_precomp"])
+        (img * grad).sum().backward()
+
+    step()
+    torch.cuda.synchronize()
+    for _ in range(reps):
+        torch.cuda._sleep(1000)
+        step()
+    torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
+    print("pmc_traffic run: done", reps, "raster forward+backward")
 
 
 def run(reps: int) -> None:
@@ -85,7 +115,7 @@ def _frames(rows, reps: int, marker: str):
     return [rows[a + 1:b] for a, b in zip(idx[:-1], idx[1:])]
 
 
-def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str):
+def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str, workload: str = "network"):
     out = {}
     for counter, d, scale in (("FETCH_SIZE", fetch_dir, 2.0), ("WRITE_SIZE", write_dir, 1.0)):
         frames = _frames(_load(d, counter), reps, marker)
@@ -103,7 +133,10 @@ def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str):
         o["bytes_per_launch"] = o["bytes_per_frame"] / max(1, o["launches_per_frame"])
     return {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                       "FETCH_SIZE x2 (gfx950 correction), KiB -> bytes",
-            "workload": "one 512x384 frame of the network (encoder + decoder + 2 heads), eager",
+            "workload": ("one 512x384 frame of the network (encoder + decoder + 2 heads), eager"
+                         if workload == "network" else
+                         "C3 rasterizer: 4,194,304 splats at 960x540, forward + backward "
+                         "(GaussianRasterizer, torch elementwise kernels included)"),
             "frames": reps, "families": dict(sorted(out.items(), key=lambda kv: -kv[1]["bytes_per_frame"]))}
 
 
@@ -112,17 +145,19 @@ def main():
     sub = ap.add_subparsers(dest="cmd", required=True)
     r = sub.add_parser("run")
     r.add_argument("--reps", type=int, default=3)
+    r.add_argument("--workload", choices=("network", "raster"), default="network")
     s = sub.add_parser("summarize")
     s.add_argument("fetch_dir")
     s.add_argument("write_dir")
     s.add_argument("--reps", type=int, default=3)
     s.add_argument("--marker", default=r"spin|sleep")
     s.add_argument("--out", default=None)
+    s.add_argument("--workload", choices=("network", "raster"), default="network")
     a = ap.parse_args()
     if a.cmd == "run":
-        run(a.reps)
+        (run_raster if a.workload == "raster" else run)(a.reps)
         return
-    res = summarize(a.fetch_dir, a.write_dir, a.reps, a.marker)
+    res = summarize(a.fetch_dir, a.write_dir, a.reps, a.marker, a.workload)
     txt = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as fh:
