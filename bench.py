@@ -82,6 +82,12 @@ def _args():
                          "default: the next frame's encoder yields to it); 0 = normal")
     ap.add_argument("--late-prefetch", action="store_true",
                     help="queue the next frame's encoder after the tracker's GN sync")
+    ap.add_argument("--enc-ahead", type=int, default=None,
+                    help="frames kept queued for encoding ahead of the current one "
+                         "(default: the next enc-batch frames once frame i+1 is not queued)")
+    ap.add_argument("--decode-ahead", action="store_true",
+                    help="decode the next frame against the same keyframe in the same "
+                         "Bp=2 pair-plan replay (used when no keyframe is added in between)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="encode each frame inside its own step (no side-stream overlap)")
     return ap.parse_args()
@@ -110,28 +116,43 @@ def _max_over_ranks(x: float, ws: int, dev) -> float:
     return float(t.item())
 
 
-def _kernel_profile(net, reps=3):
+def _frame_units(net, before, steps):
+    """[(replays per frame, plans)] of the plans the timed frames replayed:
+    the frame's network composition (with an encoder batch of kb, 1/kb of an
+    encoder replay per frame; with decode-ahead, a Bp = 2 pair replay covers
+    two frames, a Bp = 1 replay one)."""
+    out = []
+    for key, (n, plans) in net.plan_units().items():
+        d = n - before.get(key, (0, None))[0]
+        if d > 0:
+            out.append((d / steps, plans))
+    return out
+
+
+def _kernel_profile(units, reps=3):
     """Per-launch HIP-event timing of every network call (eager replay of
-    the same plans, same kernels as the graphs): {kind: [launches, flops, ms]}."""
-    torch.cuda.synchronize()
-    recs = []
-    for _ in range(reps):
-        for plan in net.plans():
-            recs += plan.run_timed()
+    the same plans, same kernels as the graphs), weighted by replays per
+    frame: {kind: [launches, flops, ms] per frame}."""
     torch.cuda.synchronize()
     agg = {}
-    for kind, flops, e0, e1, *_ in recs:
-        a = agg.setdefault(kind, [0, 0, 0.0])
-        a[0] += 1
-        a[1] += flops
-        a[2] += e0.elapsed_time(e1)
-    return {k: [v[0] // reps, v[1] / reps, v[2] / reps] for k, v in agg.items()}
+    for wgt, plans in units:
+        recs = []
+        for _ in range(reps):
+            for plan in plans:
+                recs += plan.run_timed()
+        torch.cuda.synchronize()
+        for kind, flops, e0, e1, *_ in recs:
+            a = agg.setdefault(kind, [0.0, 0.0, 0.0])
+            a[0] += wgt / reps
+            a[1] += flops * wgt / reps
+            a[2] += e0.elapsed_time(e1) * wgt / reps
+    return agg
 
 
 _KFAM = re.compile(r"k_gemm<([^>]*)>")
 
 
-def _kernel_trace(net, reps=5):
+def _kernel_trace(units, reps=5):
     """{family: [launches per frame, ms per frame]} of the network kernels:
     a torch.profiler (roctracer) kernel trace of `reps` serial replays of
     every plan's HIP graph (the graphs the frontend replays per frame), one
@@ -141,35 +162,35 @@ def _kernel_trace(net, reps=5):
     by its A-operand mode (template argument 5); split-K reduces are timed
     with the dense family (the conv launches do not split at these shapes)."""
     from torch.profiler import ProfilerActivity, profile
-    plans = list(net.plans())
-    for pl in plans:
-        pl.replay()
-    torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CUDA]) as prof:
-        for _ in range(reps):
-            for pl in plans:
-                pl.replay()
-        torch.cuda.synchronize()
     fam = {}
-    for e in prof.events():
-        if "CUDA" not in str(e.device_type):
-            continue
-        m = _KFAM.search(e.name)
-        if m:
-            k = "gemm.dense" if m.group(1).split(",")[4].strip() == "0" else "gemm.conv"
-        elif "k_splitk_reduce" in e.name:
-            k = "gemm.dense"
-        elif "k_attn" in e.name:
-            k = "s3n_attention"
-        elif "k_layernorm" in e.name:
-            k = "s3n_layernorm"
-        else:
-            continue
-        f = fam.setdefault(k, [0, 0.0])
-        if "k_splitk_reduce" not in e.name:
-            f[0] += 1
-        f[1] += e.device_time_total / 1e3
-    return {k: [c / reps, ms / reps] for k, (c, ms) in fam.items()}
+    for wgt, plans in units:
+        for pl in plans:
+            pl.replay()
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            for _ in range(reps):
+                for pl in plans:
+                    pl.replay()
+            torch.cuda.synchronize()
+        for e in prof.events():
+            if "CUDA" not in str(e.device_type):
+                continue
+            m = _KFAM.search(e.name)
+            if m:
+                k = "gemm.dense" if m.group(1).split(",")[4].strip() == "0" else "gemm.conv"
+            elif "k_splitk_reduce" in e.name:
+                k = "gemm.dense"
+            elif "k_attn" in e.name:
+                k = "s3n_attention"
+            elif "k_layernorm" in e.name:
+                k = "s3n_layernorm"
+            else:
+                continue
+            f = fam.setdefault(k, [0.0, 0.0])
+            if "k_splitk_reduce" not in e.name:
+                f[0] += wgt / reps
+            f[1] += e.device_time_total / 1e3 * wgt / reps
+    return fam
 
 
 def _pmc_traffic(kind: str):
@@ -390,16 +411,20 @@ def main():
     kb = a.enc_batch
     if a.steps % kb:
         raise SystemExit(f"--steps {a.steps} must be a multiple of --enc-batch {kb}")
-    frames = tum_like_sequence(nfr + kb, H, W, seed=rank, step_px=2.0, device=dev)
+    look = kb + max(a.enc_ahead or 1, 1)       # lookahead images handed to each step
+    frames = tum_like_sequence(nfr + look, H, W, seed=rank, step_px=2.0, device=dev)
     fe = Frontend(model, device=dev, spatial_stride=4, render=True, enc_batch=kb,
-                  main_priority=a.main_priority, late_prefetch=a.late_prefetch)
-    nxt = (lambda i: None) if a.no_pipeline else (lambda i: [frames[j] for j in range(i + 1, i + 1 + kb)])
+                  main_priority=a.main_priority, late_prefetch=a.late_prefetch,
+                  decode_ahead=a.decode_ahead, enc_ahead=a.enc_ahead)
+    nxt = (lambda i: None) if a.no_pipeline else (lambda i: [frames[j] for j in range(i + 1, i + 1 + look)])
 
     for i in range(a.warmup + 1):          # frame 0 = INIT, then W tracked frames
         fe.step(i, frames[i], next_img=nxt(i))
     torch.cuda.synchronize()
     s0 = dict(fe.stats)
     model.encoder.events = []
+    ahead0 = dict(model.encoder.ahead_counts)
+    units0 = model.encoder.plan_units()
     _barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -428,7 +453,8 @@ def main():
                                "render on, spatial stride 4", "model": "Splatt3R (MASt3RGaussians)",
                    "global_batch": ws, "seq_len": 768,
                    "parallelism": f"replicas x{ws} (tracker path does not shard)",
-                   "encoder_batch": kb},
+                   "encoder_batch": kb, "encoder_ahead": a.enc_ahead,
+                   "decode_ahead": a.decode_ahead},
         "msplats_per_s": P_frame * st["rendered"] * ws / t_max / 1e6,
         "frame_breakdown": {"network_ms": net_ms,
                             "rest_ms": t_max / a.steps * 1e3 - net_ms,
@@ -436,6 +462,8 @@ def main():
                             "keyframes": st["keyframes"],
                             "keyframe_rate": st["keyframes"] / max(1, a.steps),
                             "reloc": st["reloc"],
+                            "decode_ahead": {k: model.encoder.ahead_counts[k] - ahead0[k]
+                                             for k in ahead0},
                             "rendered": st["rendered"], "tracked": st["tracked"],
                             # a lost frame (RELOC) in this frontend-only loop would
                             # turn later frames into untracked mono inferences
@@ -447,8 +475,9 @@ def main():
     if rank == 0 and not a.no_kprof:
         # after the timed region: kernel durations of the plans' graph
         # replays (roctracer trace) and a per-launch eager profile
-        trace = _kernel_trace(model.encoder)
-        prof = _kernel_profile(model.encoder)
+        units = _frame_units(model.encoder, units0, a.steps)
+        trace = _kernel_trace(units)
+        prof = _kernel_profile(units)
         flops_frame = sum(v[1] for v in prof.values())
         net_tflops = sum(v[1] for v in prof.values()) / (sum(v[2] for v in prof.values()) * 1e-3) / 1e12
         dom = max((k for k in prof if prof[k][1] > 0), key=lambda k: prof[k][2])

@@ -29,6 +29,7 @@ MI355X-first execution:
 """
 from __future__ import annotations
 
+import functools
 import math
 import threading
 
@@ -182,11 +183,16 @@ class EncoderPlan:
 
     def __init__(self, net: "Splatt3RNet", B: int, H: int, W: int):
         cfg, w, dev = net.cfg, net.w, net.device
+        # batch-invariant: image b of a B-image replay equals a one-image
+        # replay bit for bit (ops.gemm batch=B), so the encoder lookahead
+        # batch never changes a frame's features
+        gemm = functools.partial(ops.gemm, batch=B)
         E, p = cfg.enc_dim, cfg.patch
         ht, wt = H // p, W // p
         N = ht * wt
         M = B * N
         self.B, self.H, self.W, self.N = B, H, W, N
+        self.calls = 0
         self.img = torch.zeros(B, 3, H, W, device=dev, dtype=F32)
         self.pos = positions(B, ht, wt, dev)
         a_pe = torch.empty(M, 3 * p * p, device=dev, dtype=F16)
@@ -201,29 +207,30 @@ class EncoderPlan:
         self._bufs = (a_pe, x, h, qkv, ao, u)
         P = ops.Plan()
         P.add(ops.patch_im2col(self.img, a_pe, B=B, H=H, W=W, p=p))
-        P.add(ops.gemm([a_pe], [w.pe_w], [x], M, E, 3 * p * p, lda=3 * p * p, bias=[w.pe_b]))
+        P.add(gemm([a_pe], [w.pe_w], [x], M, E, 3 * p * p, lda=3 * p * p, bias=[w.pe_b]))
         H_ = cfg.enc_heads
         for blk in w.enc:
             P.add(ops.layernorm([x], [blk["n1w"]], [blk["n1b"]], rows=M, C=E, ldx=E, eps=cfg.ln_eps,
                                 out16=[h], ld16=E))
             # q, k rotated in the GEMM epilogue (RoPE2D on columns [0, 2E))
-            P.add(ops.gemm([h], [blk["qkv_w"]], [qkv], M, 3 * E, E, lda=E, bias=[blk["qkv_b"]],
+            P.add(gemm([h], [blk["qkv_w"]], [qkv], M, 3 * E, E, lda=E, bias=[blk["qkv_b"]],
                            rope=net.rope, rope_pos=[self.pos], rope_ncols=2 * E))
             P.add(ops.attention([qkv], [qkv[:, E:]], [qkv[:, 2 * E:]], [ao], B=B, Nq=N, Nk=N, H=H_,
                                 q_stride=3 * E, k_stride=3 * E, v_stride=3 * E, o_stride=E,
                                 scale=(E // H_) ** -0.5))
-            P.add(ops.gemm([ao], [blk["proj_w"]], [x], M, E, E, lda=E, bias=[blk["proj_b"]],
+            P.add(gemm([ao], [blk["proj_w"]], [x], M, E, E, lda=E, bias=[blk["proj_b"]],
                            R1=[x], ldr1=E))
             P.add(ops.layernorm([x], [blk["n2w"]], [blk["n2b"]], rows=M, C=E, ldx=E, eps=cfg.ln_eps,
                                 out16=[h], ld16=E))
-            P.add(ops.gemm([h], [blk["fc1_w"]], [u], M, hid, E, lda=E, bias=[blk["fc1_b"]], act="gelu"))
-            P.add(ops.gemm([u], [blk["fc2_w"]], [x], M, E, hid, lda=hid, bias=[blk["fc2_b"]],
+            P.add(gemm([h], [blk["fc1_w"]], [u], M, hid, E, lda=E, bias=[blk["fc1_b"]], act="gelu"))
+            P.add(gemm([u], [blk["fc2_w"]], [x], M, E, hid, lda=hid, bias=[blk["fc2_b"]],
                            R1=[x], ldr1=E))
         P.add(ops.layernorm([x], [w.enc_nw], [w.enc_nb], rows=M, C=E, ldx=E, eps=cfg.ln_eps,
                             out16=[self.feat16], ld16=E, out32=[self.feat.view(M, E)], ld32=E))
         self.plan = P
 
     def __call__(self, img: torch.Tensor):
+        self.calls += 1
         self.img.copy_(img)
         self.plan.replay()
         return self.feat, self.pos
@@ -242,14 +249,21 @@ class PairPlan:
     KEYS = {"pts3d": 3, "conf": 0, "desc": 24, "desc_conf": 0, "scales": 3, "rotations": 4,
             "sh": 3, "opacities": 1, "means": 3}
 
-    def __init__(self, net: "Splatt3RNet", Bp: int, H: int, W: int, keep_tokens=False):
+    def __init__(self, net: "Splatt3RNet", Bp: int, H: int, W: int, keep_tokens=False,
+                 batch_invariant=False):
         cfg, w, dev = net.cfg, net.w, net.device
+        # batch_invariant: every GEMM tuned within the reduction class of the
+        # Bp = 1 shape's choice (ops.reduction_class), so each pair's outputs
+        # equal a Bp = 1 replay bit for bit (the tracker's decode-ahead)
+        self.batch_invariant = batch_invariant
+        self._gemm = functools.partial(ops.gemm, batch=Bp if batch_invariant else 1)
         E, D, p = cfg.enc_dim, cfg.dec_dim, cfg.patch
         ht, wt = H // p, W // p
         N = ht * wt
         M = Bp * N
         ED = E + D
         self.Bp, self.H, self.W, self.N = Bp, H, W, N
+        self.runs = 0
         self.cat = torch.zeros(2, M, ED, device=dev, dtype=F16)  # [enc16 | dec_norm16]
         self.pos = torch.zeros(2, Bp, N, 2, device=dev, dtype=torch.int64)
         X = torch.empty(2, M, D, device=dev, dtype=F32)
@@ -273,7 +287,7 @@ class PairPlan:
         sc = (D // Hd) ** -0.5
         pos = [self.pos[0], self.pos[1]]
         # decoder_embed (both branches, shared weights)
-        P.add(ops.gemm(g2(self.cat), [w.emb_w, w.emb_w], g2(X), M, D, E, lda=ED,
+        P.add(self._gemm(g2(self.cat), [w.emb_w, w.emb_w], g2(X), M, D, E, lda=ED,
                        bias=[w.emb_b, w.emb_b]))
         for li, blk in enumerate(w.dec):
             # y_ = norm_y(other branch's previous output), before X changes, and
@@ -281,34 +295,34 @@ class PairPlan:
             P.add(ops.layernorm([X[1], X[0], X[0], X[1]],
                                 g2(blk["nyw"]) + g2(blk["n1w"]), g2(blk["nyb"]) + g2(blk["n1b"]),
                                 rows=M, C=D, ldx=D, eps=cfg.ln_eps, out16=g2(yh) + g2(h), ld16=D))
-            P.add(ops.gemm(g2(h), g2(blk["qkv_w"]), g2(qkv), M, 3 * D, D, lda=D, bias=g2(blk["qkv_b"]),
+            P.add(self._gemm(g2(h), g2(blk["qkv_w"]), g2(qkv), M, 3 * D, D, lda=D, bias=g2(blk["qkv_b"]),
                            rope=net.rope, rope_pos=pos, rope_ncols=2 * D))
             P.add(ops.attention(g2(qkv), [qkv[0][:, D:], qkv[1][:, D:]],
                                 [qkv[0][:, 2 * D:], qkv[1][:, 2 * D:]], g2(ao), B=Bp, Nq=N, Nk=N, H=Hd,
                                 q_stride=3 * D, k_stride=3 * D, v_stride=3 * D, o_stride=D,
                                 scale=sc))
-            P.add(ops.gemm(g2(ao), g2(blk["proj_w"]), g2(X), M, D, D, lda=D, bias=g2(blk["proj_b"]),
+            P.add(self._gemm(g2(ao), g2(blk["proj_w"]), g2(X), M, D, D, lda=D, bias=g2(blk["proj_b"]),
                            R1=g2(X), ldr1=D))
             # cross attention: q from norm2(x), k/v from norm_y(y)
             P.add(ops.layernorm(g2(X), g2(blk["n2w"]), g2(blk["n2b"]), rows=M, C=D, ldx=D,
                                 eps=cfg.ln_eps, out16=g2(h), ld16=D))
-            P.add(ops.gemm(g2(h), g2(blk["q_w"]), g2(q), M, D, D, lda=D, bias=g2(blk["q_b"]),
+            P.add(self._gemm(g2(h), g2(blk["q_w"]), g2(q), M, D, D, lda=D, bias=g2(blk["q_b"]),
                            rope=net.rope, rope_pos=pos, rope_ncols=D))
             # keys come from the other branch: its positions
-            P.add(ops.gemm(g2(yh), g2(blk["kv_w"]), g2(kv), M, 2 * D, D, lda=D, bias=g2(blk["kv_b"]),
+            P.add(self._gemm(g2(yh), g2(blk["kv_w"]), g2(kv), M, 2 * D, D, lda=D, bias=g2(blk["kv_b"]),
                            rope=net.rope, rope_pos=[pos[1], pos[0]], rope_ncols=D))
             P.add(ops.attention(g2(q), g2(kv), [kv[0][:, D:], kv[1][:, D:]], g2(ao), B=Bp, Nq=N, Nk=N,
                                 H=Hd, q_stride=D, k_stride=2 * D, v_stride=2 * D, o_stride=D,
                                 scale=sc))
-            P.add(ops.gemm(g2(ao), g2(blk["cp_w"]), g2(X), M, D, D, lda=D, bias=g2(blk["cp_b"]),
+            P.add(self._gemm(g2(ao), g2(blk["cp_w"]), g2(X), M, D, D, lda=D, bias=g2(blk["cp_b"]),
                            R1=g2(X), ldr1=D))
             # MLP (+ fp16 copy of the block output when it is a DPT hook)
             P.add(ops.layernorm(g2(X), g2(blk["n3w"]), g2(blk["n3b"]), rows=M, C=D, ldx=D,
                                 eps=cfg.ln_eps, out16=g2(h), ld16=D))
-            P.add(ops.gemm(g2(h), g2(blk["fc1_w"]), g2(u), M, hid, D, lda=D, bias=g2(blk["fc1_b"]),
+            P.add(self._gemm(g2(h), g2(blk["fc1_w"]), g2(u), M, hid, D, lda=D, bias=g2(blk["fc1_b"]),
                            act="gelu"))
             hk = self.hook16.get(li + 1)
-            P.add(ops.gemm(g2(u), g2(blk["fc2_w"]), g2(X), M, D, hid, lda=hid, bias=g2(blk["fc2_b"]),
+            P.add(self._gemm(g2(u), g2(blk["fc2_w"]), g2(X), M, D, hid, lda=hid, bias=g2(blk["fc2_b"]),
                            R1=g2(X), ldr1=D, C2=g2(hk) if hk is not None else None, ldc2=D))
             if self.tokens is not None and li + 1 < cfg.dec_depth:
                 tk = self.tokens[li + 1]
@@ -336,9 +350,9 @@ class PairPlan:
         nloc = w.mlp_fc2_w.shape[1]
         um = torch.empty(2, M, hidm, device=dev, dtype=F16)
         self.feat25 = torch.empty(2, Bp, H, W, nloc // (p * p), device=dev, dtype=F32)
-        P.add(ops.gemm(_g(self.cat, 2), _g(w.mlp_fc1_w, 2), _g(um, 2), M, hidm, ED, lda=ED,
+        P.add(self._gemm(_g(self.cat, 2), _g(w.mlp_fc1_w, 2), _g(um, 2), M, hidm, ED, lda=ED,
                        bias=_g(w.mlp_fc1_b, 2), act="gelu"))
-        P.add(ops.gemm(_g(um, 2), _g(w.mlp_fc2_w, 2), _g(self.feat25, 2), M, nloc, hidm, lda=hidm,
+        P.add(self._gemm(_g(um, 2), _g(w.mlp_fc2_w, 2), _g(self.feat25, 2), M, nloc, hidm, lda=hidm,
                        bias=_g(w.mlp_fc2_b, 2),
                        store=("convt", ht, wt, p, nloc // (p * p))))   # rows pre-permuted
         # ---- DPTs: 4 groups (h1 pts, h1 gauss, h2 pts, h2 gauss)
@@ -352,19 +366,19 @@ class PairPlan:
         e = lambda *s, dt=F16: torch.empty(*s, device=dev, dtype=dt)
         # act_postprocess
         t0 = e(4, M, ld[0]); l0 = e(4, Bp, 4 * ht, 4 * wt, ld[0])
-        P.add(ops.gemm(L0, g4(w.ap0a_w), g4(t0), M, ld[0], E, lda=ED, bias=g4(w.ap0a_b)))
-        P.add(ops.gemm(g4(t0), g4(w.ap0b_w), g4(l0), M, 16 * ld[0], ld[0], lda=ld[0],
+        P.add(self._gemm(L0, g4(w.ap0a_w), g4(t0), M, ld[0], E, lda=ED, bias=g4(w.ap0a_b)))
+        P.add(self._gemm(g4(t0), g4(w.ap0b_w), g4(l0), M, 16 * ld[0], ld[0], lda=ld[0],
                        bias=g4(w.ap0b_b), store=("convt", ht, wt, 4, ld[0])))
         t1 = e(4, M, ld[1]); l1 = e(4, Bp, 2 * ht, 2 * wt, ld[1])
-        P.add(ops.gemm(L1, g4(w.ap1a_w), g4(t1), M, ld[1], D, lda=D, bias=g4(w.ap1a_b)))
-        P.add(ops.gemm(g4(t1), g4(w.ap1b_w), g4(l1), M, 4 * ld[1], ld[1], lda=ld[1],
+        P.add(self._gemm(L1, g4(w.ap1a_w), g4(t1), M, ld[1], D, lda=D, bias=g4(w.ap1a_b)))
+        P.add(self._gemm(g4(t1), g4(w.ap1b_w), g4(l1), M, 4 * ld[1], ld[1], lda=ld[1],
                        bias=g4(w.ap1b_b), store=("convt", ht, wt, 2, ld[1])))
         l2 = e(4, Bp, ht, wt, ld[2])
-        P.add(ops.gemm(L2, g4(w.ap2_w), g4(l2), M, ld[2], D, lda=D, bias=g4(w.ap2_b)))
+        P.add(self._gemm(L2, g4(w.ap2_w), g4(l2), M, ld[2], D, lda=D, bias=g4(w.ap2_b)))
         t3 = e(4, M, ld[3])
         h3, w3 = (ht + 1) // 2, (wt + 1) // 2
         l3 = e(4, Bp, h3, w3, ld[3])
-        P.add(ops.gemm(L3, g4(w.ap3a_w), g4(t3), M, ld[3], D, lda=ED, bias=g4(w.ap3a_b)))
+        P.add(self._gemm(L3, g4(w.ap3a_w), g4(t3), M, ld[3], D, lda=ED, bias=g4(w.ap3a_b)))
         P.add(self._conv(g4(t3), w.ap3b_w, g4(l3), Bp, ht, wt, ld[3], ld[3], 3, 2, 1,
                          bias=g4(w.ap3b_b)))
         # layer_rn: 3x3, no bias -> 256
@@ -400,7 +414,7 @@ class PairPlan:
                              bias=g4(blk["u2c2_b"]), R1=g4(x)))
             # out_conv 1x1 at low resolution, then x2 bilinear (align_corners)
             oc = e(4, Bp, hh, ww, Fd)
-            P.add(ops.gemm(g4(s), g4(blk["out_w"]), g4(oc), Bp * hh * ww, Fd, Fd, lda=Fd,
+            P.add(self._gemm(g4(s), g4(blk["out_w"]), g4(oc), Bp * hh * ww, Fd, Fd, lda=Fd,
                            bias=g4(blk["out_b"])))
             if stage > 0:
                 oh, ow = sizes[stage - 1]  # refinenet4 output is cropped to layer 3's grid
@@ -432,17 +446,58 @@ class PairPlan:
         # head's Gaussian parameters in one block, so the host-side copies
         # the reference semantics need (torch.stack of the two heads, the
         # gaussian_pred clones) are one copy per block (splatt3r_utils).
+        # Batch-invariant (tracker) plans with Bp > 1 keep that layout per
+        # pair ([pair][matching block | head-1 Gaussians | head-2 Gaussians]),
+        # so the copies of one pair's outputs (decode-ahead slots) are one
+        # copy per block too; the result tensors are then strided over Bp.
         mkeys = ("pts3d", "conf", "desc", "desc_conf")
         gkeys = ("means", "scales", "rotations", "sh", "opacities")
         width = lambda k: max(1, self.KEYS[k])
-        blk_m = torch.empty(2 * n * sum(width(k) for k in mkeys), device=dev, dtype=F32)
-        views, off = {}, 0
-        for k in mkeys:
-            sz = 2 * n * width(k)
-            views[k] = blk_m[off:off + sz].view(2, n * width(k))
-            off += sz
+        hw = H * W
+        per_pair = self.batch_invariant and Bp > 1
+        if per_pair:
+            offs, off = {}, 0
+            for k in mkeys:
+                for hd in range(2):
+                    offs[(hd, k)] = off
+                    off += hw * width(k)
+            for hd in range(2):
+                for k in gkeys:
+                    offs[(hd, k)] = off
+                    off += hw * width(k)
+            pstride = off
+            blk = torch.empty(Bp * pstride, device=dev, dtype=F32)
+
+            def tensor(hd, k):
+                c = self.KEYS[k]
+                cc = max(1, c)
+                shape, stride = (Bp, H, W), (pstride, W * cc, cc)
+                if c:
+                    shape, stride = shape + (c,), stride + (1,)
+                return blk.as_strided(shape, stride, offs[(hd, k)])
+        else:
+            blk_m = torch.empty(2 * n * sum(width(k) for k in mkeys), device=dev, dtype=F32)
+            views, off = {}, 0
+            for k in mkeys:
+                sz = 2 * n * width(k)
+                views[k] = blk_m[off:off + sz].view(2, n * width(k))
+                off += sz
         for hd in range(2):
             out = {}
+            if per_pair:
+                for k in mkeys + gkeys:
+                    out[k] = tensor(hd, k)
+                sh = out["sh"]
+                out["sh"] = sh.as_strided((Bp, H, W, 3, 1), sh.stride() + (1,), sh.storage_offset())
+                # one postprocess launch per pair (its outputs are not one
+                # contiguous range over the Bp pairs)
+                for b in range(Bp):
+                    P.add(ops.gaussian_postprocess(
+                        hw, self.dpt_out[2 * hd][b * hw:], w.NOUT, self.feat25[hd][b],
+                        self.dpt_out[2 * hd + 1][b * hw:], w.NOUT, cfg.use_offsets,
+                        {k: v[b] for k, v in out.items()}, desc16=self.desc16[hd][b]))
+                self.res.append(out)
+                continue
             for k in mkeys:
                 c = self.KEYS[k]
                 out[k] = views[k][hd].view((Bp, H, W) if c == 0 else (Bp, H, W, c))
@@ -465,17 +520,17 @@ class PairPlan:
         self.stages.update(self._ref_outs)
         return P
 
-    @staticmethod
-    def _conv(A, Wt, C, Bp, H, W, Cin, Cout, k, stride, pad, bias=None, relu_in=False, act="none",
-              R1=None, R2=None, tail=None):
+    def _conv(self, A, Wt, C, Bp, H, W, Cin, Cout, k, stride, pad, bias=None, relu_in=False,
+              act="none", R1=None, R2=None, tail=None):
         oh = (H + 2 * pad - k) // stride + 1
         ow = (W + 2 * pad - k) // stride + 1
         M = Bp * oh * ow
         conv = dict(H=H, W=W, C=Cin, k=k, stride=stride, pad=pad, oH=oh, oW=ow, relu_in=relu_in)
-        return ops.gemm(A, _g(Wt, len(A)), C, M, Cout, k * k * Cin, lda=0, bias=bias, act=act,
+        return self._gemm(A, _g(Wt, len(A)), C, M, Cout, k * k * Cin, lda=0, bias=bias, act=act,
                         R1=R1, ldr1=Cout, R2=R2, ldr2=Cout, conv=conv, tail=tail)
 
     def run(self):
+        self.runs += 1      # lets a holder of output views detect a later replay
         self.decoder_plan.replay()
         self.head_plan.replay()
 
@@ -511,6 +566,10 @@ class Splatt3RNet:
         # bench.py sets a list here to collect (tag, start, end) HIP events
         # around every encoder / pair-plan replay on the launch stream
         self.events = None
+        # decode-ahead bookkeeping (splatt3r_utils._decode_ahead): Bp = 2
+        # replays issued, next-frame slots used, slots dropped (new keyframe),
+        # pairings declined by the frontend's predictor
+        self.ahead_counts = {"paired": 0, "used": 0, "dropped": 0, "declined": 0}
 
     def _timed(self, tag, fn, *a):
         if self.events is None:
@@ -522,6 +581,17 @@ class Splatt3RNet:
         e1.record()
         self.events.append((tag, e0, e1))
         return out
+
+    def plan_units(self):
+        """{key: (replays so far, [plans of one replay])} of every built
+        encoder / pair plan: the frame composition of a run is the replay
+        count deltas (bench.py weights per-replay kernel times by them)."""
+        u = {}
+        for k, ep in self._enc.items():
+            u[("encoder",) + k] = (ep.calls, [ep.plan])
+        for k, pp in self._pair.items():
+            u[("pair",) + k] = (pp.runs, [pp.decoder_plan, pp.head_plan])
+        return u
 
     def plans(self):
         """Every built plan (for per-kernel profiling)."""
@@ -547,11 +617,13 @@ class Splatt3RNet:
 
     def pair_plan(self, Bp, H, W, keep_tokens=False, tag=None) -> PairPlan:
         """`tag` separates plan buffers of concurrent users of one network
-        (the frontend tracker and the backend worker thread)."""
+        (the frontend tracker and the backend worker thread).  The untagged
+        (tracker) plans are batch-invariant: pair b of a Bp > 1 replay equals
+        a Bp = 1 replay of that pair bit for bit."""
         key = (Bp, H, W, keep_tokens, tag)
         if key not in self._pair:
             with torch.inference_mode(False):
-                pp = PairPlan(self, Bp, H, W, keep_tokens)
+                pp = PairPlan(self, Bp, H, W, keep_tokens, batch_invariant=tag is None)
             if self._capture_here() and not keep_tokens:
                 pp.decoder_plan.capture()
                 pp.head_plan.capture()

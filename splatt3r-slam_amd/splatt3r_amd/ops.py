@@ -196,6 +196,33 @@ _TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14}   # the fused tail runs with
 _EXCLUDED = set(range(21, 32)) if os.environ.get("S3_GEMM_MF16", "1") == "0" else set()
 
 
+# Reduction structure of each tile (net_gemm_t*.hip launch<BM, BN, S, NWM,
+# NWN, BK, KG, MF> arguments): K tile, in-workgroup K-groups, MFMA shape
+# (32 = 32x32x16, 16 = 16x16x32), and whether the fp32 tile fits the LDS
+# ring (vector epilogue) or takes the per-register epilogue.
+_TILE_RED = {1: (64, 1, 32), 2: (64, 1, 32), 3: (64, 1, 32), 4: (64, 1, 32), 5: (64, 1, 32),
+             6: (64, 1, 32), 8: (64, 1, 32), 9: (128, 1, 32), 10: (128, 1, 32),
+             11: (128, 1, 32), 12: (128, 1, 32), 14: (64, 1, 32),
+             15: (64, 2, 32), 16: (64, 4, 32), 17: (64, 2, 32), 18: (64, 2, 32),
+             19: (128, 2, 32), 20: (64, 3, 32),
+             **{t: (64, 1, 16) for t in range(21, 31)}, 31: (128, 1, 16)}
+_REGS_EPILOGUE = {14}
+
+
+def reduction_class(K: int, tile: int, split_k: int):
+    """What fixes the summation order of every output element of a launch:
+    the MFMA shape, the K-group interleave (K-groups take every KG-th K
+    tile), the split-K boundaries (k_splitk_reduce adds the planes in split
+    order) and the epilogue form.  Two launches of one class compute
+    bit-identical elements whatever their M or tile footprint (BM, BN only
+    decide which workgroup computes an element)."""
+    bk, kg, mf = _TILE_RED[tile]
+    kt = -(-K // bk)
+    per = -(-kt // max(1, split_k))
+    bound = per * bk if -(-kt // per) > 1 else 0
+    return (mf, kg, bk if kg > 1 else 0, bound, tile in _REGS_EPILOGUE)
+
+
 def _tune_key(a):
     f = ("M", "N", "K", "groups", "lda", "ldb", "ldc", "act", "r1_f16", "r2_f16", "c_f16",
          "ldr1", "ldr2", "ldc2", "store_mode", "sS", "sCout", "a_mode", "cH", "cW", "cC", "ksize",
@@ -204,7 +231,7 @@ def _tune_key(a):
                                                bool(a.bias[0]), bool(a.C[0]))
 
 
-def _tune_candidates(a, split_ok):
+def _tune_candidates(a, split_ok, like=None):
     kt = -(-a.K // 64)
     out = []
     for tile, (bm, bn) in _TILE_SHAPES.items():
@@ -214,14 +241,20 @@ def _tune_candidates(a, split_ok):
             continue
         tiles = a.groups * -(-a.M // bm) * -(-a.N // bn)
         for sk in (1, 2, 3, 4, 6, 8):
-            if sk > 1 and (not split_ok or kt // sk < 4 or tiles * sk > 4096):
+            if like is not None:
+                # batch-invariant plan: only launches whose elements equal
+                # those of the one-item plan's choice (like = (tile, split))
+                if ((tile, sk) != like and (sk > 1 and not split_ok or
+                        reduction_class(a.K, tile, sk) != reduction_class(a.K, *like))):
+                    continue
+            elif sk > 1 and (not split_ok or kt // sk < 4 or tiles * sk > 4096):
                 continue
             out.append((tile, sk))
     return out
 
 
-def _tuned(a, A, B, bias, rope, rope_pos, split_ok):
-    key = _tune_key(a)
+def _tuned(a, A, B, bias, rope, rope_pos, split_ok, like=None):
+    key = _tune_key(a) + (like,)
     if key in _TUNE_CACHE:
         return _TUNE_CACHE[key]
     dev = next(t.device for t in (*A, *B) if isinstance(t, torch.Tensor))
@@ -273,7 +306,7 @@ def _tuned(a, A, B, bias, rope, rope_pos, split_ok):
     st = _lib.stream(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     best, best_ms = (a.tile, a.split_k), None
-    for tile, sk in _tune_candidates(a, split_ok):
+    for tile, sk in _tune_candidates(a, split_ok, like):
         t.tile, t.split_k = tile, sk
         ws = None
         if sk > 1:
@@ -315,13 +348,16 @@ def _tuned(a, A, B, bias, rope, rope_pos, split_ok):
 
 def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1=None,
          ldr1=0, R2=None, ldr2=0, C2=None, ldc2=0, conv=None, store=None, split_k=None,
-         tile=0, rope=None, rope_pos=None, rope_ncols=0, tail=None) -> Call:
+         tile=0, rope=None, rope_pos=None, rope_ncols=0, tail=None, batch=1) -> Call:
     """Grouped GEMM: A, B, C, bias, R1, R2, C2 are lists (one entry per group)
     of tensors / raw pointers.  conv = dict(H, W, C, k, stride, pad, oH, oW,
     relu_in) switches A to implicit im2col of an NHWC image.  store =
     ("convt"|"pixshuf", sH, sW, s, Cout).  tail = (W [tail_n, N] fp16, bias fp32,
     out fp32 [M, ld], tail_n, ld) lists per group: the fused 1x1 tail (s3n.h);
-    C entries may then be None."""
+    C entries may then be None.  batch = b > 1: the M rows are b items of
+    M / b rows (a pair plan's Bp pairs); the launch is tuned among the
+    configurations of the same reduction_class as the one-item shape's
+    choice, so every item's rows equal the one-item launch bit for bit."""
     a = GemmArgs()
     groups = len(A)
     a.M, a.N, a.K, a.groups = int(M), int(N), int(K), groups
@@ -373,8 +409,13 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
     a.split_k = int(auto_split_k(M, N, K, groups) if split_k is None else split_k)
     a.tile = int(tile) or TILE_OVERRIDE
     if TUNE and not tile and not TILE_OVERRIDE and torch.cuda.is_available():
-        a.tile, a.split_k = _tuned(a, A, B, bias, rope, rope_pos,
-                                   split_ok=split_k is None and rope_pos is None)
+        split_ok = split_k is None and rope_pos is None
+        like = None
+        if batch > 1 and a.M % batch == 0:
+            a1 = GemmArgs.from_buffer_copy(a)
+            a1.M = a.M // batch
+            like = _tuned(a1, A, B, bias, rope, rope_pos, split_ok)
+        a.tile, a.split_k = _tuned(a, A, B, bias, rope, rope_pos, split_ok, like)
     ws = None
     if a.split_k > 1:
         nbytes = _lib.lib().s3n_gemm_workspace_bytes(ctypes.byref(a))

@@ -47,7 +47,8 @@ class Frontend:
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
                  readback=True, enc_batch=1, main_priority=None, late_prefetch=False,
-                 viz=False, max_gaussians=4 * 1024 * 1024, backend=None, render_writer=None):
+                 viz=False, max_gaussians=4 * 1024 * 1024, backend=None, render_writer=None,
+                 decode_ahead=False, enc_ahead=None):
         self.model = model
         # dataio.RenderWriter: the per-frame gs_init_* / gs_track_* PNG export
         # (main.py:436-446, 490-506), written off the tracking thread
@@ -103,6 +104,18 @@ class Frontend:
         self.enc_stream = torch.cuda.Stream(device=device) if torch.cuda.is_available() else None
         self._queue = {}           # frame index -> (Frame whose encoder is queued, done event)
         self.enc_batch = enc_batch # images per encoder replay when lookahead frames are given
+        # frames kept queued ahead of the current one (None: queue the next
+        # enc_batch frames only when frame i + 1 is not queued yet)
+        self.enc_ahead = enc_ahead
+        self._next_enc = 0         # lowest frame index not queued for encoding
+        # decode-ahead (splatt3r_utils._decode_ahead): a frame whose decode
+        # is issued also decodes the next queued frame against the same
+        # keyframe in the same Bp = 2 replay; the result is used when that
+        # frame is tracked against the same keyframe
+        self.decode_ahead = decode_ahead
+        # min(match_frac_k, unique_frac_f) of the frames tracked against the
+        # current keyframe, in order: the decode-ahead pairing predictor
+        self._kf_fracs: list[float] = []
         self.spans = None          # list -> per-frame GPU events (encoder, main chain)
         # main chain on a stream of its own priority (the encoder side stream
         # keeps the default one): the dispatcher then prefers the frame's
@@ -135,6 +148,35 @@ class Frontend:
             f.feat, f.pos = feat[j:j + 1], pos[j:j + 1]
             f.img.record_stream(self.enc_stream)
             self._queue[i + j] = (f, done)
+
+    def _pair_likely_kept(self) -> bool:
+        """Whether frame i + 1's slot is likely to be used: it is dropped when
+        frame i becomes a keyframe, i.e. when frame i's min(match_frac_k,
+        unique_frac_f) falls below match_frac_thresh (tracker.py:104-110).
+        The fraction decays as the camera leaves the keyframe; frame i's is
+        predicted by linear extrapolation of the last two frames tracked
+        against the same keyframe (no history: pair).  A wrong guess costs
+        speed only, never results."""
+        fr = self._kf_fracs
+        if len(fr) < 2:
+            return True
+        return 2.0 * fr[-1] - fr[-2] >= config["tracking"]["match_frac_thresh"]
+
+    def _ahead_source(self, i):
+        """decode-ahead: the queued Frame i + 1 with its encoder ordered
+        before the current stream (called only when a decode is issued), or
+        None when the pairing predictor expects frame i to become a
+        keyframe."""
+        def ahead():
+            q = self._queue.get(i + 1)
+            if q is None:
+                return None
+            if not self._pair_likely_kept():
+                self.model.encoder.ahead_counts["declined"] += 1
+                return None
+            torch.cuda.current_stream(self.device).wait_event(q[1])
+            return q[0]
+        return ahead
 
     def _take_prefetched(self, i, T_WC):
         if i not in self._queue:
@@ -306,19 +348,29 @@ class Frontend:
             frame = self._take_prefetched(i, T_WC)
         if frame is None:
             frame = create_frame(i, img, T_WC, device=self.device)
-        if next_img is not None and self.enc_stream is not None and (i + 1) not in self._queue:
+        self._next_enc = max(self._next_enc, i + 1)
+        pending = []
+        if next_img is not None and self.enc_stream is not None:
             # next_img: the next frame's image, or a list of the next frames'
-            # images (lookahead); up to enc_batch of them are encoded together
+            # images (lookahead); up to enc_batch of them are encoded together,
+            # until frames up to i + enc_ahead are queued
             nxt = list(next_img) if isinstance(next_img, (list, tuple)) else [next_img]
-            pending = (i + 1, nxt[:max(1, self.enc_batch)])
+            kb = max(1, self.enc_batch)
+            want = i + max(1, self.enc_ahead or 1)
+            while self._next_enc <= want:
+                off = self._next_enc - (i + 1)
+                imgs = nxt[off:off + kb]
+                if not imgs:
+                    break
+                pending.append((self._next_enc, imgs))
+                self._next_enc += len(imgs)
             # late prefetch: a tracked frame queues the next encoder after
             # its GN sync, so the encoder fills the device while the host
             # issues the post-GN launches (pose update, map, render)
             if not (self.late_prefetch and self.mode == Mode.TRACKING):
-                self._prefetch(*pending)
-                pending = None
-        else:
-            pending = None
+                for b in pending:
+                    self._prefetch(*b)
+                pending = []
         if e0 is not None:
             e0[0] = self._event()
         self._stats["frames"] += 1
@@ -340,16 +392,22 @@ class Frontend:
         if self.mode == Mode.TRACKING:
             hook = self._speculate(frame, self.keyframes.last_keyframe()) if self.gmap is None \
                 else None
-            add_new_kf, _, try_reloc = self.tracker.track(frame, before_sync=hook)
+            add_new_kf, _, try_reloc = self.tracker.track(
+                frame, before_sync=hook,
+                ahead=self._ahead_source(i) if self.decode_ahead else None)
             # states.set_frame(frame) (main.py:455): the next frame starts from
             # the tracked pose, not from what the backend later writes into
             # the keyframe (the same object here, a shared-memory copy there)
             T_state = frame.T_WC
             spec = self.tracker.spec if (self.tracker.spec_valid and not try_reloc) else None
-            if pending is not None:
-                self._prefetch(*pending)
+            for b in pending:
+                self._prefetch(*b)
             self._stats["gn_iters"] += self.tracker.last_iters
             self._stats["tracked"] += 1
+            if try_reloc or add_new_kf:
+                self._kf_fracs = []
+            else:
+                self._kf_fracs.append(min(self.tracker.last_fracs[1:]))
             if try_reloc:
                 self.mode = Mode.RELOC
             if not try_reloc and should_append_gaussians(

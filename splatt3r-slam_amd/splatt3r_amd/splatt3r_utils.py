@@ -179,20 +179,73 @@ def splatt3r_inference_mono(model, frame):
     return Xii[0], Cii[0]
 
 
+def _slot(res, b):
+    """Batch element b of a pair plan's result dict, as [1, ...] views."""
+    return {k: v[b:b + 1] for k, v in res.items()}
+
+
+def _ahead_key(frame, keyframe):
+    return (frame.frame_id, keyframe.frame_id, keyframe.feat.data_ptr(),
+            tuple(frame.img.shape))
+
+
+def _decode_ahead(model, frame_i, frame_j, ahead):
+    """Decoder + heads of (frame_i, frame_j), sharing one Bp = 2 pair-plan
+    replay with the next frame (decode-ahead).
+
+    The decoder of a tracked frame depends only on its encoder features and
+    those of the last keyframe (splatt3r_utils.py:580-607), so the next
+    frame's decode against the same keyframe can be issued with this one:
+    one replay of the Bp = 2 plan (M = 1536-row GEMMs per branch) instead of
+    two Bp = 1 replays.  Slot 1 is kept (views of the plan's output buffers,
+    valid until the plan's next replay: `PairPlan.runs`) and used by the next
+    call when that frame is tracked against the same keyframe; a new
+    keyframe in between discards it.  `ahead()` returns the next Frame
+    (encoded, its encoder ordered before the current stream) or None; it is
+    only called when a decode is issued."""
+    net = model.encoder
+    cached = getattr(net, "_ahead_slot", None)
+    net._ahead_slot = None
+    if cached is not None:
+        key, pp, runs = cached
+        if key == _ahead_key(frame_i, frame_j) and pp.runs == runs:
+            net.ahead_counts["used"] += 1
+            return _slot(pp.res[0], 1), _slot(pp.res[1], 1)
+        net.ahead_counts["dropped"] += 1
+    nxt = ahead() if ahead is not None else None
+    if (nxt is None or nxt.feat is None or nxt.img.shape != frame_i.img.shape
+            or nxt.feat.shape != frame_i.feat.shape):
+        return decoder(model, frame_i.feat, frame_j.feat, frame_i.pos, frame_j.pos,
+                       frame_i.img_true_shape, frame_j.img_true_shape)
+    H, W = _hw(frame_i.img_true_shape)
+    feat1 = torch.cat((frame_i.feat, nxt.feat))
+    pos1 = torch.cat((frame_i.pos, nxt.pos))
+    r1, r2, pp = net.infer_pair(feat1, pos1, frame_j.feat.expand(2, -1, -1),
+                                frame_j.pos.expand(2, -1, -1), (H, W))
+    net._ahead_slot = (_ahead_key(nxt, frame_j), pp, pp.runs)
+    net.ahead_counts["paired"] += 1
+    return _slot(r1, 0), _slot(r2, 0)
+
+
 @torch.inference_mode()
-def splatt3r_asymmetric_inference(model, frame_i, frame_j):
-    """splatt3r_utils.py:580-607."""
+def splatt3r_asymmetric_inference(model, frame_i, frame_j, ahead=None):
+    """splatt3r_utils.py:580-607.  `ahead`: decode-ahead source of the next
+    frame (see _decode_ahead); None decodes this pair alone."""
     _ensure_encoded(model, frame_i)
     _ensure_encoded(model, frame_j)
-    res11, res21 = decoder(model, frame_i.feat, frame_j.feat, frame_i.pos, frame_j.pos,
-                           frame_i.img_true_shape, frame_j.img_true_shape)
+    if ahead is not None or getattr(model.encoder, "_ahead_slot", None) is not None:
+        res11, res21 = _decode_ahead(model, frame_i, frame_j, ahead)
+    else:
+        res11, res21 = decoder(model, frame_i.feat, frame_j.feat, frame_i.pos, frame_j.pos,
+                               frame_i.img_true_shape, frame_j.img_true_shape)
     X, C, D, Q = _stack_outputs([res11, res21])
     return X, C, D, Q, (res11, res21)
 
 
-def splatt3r_match_asymmetric(model, frame_i, frame_j, idx_i2j_init=None):
+def splatt3r_match_asymmetric(model, frame_i, frame_j, idx_i2j_init=None, ahead=None):
     """splatt3r_utils.py:610-644."""
-    X, C, D, Q, (res_self, res_cross) = splatt3r_asymmetric_inference(model, frame_i, frame_j)
+    X, C, D, Q, (res_self, res_cross) = splatt3r_asymmetric_inference(model, frame_i, frame_j,
+                                                                       ahead)
     frame_i.gaussian_pred = _extract_gaussian_params(res_self)
     frame_i.gaussian_pred_cross = _extract_gaussian_params(res_cross)
     b = X.shape[0] // 2

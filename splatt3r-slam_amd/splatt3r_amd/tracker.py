@@ -214,19 +214,21 @@ class FrameTracker:
     def reset_idx_f2k(self):
         self.idx_f2k = None
 
-    def track(self, frame, before_sync=None):
+    def track(self, frame, before_sync=None, ahead=None):
         """tracker.py:28-127; returns (new_kf, match_info, try_reloc).
 
         before_sync(T_WC): called with the device-side pose after the first
         queued GN chunk, before the host waits for it, so the caller can
         queue work that depends only on that pose (the frontend's render).
         Its result is kept in self.spec; self.spec_valid says whether that
-        pose is the final one (GN stopped inside the first chunk)."""
+        pose is the final one (GN stopped inside the first chunk).
+        ahead(): the next frame for a shared decode (splatt3r_utils
+        _decode_ahead), or None."""
         self.spec, self.spec_valid = None, False
         from splatt3r_amd.splatt3r_utils import splatt3r_match_asymmetric
         keyframe = self.keyframes.last_keyframe()
         idx_f2k, valid_match_k, Xff, Cff, Qff, Xkf, Ckf, Qkf = splatt3r_match_asymmetric(
-            self.model, frame, keyframe, idx_i2j_init=self.idx_f2k)
+            self.model, frame, keyframe, idx_i2j_init=self.idx_f2k, ahead=ahead)
         self.idx_f2k = idx_f2k.clone()
         idx_f2k = idx_f2k[0]
         valid_match_k = valid_match_k[0]
@@ -282,6 +284,7 @@ class FrameTracker:
 
         match_frac_k = n_kf / n
         unique_frac_f = n_unique / n
+        self.last_fracs = (n_opt / n, match_frac_k, unique_frac_f)
         new_kf = min(match_frac_k, unique_frac_f) < self.cfg["match_frac_thresh"]
         if new_kf:
             self.reset_idx_f2k()

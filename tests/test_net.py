@@ -217,6 +217,56 @@ def test_pair_batch_bp2_matches_bp1_and_golden(parity):
         _check(parity, f"bp2_pair0_vs_golden_{k}", R1[k][0], g["res1_" + k][0], TOL["head"])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw", [(384, 512), (48, 64)])
+def test_tracker_pair_plan_is_batch_invariant(hw):
+    """The tracker's (untagged) pair plans tune every GEMM within the
+    reduction class of the Bp = 1 shape's choice (ops.reduction_class), so
+    pair b of a Bp = 2 replay equals the Bp = 1 replay of that pair bit for
+    bit -- what the frontend's decode-ahead relies on.  Full size (C2) and
+    the small config, portable-PRNG weights, random landscape images."""
+    from splatt3r_amd import weights as W
+    from splatt3r_amd.net import Splatt3RNet
+    H, W_ = hw
+    cfg = W.FULL if H >= 384 else W.SMALL
+    net = Splatt3RNet(cfg, seed=1234)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    imgs = [torch.rand(1, 3, H, W_, device="cuda", generator=gen) * 2 - 1 for _ in range(3)]
+    enc = [net._encode_image(im, None)[:2] for im in imgs]
+    keys = ("pts3d", "conf", "desc", "desc_conf", "scales", "rotations", "sh", "opacities",
+            "means")
+    ref = []
+    for i in (0, 1):
+        (fa, pa), (fk, pk) = enc[i], enc[2]
+        r1, r2, _ = net.infer_pair(fa, pa, fk, pk, (H, W_))
+        ref.append(({k: r1[k].clone() for k in keys}, {k: r2[k].clone() for k in keys}))
+    fk, pk = enc[2]
+    R1, R2, pp = net.infer_pair(torch.cat([enc[0][0], enc[1][0]]), torch.cat([enc[0][1], enc[1][1]]),
+                                fk.expand(2, -1, -1), pk.expand(2, -1, -1), (H, W_))
+    assert pp.Bp == 2
+    for b in (0, 1):
+        for k in keys:
+            assert torch.equal(R1[k][b], ref[b][0][k][0]), (b, "res1", k)
+            assert torch.equal(R2[k][b], ref[b][1][k][0]), (b, "res2", k)
+
+
+@pytest.mark.gpu
+def test_encoder_is_batch_invariant():
+    """Image b of a B-image encoder replay equals its one-image replay bit for
+    bit (ops.gemm batch=B): the frontend's encoder lookahead batch never
+    changes a frame's features."""
+    from splatt3r_amd import weights as W
+    from splatt3r_amd.net import Splatt3RNet
+    net = Splatt3RNet(W.FULL, seed=1234)
+    gen = torch.Generator(device="cuda").manual_seed(6)
+    imgs = torch.rand(3, 3, 384, 512, device="cuda", generator=gen) * 2 - 1
+    one = [net._encode_image(imgs[b:b + 1], None)[0] for b in range(3)]
+    for B in (2, 3):
+        fb, _, _ = net._encode_image(imgs[:B], None)
+        for b in range(B):
+            assert torch.equal(fb[b:b + 1], one[b]), (B, b, float((fb[b] - one[b][0]).abs().max()))
+
+
 def _small_model(use_offsets=True):
     import dataclasses
     from splatt3r_amd import weights as W

@@ -53,6 +53,55 @@ def test_pipelined_frontend_matches_sequential():
 
 
 @pytest.mark.gpu
+def test_decode_ahead_frontend_matches_sequential():
+    """Decode-ahead (splatt3r_utils._decode_ahead): the next frame is decoded
+    against the same keyframe in the tracked frame's Bp = 2 replay and used
+    when no keyframe is added in between.  The tracker's pair plans are
+    batch-invariant, so poses, renders, keyframes and counters equal the
+    frame-by-frame frontend bit for bit; slots are both used and dropped."""
+    from splatt3r_amd.slam import Frontend
+    from splatt3r_amd.splatt3r_utils import load_splatt3r
+    from splatt3r_amd.synthetic import tum_like_sequence
+    from splatt3r_amd.weights import FULL
+
+    dev = torch.device("cuda", 0)
+    model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
+    n = 12
+    frames = tum_like_sequence(n + 6, 384, 512, seed=3, step_px=2.0, device=dev)
+
+    def run(ahead, kb=None):
+        kb = kb or (2 if ahead else 1)
+        fe = Frontend(model, device=dev, spatial_stride=4, render=True,
+                      enc_batch=kb, enc_ahead=3 if kb > 1 else None, decode_ahead=ahead)
+        poses, renders = [], []
+        c0 = dict(model.encoder.ahead_counts)
+        for i in range(n):
+            nxt = [frames[j] for j in range(i + 1, min(n, i + 6))]
+            f = fe.step(i, frames[i], next_img=nxt)
+            poses.append(f.T_WC.data.clone())
+            renders.append(fe.last_render.clone())
+        torch.cuda.synchronize()
+        counts = {k: model.encoder.ahead_counts[k] - c0[k] for k in c0}
+        return poses, renders, list(fe.new_kf_frames), dict(fe.stats), counts
+
+    p0, r0, kf0, st0, c0 = run(False)
+    for ahead, kb in ((False, 2), (True, 1)):    # the two factors alone (diagnostic)
+        pa, _, _, _, ca = run(ahead, kb)
+        print(f"ahead={ahead} kb={kb}:", [float((a - b).abs().max()) for a, b in zip(p0, pa)], ca)
+    p1, r1, kf1, st1, c1 = run(True)
+    d = [float((a - b).abs().max()) for a, b in zip(p0, p1)]
+    print("decode-ahead pose differences per frame:", d, c1)
+    assert c0 == {"paired": 0, "used": 0, "dropped": 0, "declined": 0}
+    assert c1["paired"] > 0 and c1["used"] > 0, c1
+    assert st0["tracked"] == n - 1 and st0["reloc"] == 0
+    assert kf0 == kf1 and st0 == st1
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
+    for a, b in zip(r0, r1):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
 def test_factor_graph_rays_matches_oracle():
     """global_opt.FactorGraph on real frontend keyframes: symmetric pair
     decode + matching -> two-way edges -> device GN; the solve agrees with

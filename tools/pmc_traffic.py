@@ -68,26 +68,35 @@ def run_raster(reps: int) -> None:
     print("pmc_traffic run: done", reps, "raster forward+backward")
 
 
-def run(reps: int) -> None:
+def run(reps: int, kb: int = 1, bp: int = 1) -> None:
+    """One rep = kb frames: one encoder replay of kb images and kb / bp
+    replays of the Bp = bp pair plan (the bench's frame composition with
+    --enc-batch kb and, for bp = 2, --decode-ahead with every slot used)."""
     import torch
     from splatt3r_amd import weights as W
     from splatt3r_amd.net import Splatt3RNet
+    if kb % bp:
+        raise SystemExit("kb must be a multiple of bp")
     H, Wd = 384, 512
     net = Splatt3RNet(W.FULL, seed=1234, graphs=False)
-    img = torch.rand(1, 3, H, Wd, device="cuda") * 2 - 1
+    img = torch.rand(kb, 3, H, Wd, device="cuda") * 2 - 1
     f, p, _ = net._encode_image(img)
-    net.infer_pair(f, p, f, p, (H, Wd))
+    fb, pb = f[:1].expand(bp, -1, -1), p[:1].expand(bp, -1, -1)
+    net.infer_pair(fb, pb, fb, pb, (H, Wd))
+    enc = net.encoder_plan(kb, H, Wd).plan
+    pair = net.pair_plan(bp, H, Wd)
+    plans = [enc] + [pair.decoder_plan, pair.head_plan] * (kb // bp)
     torch.cuda.synchronize()
-    for plan in net.plans():
+    for plan in plans:
         plan.run()
     torch.cuda.synchronize()
     for _ in range(reps):
         torch.cuda._sleep(1000)
-        for plan in net.plans():
+        for plan in plans:
             plan.run()
     torch.cuda._sleep(1000)
     torch.cuda.synchronize()
-    print("pmc_traffic run: done", reps, "frames")
+    print("pmc_traffic run: done", reps, "reps of", kb, "frames")
 
 
 def _load(d: str, counter: str):
@@ -115,7 +124,8 @@ def _frames(rows, reps: int, marker: str):
     return [rows[a + 1:b] for a, b in zip(idx[:-1], idx[1:])]
 
 
-def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str, workload: str = "network"):
+def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str, workload: str = "network",
+              kb: int = 1, bp: int = 1):
     out = {}
     for counter, d, scale in (("FETCH_SIZE", fetch_dir, 2.0), ("WRITE_SIZE", write_dir, 1.0)):
         frames = _frames(_load(d, counter), reps, marker)
@@ -125,15 +135,18 @@ def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str, workload: 
                 a = agg[_family(name)]
                 a[0] += 1
                 a[1] += kib * 1024.0 * scale
+        nf = reps * kb     # frames
         for fam, (n, b) in agg.items():
-            o = out.setdefault(fam, {"launches_per_frame": n // reps})
-            o[("read" if counter == "FETCH_SIZE" else "write") + "_bytes_per_frame"] = b / reps
+            o = out.setdefault(fam, {"launches_per_frame": n / nf})
+            o[("read" if counter == "FETCH_SIZE" else "write") + "_bytes_per_frame"] = b / nf
     for o in out.values():
         o["bytes_per_frame"] = o.get("read_bytes_per_frame", 0.0) + o.get("write_bytes_per_frame", 0.0)
-        o["bytes_per_launch"] = o["bytes_per_frame"] / max(1, o["launches_per_frame"])
+        o["bytes_per_launch"] = o["bytes_per_frame"] / max(1e-9, o["launches_per_frame"])
     return {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                       "FETCH_SIZE x2 (gfx950 correction), KiB -> bytes",
-            "workload": ("one 512x384 frame of the network (encoder + decoder + 2 heads), eager"
+            "workload": (f"512x384 frames of the network (encoder + decoder + 2 heads), eager; "
+                         f"encoder batch {kb}, pair plan Bp={bp} ({kb // bp} pair replays per "
+                         f"encoder replay), per frame"
                          if workload == "network" else
                          "C3 rasterizer: 4,194,304 splats at 960x540, forward + backward "
                          "(GaussianRasterizer, torch elementwise kernels included)"),
@@ -146,7 +159,11 @@ def main():
     r = sub.add_parser("run")
     r.add_argument("--reps", type=int, default=3)
     r.add_argument("--workload", choices=("network", "raster"), default="network")
+    r.add_argument("--kb", type=int, default=1, help="encoder batch (frames per rep)")
+    r.add_argument("--bp", type=int, default=1, help="pairs per pair-plan replay")
     s = sub.add_parser("summarize")
+    s.add_argument("--kb", type=int, default=1)
+    s.add_argument("--bp", type=int, default=1)
     s.add_argument("fetch_dir")
     s.add_argument("write_dir")
     s.add_argument("--reps", type=int, default=3)
@@ -155,9 +172,12 @@ def main():
     s.add_argument("--workload", choices=("network", "raster"), default="network")
     a = ap.parse_args()
     if a.cmd == "run":
-        (run_raster if a.workload == "raster" else run)(a.reps)
+        if a.workload == "raster":
+            run_raster(a.reps)
+        else:
+            run(a.reps, a.kb, a.bp)
         return
-    res = summarize(a.fetch_dir, a.write_dir, a.reps, a.marker, a.workload)
+    res = summarize(a.fetch_dir, a.write_dir, a.reps, a.marker, a.workload, a.kb, a.bp)
     txt = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as fh:

@@ -21,10 +21,12 @@ def main():
     ap.add_argument("--W", type=int, default=512)
     ap.add_argument("--Bp", type=int, default=1)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--EB", type=int, default=1, help="encoder batch (frames per encoder replay)")
     a = ap.parse_args()
     net = Splatt3RNet(W.FULL, seed=1234, graphs=False)
-    img = torch.rand(1, 3, a.H, a.W, device="cuda") * 2 - 1
+    img = torch.rand(a.EB, 3, a.H, a.W, device="cuda") * 2 - 1
     f, p, _ = net._encode_image(img)
+    f, p = f[:1], p[:1]
     fb, pb = f.expand(a.Bp, -1, -1).contiguous(), p.expand(a.Bp, -1, -1).contiguous()
     net.infer_pair(fb, pb, fb, pb, (a.H, a.W))
     torch.cuda.synchronize()
@@ -43,7 +45,7 @@ def main():
             d[1] += e0.elapsed_time(e1) * 1e3
             d[2] += flops
     tot = sum(v[1] for v in agg.values()) / a.reps
-    print(f"network total {tot / 1e3:.3f} ms per frame ({a.H}x{a.W}, Bp={a.Bp})")
+    print(f"network total {tot / 1e3:.3f} ms per call set ({a.H}x{a.W}, Bp={a.Bp}, encoder batch {a.EB})")
     print(f"{'launch':48s} {'n':>4s} {'us/launch':>10s} {'TFLOP/s':>8s} {'share':>6s}")
     for desc, (n, us, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         per = us / n
