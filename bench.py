@@ -74,7 +74,7 @@ def _args():
     ap.add_argument("--pairs-per-rank", type=int, default=4)
     ap.add_argument("--no-kprof", action="store_true",
                     help="skip the per-launch network profile (roofline object)")
-    ap.add_argument("--enc-batch", type=int, default=1,
+    ap.add_argument("--enc-batch", type=int, default=4,
                     help="frames per encoder replay (lookahead over the sequence); "
                          "the timed region then holds steps/enc-batch encoder replays")
     ap.add_argument("--main-priority", type=int, default=-1,
@@ -82,12 +82,13 @@ def _args():
                          "default: the next frame's encoder yields to it); 0 = normal")
     ap.add_argument("--late-prefetch", action="store_true",
                     help="queue the next frame's encoder after the tracker's GN sync")
-    ap.add_argument("--enc-ahead", type=int, default=None,
+    ap.add_argument("--enc-ahead", type=int, default=5,
                     help="frames kept queued for encoding ahead of the current one "
-                         "(default: the next enc-batch frames once frame i+1 is not queued)")
-    ap.add_argument("--decode-ahead", action="store_true",
-                    help="decode the next frame against the same keyframe in the same "
-                         "Bp=2 pair-plan replay (used when no keyframe is added in between)")
+                         "(0: the next enc-batch frames once frame i+1 is not queued)")
+    ap.add_argument("--no-decode-ahead", dest="decode_ahead", action="store_false",
+                    help="decode each frame alone (default: the next frame is decoded "
+                         "against the same keyframe in the same Bp=2 pair-plan replay, "
+                         "used when no keyframe is added in between)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="encode each frame inside its own step (no side-stream overlap)")
     return ap.parse_args()
@@ -312,7 +313,8 @@ def bench_backend(model, dev, steps, rank):
             "mode": "single_thread: False (worker thread + HIP stream, same GPU)"}
 
 
-def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, writers=3):
+def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, writers=3,
+                     enc_batch=1, enc_ahead=None, decode_ahead=False):
     """The reference's FPS definition (main.py:363-535): frames / wall time of
     the whole loop, with the host work inside it -- the dataset read (PNG
     decode of 640x480 TUM-layout frames), create_frame's resize_img (PIL
@@ -327,24 +329,26 @@ def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, wri
     from splatt3r_amd.slam import Frontend
     root = tempfile.mkdtemp(prefix="s3_tum_")
     try:
-        n = warmup + steps + 2
+        n = warmup + steps + 2 + enc_batch + max(1, enc_ahead or 1)
         write_synthetic_tum(os.path.join(root, "seq"), n, seed=7)
         ds = TUMDataset(os.path.join(root, "seq"))
         writer = RenderWriter(os.path.join(root, "renders"), workers=writers)
         fe = Frontend(model, device=dev, spatial_stride=4, render=True, render_writer=writer,
-                      main_priority=main_priority)
-        loader = FrameLoader(ds, dev, workers=workers, depth=2 * workers)
-        cur = next(loader)
+                      main_priority=main_priority, enc_batch=enc_batch, enc_ahead=enc_ahead,
+                      decode_ahead=decode_ahead)
+        look = enc_batch + max(1, enc_ahead or 1)   # lookahead frames, as the headline
+        n = warmup + steps + 1 + look
+        loader = FrameLoader(ds, dev, workers=workers, depth=max(2 * workers, look + 2))
+        win = [next(loader).consume() for _ in range(look + 1)]   # frames i .. i + look
         t0 = None
-        for i in range(n - 1):
+        for i in range(warmup + steps + 1):
             if i == warmup + 1:                  # frame 0 = INIT, W warm-up frames
                 writer.flush()
                 torch.cuda.synchronize()
                 s0 = dict(fe.stats)
                 t0 = time.perf_counter()
-            nxt = next(loader)
-            fe.step(i, cur.consume(), next_img=[nxt.consume()])
-            cur = nxt
+            fe.step(i, win[0], next_img=win[1:])
+            win = win[1:] + ([next(loader).consume()] if i + look + 1 < n else [])
         torch.cuda.synchronize()
         writer.flush()
         t = time.perf_counter() - t0
@@ -411,8 +415,13 @@ def main():
     kb = a.enc_batch
     if a.steps % kb:
         raise SystemExit(f"--steps {a.steps} must be a multiple of --enc-batch {kb}")
+    a.enc_ahead = a.enc_ahead or None
     look = kb + max(a.enc_ahead or 1, 1)       # lookahead images handed to each step
-    frames = tum_like_sequence(nfr + look, H, W, seed=rank, step_px=2.0, device=dev)
+    if look > 16:
+        raise SystemExit("--enc-batch + --enc-ahead must be <= 16")
+    # a fixed length past the timed frames: the texture (and so every frame)
+    # does not depend on the lookahead configuration
+    frames = tum_like_sequence(nfr + 16, H, W, seed=rank, step_px=2.0, device=dev)
     fe = Frontend(model, device=dev, spatial_stride=4, render=True, enc_batch=kb,
                   main_priority=a.main_priority, late_prefetch=a.late_prefetch,
                   decode_ahead=a.decode_ahead, enc_ahead=a.enc_ahead)
@@ -513,7 +522,8 @@ def main():
                              "tflops_wall": flops_frame / (net_ms * 1e-3) / 1e12}
     result["device_path_fps"] = value
     if rank == 0 and not a.no_e2e:
-        e2e = bench_end_to_end(model, dev, a.steps, a.warmup, a.main_priority)
+        e2e = bench_end_to_end(model, dev, a.steps, a.warmup, a.main_priority,
+                               enc_batch=kb, enc_ahead=a.enc_ahead, decode_ahead=a.decode_ahead)
         result["end_to_end_fps"] = e2e["frames_per_s"]
         result["end_to_end"] = e2e
     if not a.no_pairs:

@@ -96,6 +96,24 @@ __device__ float quantile_linear(const float* sorted, uint32_t n, float q) {
   return fabsf(w) < 0.5f ? a + w * (b - a) : b - (b - a) * (1.0f - w);
 }
 
+// The three splash filters of one Gaussian (splatt3r_utils.py:296-312).
+__device__ __forceinline__ bool keep(int64_t p, const float* __restrict__ means,
+                                     const float* __restrict__ scales,
+                                     const float* __restrict__ conf, float depth_min, bool use_q,
+                                     float zq, float max_scale, float min_conf) {
+  const float z = means[p * 3 + 2];
+  bool v = z > depth_min;
+  if (use_q) v = v && (z <= zq);
+  // torch max propagates NaN
+  float m = scales[p * 3 + 0];
+  const float s1 = scales[p * 3 + 1], s2 = scales[p * 3 + 2];
+  if (!(s1 <= m) && !isnan(m)) m = s1;
+  if (!(s2 <= m) && !isnan(m)) m = s2;
+  v = v && (m < max_scale);
+  if (conf && min_conf > 0.0f) v = v && (conf[p] >= min_conf);
+  return v;
+}
+
 __global__ void __launch_bounds__(kThreads)
 k_flags(int64_t n, Grid g, const float* __restrict__ means, const float* __restrict__ scales,
         const float* __restrict__ conf, float depth_min, float q, float max_scale, float min_conf,
@@ -104,28 +122,18 @@ k_flags(int64_t n, Grid g, const float* __restrict__ means, const float* __restr
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const int64_t p = g.pix(i);
-  const float z = means[p * 3 + 2];
-  bool v = z > depth_min;
   const uint32_t n0 = *n_valid0;
-  if (n0 > 0 && q < 1.0f) v = v && (z <= quantile_linear(sorted, n0, q));
-  // torch max propagates NaN
-  float m = scales[p * 3 + 0];
-  const float s1 = scales[p * 3 + 1], s2 = scales[p * 3 + 2];
-  if (!(s1 <= m) && !isnan(m)) m = s1;
-  if (!(s2 <= m) && !isnan(m)) m = s2;
-  v = v && (m < max_scale);
-  if (conf && min_conf > 0.0f) v = v && (conf[p] >= min_conf);
-  flags[i] = v ? 1u : 0u;
+  const bool use_q = n0 > 0 && q < 1.0f;
+  flags[i] = keep(p, means, scales, conf, depth_min, use_q,
+                  use_q ? quantile_linear(sorted, n0, q) : 0.0f, max_scale, min_conf) ? 1u : 0u;
 }
 
-__global__ void __launch_bounds__(kThreads)
-k_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44, const uint32_t* __restrict__ flags,
-       const uint32_t* __restrict__ offsets, float* __restrict__ out, int64_t* __restrict__ count) {
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
-  if (i == n - 1) *count = (int64_t)offsets[i] + flags[i];
-  if (!flags[i]) return;
-  const int64_t p = g.pix(i);
+// One world record (13 floats) of the Gaussian at pixel p: world transform,
+// covariance, colour, opacity (shared by both paths, so they agree bit for
+// bit).
+__device__ __forceinline__ void emit_record(const s3w_view& v, const Grid& g,
+                                            const float* __restrict__ T44, int64_t p,
+                                            float* __restrict__ o) {
   // T44: row-major [4,4] (s R | t); M[0..8] = s R, M[9..11] = t
   float M[12];
 #pragma unroll
@@ -135,7 +143,6 @@ k_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44, const uint3
     M[9 + r] = T44[r * 4 + 3];
   }
   const float x = v.means[p * 3 + 0], y = v.means[p * 3 + 1], z = v.means[p * 3 + 2];
-  float* o = out + (int64_t)offsets[i] * 13;
   for (int r = 0; r < 3; ++r) o[r] = (M[r * 3 + 0] * x + M[r * 3 + 1] * y + M[r * 3 + 2] * z) + M[9 + r];
   // quaternion_to_matrix (xyzw, two_s = 2 / (|q|^2 + 1e-8)), utils/geometry.py:24-49
   const float qi = v.rotations[p * 4 + 0], qj = v.rotations[p * 4 + 1];
@@ -171,11 +178,152 @@ k_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44, const uint3
   o[12] = v.opacities[p];
 }
 
+__global__ void __launch_bounds__(kThreads)
+k_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44, const uint32_t* __restrict__ flags,
+       const uint32_t* __restrict__ offsets, float* __restrict__ out, int64_t* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  if (i == n - 1) *count = (int64_t)offsets[i] + flags[i];
+  if (!flags[i]) return;
+  emit_record(v, g, T44, g.pix(i), out + (int64_t)offsets[i] * 13);
+}
+
+// ---- one-workgroup path (n <= kFusedMax): the whole of gaussians_to_world
+// for one view in a single launch.  The depth keys stay in LDS; the two
+// order statistics the quantile needs (ranks floor / ceil of q (n0 - 1))
+// are found by a 4-pass MSB radix select over them (8-bit digits, LDS
+// histograms, one wave per rank), the filters and a block scan give the
+// stable compaction order, and emit_record writes the records.  Same
+// values as sort -> k_flags -> scan -> k_emit, bit for bit.
+constexpr int kFusedThreads = 1024;
+constexpr int kFusedMax = 32768;
+int g_g2w_path = 0;   // s3w_set_path: 0 auto, 1 multi-kernel only, 2 fused whenever n fits
+
+// order-preserving float <-> uint32 (the radix-sort key transform)
+__device__ __forceinline__ uint32_t fkey(float z) {
+  const uint32_t u = __float_as_uint(z);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fval(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+__global__ void __launch_bounds__(kFusedThreads)
+k_g2w_fused(int n, Grid g, s3w_view v, const float* __restrict__ T44, float depth_min,
+            float q, float max_scale, float min_conf, float* __restrict__ out,
+            int64_t* __restrict__ count) {
+  __shared__ uint32_t keys[kFusedMax];
+  __shared__ uint32_t hist[2][256];
+  __shared__ uint32_t wpart[kFusedThreads / 64];
+  __shared__ uint32_t sel[2][2];   // [rank][prefix, remaining rank]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = kFusedThreads / 64;
+  // depth keys (+ the count n0 of z > depth_min)
+  uint32_t cnt = 0;
+  for (int i = tid; i < n; i += kFusedThreads) {
+    const float z = v.means[g.pix(i) * 3 + 2];
+    const bool ok = z > depth_min;
+    keys[i] = ok ? fkey(z) : 0xFFFFFFFFu;
+    cnt += ok ? 1u : 0u;
+  }
+  cnt = wave_incl_scan(cnt, lane);
+  if (lane == 63) wpart[wave] = cnt;
+  __syncthreads();
+  uint32_t n0 = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) n0 += wpart[w];
+  const bool use_q = n0 > 0 && q < 1.0f;
+  float zq = 0.0f;
+  if (use_q) {
+    // torch.quantile linear: ranks = q (n0 - 1), below / above order statistics
+    const float ranks = q * (float)(n0 - 1);
+    const uint32_t lo = (uint32_t)(int64_t)ranks, hi = (uint32_t)(int64_t)ceilf(ranks);
+    if (tid < 2) {
+      sel[tid][0] = 0u;
+      sel[tid][1] = tid == 0 ? lo : hi;
+    }
+    uint32_t mask = 0u;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int b = tid; b < 512; b += kFusedThreads) (&hist[0][0])[b] = 0u;
+      __syncthreads();
+      const uint32_t p0 = sel[0][0], p1 = sel[1][0];
+      for (int i = tid; i < n; i += kFusedThreads) {
+        const uint32_t k = keys[i];
+        const uint32_t d = (k >> shift) & 255u;
+        if ((k & mask) == p0) atomicAdd(&hist[0][d], 1u);
+        if ((k & mask) == p1) atomicAdd(&hist[1][d], 1u);
+      }
+      __syncthreads();
+      if (wave < 2) {
+        // wave t finds the digit holding its remaining rank: 4 bins per lane
+        const uint32_t rem = sel[wave][1];
+        uint32_t h[4], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { h[j] = hist[wave][4 * lane + j]; sum += h[j]; }
+        const uint32_t incl = wave_incl_scan(sum, lane);
+        const uint64_t hit = __ballot(rem < incl);
+        const int L = __ffsll((unsigned long long)hit) - 1;
+        if (lane == L) {
+          uint32_t c = incl - sum;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (rem < c + h[j]) {
+              sel[wave][0] |= (uint32_t)(4 * lane + j) << shift;
+              sel[wave][1] = rem - c;
+              break;
+            }
+            c += h[j];
+          }
+        }
+      }
+      mask |= 255u << shift;
+      __syncthreads();
+    }
+    const float a = fval(sel[0][0]), b = fval(sel[1][0]);
+    const float w = ranks - (float)(int64_t)ranks;
+    zq = fabsf(w) < 0.5f ? a + w * (b - a) : b - (b - a) * (1.0f - w);
+  }
+  // filters + stable compaction: thread t owns the contiguous index chunk t
+  const int chunk = (n + kFusedThreads - 1) / kFusedThreads;
+  const int c0 = min(n, tid * chunk), c1 = min(n, c0 + chunk);
+  uint32_t mine = 0;
+  for (int i = c0; i < c1; ++i)
+    mine += keep(g.pix(i), v.means, v.scales, v.conf, depth_min, use_q, zq, max_scale, min_conf);
+  const uint32_t incl = wave_incl_scan(mine, lane);
+  __syncthreads();                       // wpart reuse
+  if (lane == 63) wpart[wave] = incl;
+  __syncthreads();
+  uint32_t base = incl - mine, total = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    if (w < wave) base += wpart[w];
+    total += wpart[w];
+  }
+  if (tid == 0) *count = (int64_t)total;
+  for (int i = c0; i < c1; ++i) {
+    const int64_t p = g.pix(i);
+    if (!keep(p, v.means, v.scales, v.conf, depth_min, use_q, zq, max_scale, min_conf)) continue;
+    emit_record(v, g, T44, p, out + (int64_t)base * 13);
+    ++base;
+  }
+}
+
 int64_t count_for(const s3w_view* v) {
   return s3::cdiv(v->H, v->stride) * s3::cdiv(v->W, v->stride);
 }
 
 }  // namespace
+
+extern "C" void s3w_set_path(int path) { g_g2w_path = path; }
 
 extern "C" size_t s3w_workspace_bytes(int64_t n) {
   if (n <= 0) return 256;
@@ -194,8 +342,17 @@ extern "C" int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, floa
   hipStream_t st = s3::as_stream(stream);
   const int64_t n = count_for(v);
   S3_REQUIRE(n < (int64_t)1 << 31, "s3w_gaussians_to_world: too many Gaussians");
-  Ws w = carve(workspace, n);
   Grid g{v->H, v->W, v->stride, (int)s3::cdiv(v->W, v->stride)};
+  if (n <= kFusedMax && g_g2w_path != 1) {
+    // one launch (the tracked frame's stride-4 view: n = 12288 at 512x384)
+    const bool use_q = depth_max_percentile < 1.0f;
+    k_g2w_fused<<<1, kFusedThreads, 0, st>>>((int)n, g, *v, T_WC, depth_min,
+                                              use_q ? depth_max_percentile : 1.0f, max_scale,
+                                              min_confidence, out, count_dev);
+    S3_LAUNCH_CHECK();
+    return S3_OK;
+  }
+  Ws w = carve(workspace, n);
   const int blocks = (int)s3::cdiv(n, kThreads);
   S3_HIP(hipMemsetAsync(w.n_valid0, 0, sizeof(uint32_t), st));
   k_prep<<<blocks, kThreads, 0, st>>>(n, g, v->means, depth_min, w.keys_in, w.n_valid0);

@@ -116,6 +116,10 @@ class Frontend:
         # min(match_frac_k, unique_frac_f) of the frames tracked against the
         # current keyframe, in order: the decode-ahead pairing predictor
         self._kf_fracs: list[float] = []
+        # frames tracked / keyframes made at each distance (in frames) from
+        # the last keyframe: the predictor's online keyframe-rate estimate
+        self._kf_at_dist: dict[int, list[int]] = {}
+        self._last_kf_i = 0
         self.spans = None          # list -> per-frame GPU events (encoder, main chain)
         # main chain on a stream of its own priority (the encoder side stream
         # keeps the default one): the dispatcher then prefers the frame's
@@ -149,18 +153,23 @@ class Frontend:
             f.img.record_stream(self.enc_stream)
             self._queue[i + j] = (f, done)
 
-    def _pair_likely_kept(self) -> bool:
+    def _pair_likely_kept(self, i) -> bool:
         """Whether frame i + 1's slot is likely to be used: it is dropped when
         frame i becomes a keyframe, i.e. when frame i's min(match_frac_k,
         unique_frac_f) falls below match_frac_thresh (tracker.py:104-110).
-        The fraction decays as the camera leaves the keyframe; frame i's is
-        predicted by linear extrapolation of the last two frames tracked
-        against the same keyframe (no history: pair).  A wrong guess costs
-        speed only, never results."""
+        Two estimates, either of which declines the pairing: the fraction
+        decays as the camera leaves the keyframe, so frame i's is linearly
+        extrapolated from the last two frames tracked against the same
+        keyframe; and the sequence's own rate of keyframes at frame i's
+        distance from the last keyframe (>= 4 samples), declined above 0.44
+        (a Bp = 2 replay costs ~1.56 Bp = 1 replays, profiles/r03f: pairing
+        pays while the slot is kept with probability > 0.56).  A wrong
+        guess costs speed only, never results."""
         fr = self._kf_fracs
-        if len(fr) < 2:
-            return True
-        return 2.0 * fr[-1] - fr[-2] >= config["tracking"]["match_frac_thresh"]
+        if len(fr) >= 2 and 2.0 * fr[-1] - fr[-2] < config["tracking"]["match_frac_thresh"]:
+            return False
+        made, seen = self._kf_at_dist.get(i - self._last_kf_i, (0, 0))
+        return not (seen >= 4 and made > 0.44 * seen)
 
     def _ahead_source(self, i):
         """decode-ahead: the queued Frame i + 1 with its encoder ordered
@@ -171,7 +180,7 @@ class Frontend:
             q = self._queue.get(i + 1)
             if q is None:
                 return None
-            if not self._pair_likely_kept():
+            if not self._pair_likely_kept(i):
                 self.model.encoder.ahead_counts["declined"] += 1
                 return None
             torch.cuda.current_stream(self.device).wait_event(q[1])
@@ -381,6 +390,7 @@ class Frontend:
             frame.update_pointmap(X, C)
             self.keyframes.append(frame)
             self.new_kf_frames.append(i)
+            self._last_kf_i, self._kf_fracs = i, []
             self._stats["keyframes"] += 1
             self._kf_added(frame)
             self.mode = Mode.TRACKING
@@ -404,6 +414,10 @@ class Frontend:
                 self._prefetch(*b)
             self._stats["gn_iters"] += self.tracker.last_iters
             self._stats["tracked"] += 1
+            if not try_reloc:
+                st = self._kf_at_dist.setdefault(i - self._last_kf_i, [0, 0])
+                st[0] += int(add_new_kf)
+                st[1] += 1
             if try_reloc or add_new_kf:
                 self._kf_fracs = []
             else:
@@ -437,9 +451,11 @@ class Frontend:
                 if self.backend.relocalization(frame):
                     self._stats["keyframes"] += 1
                     self.new_kf_frames.append(i)
+                    self._last_kf_i, self._kf_fracs = i, []
                     self.tracker.reset_idx_f2k()
                     self.mode = Mode.TRACKING
         if add_new_kf:
+            self._last_kf_i = i
             self.keyframes.append(frame)
             self.new_kf_frames.append(i)
             self._stats["keyframes"] += 1

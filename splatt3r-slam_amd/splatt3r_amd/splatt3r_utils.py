@@ -356,6 +356,7 @@ class S3wView(ctypes.Structure):
 _P = ctypes.c_void_p
 _lib.register({
     "s3w_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64]),
+    "s3w_set_path": (None, [ctypes.c_int]),
     "s3w_gaussians_to_world": (ctypes.c_int, [ctypes.POINTER(S3wView), _P, ctypes.c_float,
                                               ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                               _P, _P, _P, _P]),

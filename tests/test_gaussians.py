@@ -78,3 +78,37 @@ def test_gaussians_to_world_all_filtered_returns_none():
     fr = Frame(0, img.cuda(), None, None, T_WC=lietorch.Sim3.Identity(1, device="cuda"))
     fr.gaussian_pred = {k: v.cuda() for k, v in p.items()}
     assert gaussians_to_world(fr, include_cross=False, spatial_stride=2) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,stride,q,maxs,minc,dmin", [
+    (384, 512, 4, 0.98, 1.0, 1.5, 0.05), (96, 128, 1, 0.98, 0.5, 1.5, 0.05),
+    (48, 64, 3, 1.0, 0.5, 0.0, 0.05), (50, 70, 4, 0.5, 10.0, 2.0, 0.05),
+    (181, 181, 1, 0.3, 10.0, 0.0, float("-inf")), (1, 1, 1, 0.98, 10.0, 0.0, 0.05),
+    (256, 256, 2, 0.98, 10.0, 0.0, 5.0)])
+def test_single_launch_path_equals_multi_pass(H, W, stride, q, maxs, minc, dmin):
+    """s3w_gaussians_to_world's one-workgroup path (n <= 32768: radix select
+    of the two quantile order statistics in LDS, block-scan compaction)
+    returns the multi-pass path's records and count bit for bit: the
+    tracker's stride-4 view, stride 1, no quantile, n0 = 0 (every z below
+    depth_min), depth_min = -inf (negative z, 32761 Gaussians), n = 1."""
+    from splatt3r_amd import _lib
+    from splatt3r_amd.splatt3r_utils import world_records
+    p, img = _pred(H, W, 7 * H + W)
+    if dmin == float("-inf"):
+        p["means"][..., 2] -= 1.0
+    view = {k: v[0].cuda() for k, v in p.items()}
+    T = _pose().cuda()
+    lib = _lib.lib()
+    outs = []
+    try:
+        for path in (1, 2):
+            lib.s3w_set_path(path)
+            rec, cnt = world_records(view, img[0].cuda(), T, stride, dmin, q, maxs, minc)
+            torch.cuda.synchronize()
+            outs.append((rec[:int(cnt.item())].cpu(), int(cnt.item())))
+    finally:
+        lib.s3w_set_path(0)
+    (r1, c1), (r2, c2) = outs
+    assert c1 == c2
+    assert torch.equal(r1, r2)

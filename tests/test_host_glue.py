@@ -139,9 +139,12 @@ def test_add_factors_vs_reference():
         fg = FactorGraph(None, [KF()] * 5, device="cpu", match_fn=lambda *a: m)
         ret = fg.add_factors(ii, jj, config["local_opt"]["min_match_frac"], is_reloc=reloc)
         assert bool(ret) == bool(g[f"af_{case}_ret"])
-        for k in ("ii", "jj", "idx_ii2jj", "idx_jj2ii", "valid_match_j", "valid_match_i",
-                  "Q_ii2jj", "Q_jj2ii"):
+        for k in ("ii", "jj", "idx_ii2jj", "idx_jj2ii", "valid_match_j", "valid_match_i"):
             np.testing.assert_array_equal(getattr(fg, k).numpy(), g[f"af_{case}_{k}"], err_msg=k)
+        # Q = sqrt(Qa * Qb) in host torch: exact on the generating machine,
+        # within 1 ulp on another CPU's vector sqrt (measured on the GPU box)
+        for k in ("Q_ii2jj", "Q_jj2ii"):
+            np.testing.assert_array_max_ulp(getattr(fg, k).numpy(), g[f"af_{case}_{k}"], maxulp=1)
 
 
 @pytest.mark.parametrize("c", [0, 1])
