@@ -46,9 +46,10 @@ int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, float depth_min
                            float depth_max_percentile, float max_scale, float min_confidence,
                            void* workspace, float* out, int64_t* count_dev, void* stream);
 
-/* Testing hook: 0 = automatic (one-workgroup single launch when n <= 32768,
- * else sort + scan passes), 1 = always the multi-pass path, 2 = the single
- * launch whenever n fits.  Both paths give identical records and counts. */
+/* Testing hook: 0 = automatic (two launches, a one-workgroup select and a
+ * chip-wide emit, when n <= 30720; else sort + scan passes), 1 = always the
+ * multi-pass path, 2 = the two-launch path whenever n fits.  Both paths give
+ * identical records and counts. */
 void s3w_set_path(int path);
 
 /* ---- SharedGaussians map buffer (splatt3r_slam/frame.py:357-463) ----

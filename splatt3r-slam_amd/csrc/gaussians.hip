@@ -188,16 +188,18 @@ k_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44, const uint3
   emit_record(v, g, T44, g.pix(i), out + (int64_t)offsets[i] * 13);
 }
 
-// ---- one-workgroup path (n <= kFusedMax): the whole of gaussians_to_world
-// for one view in a single launch.  The depth keys stay in LDS; the two
-// order statistics the quantile needs (ranks floor / ceil of q (n0 - 1))
-// are found by a 4-pass MSB radix select over them (8-bit digits, LDS
-// histograms, one wave per rank), the filters and a block scan give the
-// stable compaction order, and emit_record writes the records.  Same
-// values as sort -> k_flags -> scan -> k_emit, bit for bit.
-constexpr int kFusedThreads = 1024;
-constexpr int kFusedMax = 32768;
-int g_g2w_path = 0;   // s3w_set_path: 0 auto, 1 multi-kernel only, 2 fused whenever n fits
+// ---- two-launch path (n <= kSelMax): k_g2w_select, one workgroup, holds
+// the depth keys in LDS and finds the two order statistics the quantile
+// needs (ranks floor / ceil of q (n0 - 1)) by a 4-pass MSB radix select
+// (8-bit digits, LDS histograms, one wave per rank); it then evaluates the
+// filters into an LDS flag array and scans it (stable compaction order),
+// writing each kept Gaussian's record slot (0xffffffff = dropped) and the
+// count.  k_g2w_emit writes the records on the whole chip.  Same values as
+// sort -> k_flags -> scan -> k_emit, bit for bit, in 2 launches instead of
+// ~10 (memset, prep, the radix sort's passes, flags, the scan's passes, emit).
+constexpr int kSelThreads = 1024;
+constexpr int kSelMax = 30720;   // keys (4 B) + flags (1 B) per Gaussian in 160 KiB of LDS
+int g_g2w_path = 0;   // s3w_set_path: 0 auto, 1 multi-pass only, 2 two-launch whenever n fits
 
 // order-preserving float <-> uint32 (the radix-sort key transform)
 __device__ __forceinline__ uint32_t fkey(float z) {
@@ -217,20 +219,23 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
   return x;
 }
 
-__global__ void __launch_bounds__(kFusedThreads)
-k_g2w_fused(int n, Grid g, s3w_view v, const float* __restrict__ T44, float depth_min,
-            float q, float max_scale, float min_conf, float* __restrict__ out,
-            int64_t* __restrict__ count) {
-  __shared__ uint32_t keys[kFusedMax];
+__global__ void __launch_bounds__(kSelThreads)
+k_g2w_select(int n, Grid g, const float* __restrict__ means, const float* __restrict__ scales,
+             const float* __restrict__ conf, float depth_min, float q, float max_scale,
+             float min_conf, uint32_t* __restrict__ slot, int64_t* __restrict__ count) {
+  __shared__ uint32_t keys[kSelMax];
+  __shared__ uint8_t kept[kSelMax];
   __shared__ uint32_t hist[2][256];
-  __shared__ uint32_t wpart[kFusedThreads / 64];
+  __shared__ uint32_t wpart[kSelThreads / 64];
   __shared__ uint32_t sel[2][2];   // [rank][prefix, remaining rank]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int NW = kFusedThreads / 64;
-  // depth keys (+ the count n0 of z > depth_min)
+  constexpr int NW = kSelThreads / 64;
+  // depth keys (+ the count n0 of z > depth_min); consecutive threads take
+  // consecutive Gaussians, 4 loads in flight per thread
   uint32_t cnt = 0;
-  for (int i = tid; i < n; i += kFusedThreads) {
-    const float z = v.means[g.pix(i) * 3 + 2];
+#pragma unroll 4
+  for (int i = tid; i < n; i += kSelThreads) {
+    const float z = means[g.pix(i) * 3 + 2];
     const bool ok = z > depth_min;
     keys[i] = ok ? fkey(z) : 0xFFFFFFFFu;
     cnt += ok ? 1u : 0u;
@@ -253,10 +258,10 @@ k_g2w_fused(int n, Grid g, s3w_view v, const float* __restrict__ T44, float dept
     }
     uint32_t mask = 0u;
     for (int shift = 24; shift >= 0; shift -= 8) {
-      for (int b = tid; b < 512; b += kFusedThreads) (&hist[0][0])[b] = 0u;
+      for (int b = tid; b < 512; b += kSelThreads) (&hist[0][0])[b] = 0u;
       __syncthreads();
       const uint32_t p0 = sel[0][0], p1 = sel[1][0];
-      for (int i = tid; i < n; i += kFusedThreads) {
+      for (int i = tid; i < n; i += kSelThreads) {
         const uint32_t k = keys[i];
         const uint32_t d = (k >> shift) & 255u;
         if ((k & mask) == p0) atomicAdd(&hist[0][d], 1u);
@@ -292,15 +297,18 @@ k_g2w_fused(int n, Grid g, s3w_view v, const float* __restrict__ T44, float dept
     const float w = ranks - (float)(int64_t)ranks;
     zq = fabsf(w) < 0.5f ? a + w * (b - a) : b - (b - a) * (1.0f - w);
   }
-  // filters + stable compaction: thread t owns the contiguous index chunk t
-  const int chunk = (n + kFusedThreads - 1) / kFusedThreads;
+  // the filters, coalesced over Gaussians, into LDS flags
+#pragma unroll 4
+  for (int i = tid; i < n; i += kSelThreads)
+    kept[i] = keep(g.pix(i), means, scales, conf, depth_min, use_q, zq, max_scale, min_conf);
+  __syncthreads();
+  // stable compaction: thread t scans the contiguous chunk t of the flags
+  const int chunk = (n + kSelThreads - 1) / kSelThreads;
   const int c0 = min(n, tid * chunk), c1 = min(n, c0 + chunk);
   uint32_t mine = 0;
-  for (int i = c0; i < c1; ++i)
-    mine += keep(g.pix(i), v.means, v.scales, v.conf, depth_min, use_q, zq, max_scale, min_conf);
+  for (int i = c0; i < c1; ++i) mine += kept[i];
   const uint32_t incl = wave_incl_scan(mine, lane);
-  __syncthreads();                       // wpart reuse
-  if (lane == 63) wpart[wave] = incl;
+  if (lane == 63) wpart[wave] = incl;   // (the n0 reads of wpart are behind a barrier)
   __syncthreads();
   uint32_t base = incl - mine, total = 0;
 #pragma unroll
@@ -310,11 +318,20 @@ k_g2w_fused(int n, Grid g, s3w_view v, const float* __restrict__ T44, float dept
   }
   if (tid == 0) *count = (int64_t)total;
   for (int i = c0; i < c1; ++i) {
-    const int64_t p = g.pix(i);
-    if (!keep(p, v.means, v.scales, v.conf, depth_min, use_q, zq, max_scale, min_conf)) continue;
-    emit_record(v, g, T44, p, out + (int64_t)base * 13);
-    ++base;
+    const bool k = kept[i];
+    slot[i] = k ? base : 0xFFFFFFFFu;
+    base += k ? 1u : 0u;
   }
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_g2w_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44,
+           const uint32_t* __restrict__ slot, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t o = slot[i];
+  if (o == 0xFFFFFFFFu) return;
+  emit_record(v, g, T44, g.pix(i), out + (int64_t)o * 13);
 }
 
 int64_t count_for(const s3w_view* v) {
@@ -343,12 +360,15 @@ extern "C" int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, floa
   const int64_t n = count_for(v);
   S3_REQUIRE(n < (int64_t)1 << 31, "s3w_gaussians_to_world: too many Gaussians");
   Grid g{v->H, v->W, v->stride, (int)s3::cdiv(v->W, v->stride)};
-  if (n <= kFusedMax && g_g2w_path != 1) {
-    // one launch (the tracked frame's stride-4 view: n = 12288 at 512x384)
+  if (n <= kSelMax && g_g2w_path != 1) {
+    // two launches (the tracked frame's stride-4 view: n = 12288 at 512x384)
     const bool use_q = depth_max_percentile < 1.0f;
-    k_g2w_fused<<<1, kFusedThreads, 0, st>>>((int)n, g, *v, T_WC, depth_min,
-                                              use_q ? depth_max_percentile : 1.0f, max_scale,
-                                              min_confidence, out, count_dev);
+    uint32_t* slot = static_cast<uint32_t*>(workspace);
+    k_g2w_select<<<1, kSelThreads, 0, st>>>((int)n, g, v->means, v->scales, v->conf, depth_min,
+                                             use_q ? depth_max_percentile : 1.0f, max_scale,
+                                             min_confidence, slot, count_dev);
+    S3_LAUNCH_CHECK();
+    k_g2w_emit<<<(unsigned)s3::cdiv(n, kThreads), kThreads, 0, st>>>(n, g, *v, T_WC, slot, out);
     S3_LAUNCH_CHECK();
     return S3_OK;
   }

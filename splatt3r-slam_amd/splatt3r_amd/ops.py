@@ -190,8 +190,10 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
                 # v_mfma_f32_16x16x32 tiles, 4 waves (net_gemm_t4/t5.hip)
                 21: (64, 160), 22: (96, 64), 23: (128, 96), 24: (160, 128), 25: (256, 128),
                 26: (64, 64), 27: (128, 128), 28: (64, 128), 29: (96, 128), 30: (64, 192),
-                31: (64, 64)}
-_TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14}   # the fused tail runs with one K-group
+                31: (64, 64),
+                # 3x3 conv with halo reuse of the input row segment (net_gemm_t6.hip)
+                40: (128, 128), 41: (256, 64), 42: (128, 128), 43: (128, 128), 45: (128, 128)}
+_TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14, 40, 42, 43, 45}   # one K-group, BN == N
 # S3_GEMM_MF16=0: leave the 16x16x32 tile family out of the tuner (A/B)
 _EXCLUDED = set(range(21, 32)) if os.environ.get("S3_GEMM_MF16", "1") == "0" else set()
 
@@ -205,8 +207,12 @@ _TILE_RED = {1: (64, 1, 32), 2: (64, 1, 32), 3: (64, 1, 32), 4: (64, 1, 32), 5: 
              11: (128, 1, 32), 12: (128, 1, 32), 14: (64, 1, 32),
              15: (64, 2, 32), 16: (64, 4, 32), 17: (64, 2, 32), 18: (64, 2, 32),
              19: (128, 2, 32), 20: (64, 3, 32),
-             **{t: (64, 1, 16) for t in range(21, 31)}, 31: (128, 1, 16)}
+             **{t: (64, 1, 16) for t in range(21, 31)}, 31: (128, 1, 16),
+             40: (64, 1, 16), 41: (64, 1, 16), 42: (64, 1, 32), 43: (64, 1, 16),
+             45: (64, 1, 32)}
 _REGS_EPILOGUE = {14}
+# K tiles in (ky, channel chunk, kx) order instead of (ky, kx, channel chunk)
+_HALO = {40, 41, 42, 43, 45}
 
 
 def reduction_class(K: int, tile: int, split_k: int):
@@ -220,7 +226,7 @@ def reduction_class(K: int, tile: int, split_k: int):
     kt = -(-K // bk)
     per = -(-kt // max(1, split_k))
     bound = per * bk if -(-kt // per) > 1 else 0
-    return (mf, kg, bk if kg > 1 else 0, bound, tile in _REGS_EPILOGUE)
+    return (mf, kg, bk if kg > 1 else 0, bound, tile in _REGS_EPILOGUE, tile in _HALO)
 
 
 def _tune_key(a):
@@ -239,8 +245,13 @@ def _tune_candidates(a, split_ok, like=None):
             continue
         if a.tail_n and (bn != a.N or tile not in _TAIL_OK):
             continue
+        if tile in _HALO and not (a.a_mode == 1 and a.ksize == 3 and a.stride == 1 and
+                                  a.oW % bm == 0 and a.cC % 64 == 0):
+            continue
         tiles = a.groups * -(-a.M // bm) * -(-a.N // bn)
         for sk in (1, 2, 3, 4, 6, 8):
+            if sk > 1 and tile in _HALO:
+                continue
             if like is not None:
                 # batch-invariant plan: only launches whose elements equal
                 # those of the one-item plan's choice (like = (tile, split))

@@ -84,14 +84,15 @@ def test_gaussians_to_world_all_filtered_returns_none():
 @pytest.mark.parametrize("H,W,stride,q,maxs,minc,dmin", [
     (384, 512, 4, 0.98, 1.0, 1.5, 0.05), (96, 128, 1, 0.98, 0.5, 1.5, 0.05),
     (48, 64, 3, 1.0, 0.5, 0.0, 0.05), (50, 70, 4, 0.5, 10.0, 2.0, 0.05),
-    (181, 181, 1, 0.3, 10.0, 0.0, float("-inf")), (1, 1, 1, 0.98, 10.0, 0.0, 0.05),
+    (175, 175, 1, 0.3, 10.0, 0.0, float("-inf")), (1, 1, 1, 0.98, 10.0, 0.0, 0.05),
     (256, 256, 2, 0.98, 10.0, 0.0, 5.0)])
 def test_single_launch_path_equals_multi_pass(H, W, stride, q, maxs, minc, dmin):
-    """s3w_gaussians_to_world's one-workgroup path (n <= 32768: radix select
-    of the two quantile order statistics in LDS, block-scan compaction)
-    returns the multi-pass path's records and count bit for bit: the
-    tracker's stride-4 view, stride 1, no quantile, n0 = 0 (every z below
-    depth_min), depth_min = -inf (negative z, 32761 Gaussians), n = 1."""
+    """s3w_gaussians_to_world's two-launch path (n <= 30720: one workgroup
+    radix-selects the two quantile order statistics in LDS and block-scans
+    the filter flags, then a chip-wide emit) returns the multi-pass path's
+    records and count bit for bit: the tracker's stride-4 view, stride 1,
+    no quantile, n0 = 0 (every z below depth_min), depth_min = -inf
+    (negative z, 30625 Gaussians), n = 1."""
     from splatt3r_amd import _lib
     from splatt3r_amd.splatt3r_utils import world_records
     p, img = _pred(H, W, 7 * H + W)

@@ -451,6 +451,67 @@ def test_gemm_conv_fused_1x1_tail(tile, tn, store_c):
             assert rel_err(C[i], y.permute(0, 2, 3, 1)) < 2e-3
 
 
+@pytest.mark.parametrize("tile,B,H,W,Cin,Cout,relu,res,tail", [
+    (40, 2, 5, 256, 128, 128, True, False, False), (41, 1, 4, 256, 128, 128, False, True, False),
+    (42, 1, 6, 128, 256, 256, True, True, False), (40, 1, 7, 128, 64, 128, False, False, True),
+    (42, 2, 3, 256, 128, 128, True, False, True), (41, 1, 3, 512, 128, 64, False, False, False),
+    (43, 2, 5, 256, 128, 128, True, True, True), (43, 1, 4, 256, 256, 128, True, False, False),
+    (45, 1, 6, 128, 128, 128, False, True, True)])
+def test_gemm_halo_conv_vs_torch(tile, B, H, W, Cin, Cout, relu, res, tail):
+    """Halo-reuse 3x3 conv tiles (net_gemm_t6.hip: one input row segment per
+    (ky, channel chunk) serves the three kx taps) vs torch fp32: bias, ReLU on
+    the input, residual operands, the fused 1x1 tail, image edges (top and
+    bottom rows, the first and last column of every segment), two images."""
+    from splatt3r_amd import ops, _lib
+    g = 2
+    xs = [_rand(B, H, W, Cin, seed=81 + i) for i in range(g)]
+    ws = [_rand(Cout, Cin, 3, 3, scale=(Cin * 9) ** -0.5, seed=83 + i) for i in range(g)]
+    bs = [_rand(Cout, dtype=torch.float32, seed=85 + i) for i in range(g)]
+    r1 = [_rand(B, H, W, Cout, dtype=torch.float32, seed=87 + i) for i in range(g)] if res else None
+    wk = [w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous() for w in ws]
+    out = [torch.empty(B, H, W, Cout, device="cuda") for _ in range(g)]
+    conv = dict(H=H, W=W, C=Cin, k=3, stride=1, pad=1, oH=H, oW=W, relu_in=relu)
+    kw = dict(lda=0, conv=conv, bias=bs, act="relu" if tail else "none", tile=tile, split_k=1)
+    if res:
+        kw.update(R1=r1, ldr1=Cout)
+    tn = 16
+    if tail:
+        tw = [_rand(tn, Cout, scale=Cout ** -0.5, seed=89 + i) for i in range(g)]
+        tb = [_rand(tn, dtype=torch.float32, seed=91 + i) for i in range(g)]
+        tout = [torch.empty(B * H * W, tn, device="cuda") for _ in range(g)]
+        kw["tail"] = (tw, tb, tout, tn, tn)
+    ops.gemm(xs, wk, out, B * H * W, Cout, 9 * Cin, **kw)(_lib.stream())
+    for i in range(g):
+        xin = xs[i].float().permute(0, 3, 1, 2)
+        if relu:
+            xin = xin.clamp_min(0)
+        y = F.conv2d(xin, ws[i].float(), bs[i], padding=1).permute(0, 2, 3, 1)
+        if tail:
+            y = F.relu(y)
+        if res:
+            y = y + r1[i]
+        assert rel_err(out[i], y) < 1e-5, (i, rel_err(out[i], y))
+        if tail:
+            ref = y.reshape(-1, Cout) @ tw[i].float().T + tb[i]
+            assert rel_err(tout[i], ref) < 2e-5, (i, rel_err(tout[i], ref))
+
+
+def test_gemm_halo_conv_rejects_unsupported_shapes():
+    """A halo tile on a shape it cannot tile (segment not dividing the width,
+    stride 2, Cin % 64 != 0, dense A) fails loudly; the tuner skips it."""
+    from splatt3r_amd import ops, _lib
+    x = _rand(1, 4, 96, 128, seed=1)
+    w = _rand(128, 9 * 128, scale=0.03, seed=2)
+    out = torch.empty(1, 4, 96, 128, device="cuda")
+    conv = dict(H=4, W=96, C=128, k=3, stride=1, pad=1, oH=4, oW=96)
+    with pytest.raises(RuntimeError):
+        ops.gemm([x], [w], [out], 4 * 96, 128, 9 * 128, lda=0, conv=conv, tile=40,
+                 split_k=1)(_lib.stream())
+    with pytest.raises(RuntimeError):
+        ops.gemm([x.view(384, 128)], [w[:, :128].contiguous()], [out.view(384, 128)], 384, 128,
+                 128, lda=128, tile=40, split_k=1)(_lib.stream())
+
+
 def test_gemm_and_layernorm_fp16_range_guard():
     """fp16 activations saturate at +-65504 (not inf) and raise the device
     flag s3n_f16_saturations reports; in-range outputs leave it clear."""

@@ -22,11 +22,13 @@ SHAPES = [(1, 384, 512, 128, 128), (1, 192, 256, 256, 128), (1, 96, 128, 256, 25
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="3,5,28")
+    ap.add_argument("--B", type=int, default=1, help="images per group (pairs per replay)")
     a = ap.parse_args()
     tiles = [int(t) for t in a.tiles.split(",")]
     L = _lib.lib()
     G = 4
     for B, H, W, Cin, Cout in SHAPES:
+        B *= a.B
         x = [torch.randn(B, H, W, Cin, device="cuda").half() for _ in range(G)]
         w = [(torch.randn(Cout, 9 * Cin, device="cuda") * (9 * Cin) ** -0.5).half()
              for _ in range(G)]
@@ -36,6 +38,11 @@ def main():
         fl = 2 * M * Cout * K * G
         for tile in tiles:
             c = ops.gemm(x, w, out, M, Cout, K, lda=0, conv=conv, split_k=1, tile=tile)
+            try:
+                c(_lib.stream())
+            except RuntimeError as e:          # a tile that cannot run this shape
+                print(f"{M}x{Cout}x{K} g{G} conv t{tile}: skipped ({e})", flush=True)
+                continue
             r = []
             for dbg in (0, 1, 2, 3, 8):
                 L.s3n_gemm_set_debug(dbg)

@@ -1,19 +1,19 @@
 #!/bin/bash
-# A/B of launch options on the C2 bench (no CPU / C3 / pairs legs).
-# Usage: gpurun_ab.sh TAG=ENV[,ENV...] ...   e.g. v0=S3_ATTN_VARIANT=0
+# headline A/B over $CONFIGS (';'-separated bench argument sets), device path only
 set -o pipefail
 mkdir -p gpurun_out
-run() {
-  local tag=${1%%=*} envs=${1#*=}
-  env ${envs//,/ } timeout -k 10 240 python -u bench.py --no-cpu-baseline --no-c3 --no-pairs > gpurun_out/ab_$tag.log 2>&1 || { tail -20 gpurun_out/ab_$tag.log; exit 1; }
-  python3 - gpurun_out/ab_$tag.log "$tag" <<'EOF'
-import json, sys
-line = [l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1]
-d = json.loads(line)
-r = d["roofline"]
-print(sys.argv[2], "fps", round(d["value"], 2), "ms/step", round(d["ms_per_step"], 3),
-      "gemm frac", round(r["frac"], 4),
-      "trace", {k: round(v, 3) for k, v in r.get("trace_ms_per_frame", {}).items()})
-EOF
-}
-for a in "$@"; do run "$a" || exit 1; done
+Q="--no-cpu-baseline --no-c3 --no-pairs --no-backend --no-map --no-e2e --no-kprof"
+rm -f gpurun_out/ab.log
+IFS=';' read -ra CFG <<< "$CONFIGS"
+for args in "${CFG[@]}"; do
+  echo "== $args" >> gpurun_out/ab.log
+  timeout -k 10 300 python -u bench.py $Q $args > gpurun_out/ab_run.log 2>&1 || { tail -30 gpurun_out/ab_run.log; exit 1; }
+  grep '^{' gpurun_out/ab_run.log >> gpurun_out/ab.log || { tail -30 gpurun_out/ab_run.log; exit 1; }
+done
+python - <<'PY'
+import json
+for l in open("gpurun_out/ab.log"):
+    if l.startswith("=="): print(l.strip()); continue
+    d=json.loads(l); fb=d["frame_breakdown"]
+    print(f"  {d['value']:.1f} fps  kf_rate {fb['keyframe_rate']:.2f} ahead {fb.get('decode_ahead')}")
+PY
