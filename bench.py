@@ -74,7 +74,7 @@ def _args():
     ap.add_argument("--pairs-per-rank", type=int, default=4)
     ap.add_argument("--no-kprof", action="store_true",
                     help="skip the per-launch network profile (roofline object)")
-    ap.add_argument("--enc-batch", type=int, default=4,
+    ap.add_argument("--enc-batch", type=int, default=8,
                     help="frames per encoder replay (lookahead over the sequence); "
                          "the timed region then holds steps/enc-batch encoder replays")
     ap.add_argument("--main-priority", type=int, default=-1,
@@ -82,7 +82,7 @@ def _args():
                          "default: the next frame's encoder yields to it); 0 = normal")
     ap.add_argument("--late-prefetch", action="store_true",
                     help="queue the next frame's encoder after the tracker's GN sync")
-    ap.add_argument("--enc-ahead", type=int, default=5,
+    ap.add_argument("--enc-ahead", type=int, default=8,
                     help="frames kept queued for encoding ahead of the current one "
                          "(0: the next enc-batch frames once frame i+1 is not queued)")
     ap.add_argument("--no-decode-ahead", dest="decode_ahead", action="store_false",
@@ -204,10 +204,15 @@ def _pmc_traffic(kind: str):
     import glob
     fam = {"gemm.dense": "gemm_dense", "gemm.conv": "gemm_conv"}.get(kind)
     paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
-    if not fam or not paths:
+    if not fam:
         return None
-    with open(paths[-1]) as fh:
-        d = json.load(fh)["families"].get(fam)
+    d = None
+    for path in reversed(paths):          # the newest summary that has the family
+        with open(path) as fh:
+            d = json.load(fh)["families"].get(fam)
+        if d:
+            paths = [path]
+            break
     if not d:
         return None
     return {"bytes_per_launch": d["bytes_per_launch"], "bytes_per_frame": d["bytes_per_frame"],

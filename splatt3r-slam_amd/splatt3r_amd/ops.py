@@ -196,6 +196,9 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
 _TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14, 40, 42, 43, 45}   # one K-group, BN == N
 # S3_GEMM_MF16=0: leave the 16x16x32 tile family out of the tuner (A/B)
 _EXCLUDED = set(range(21, 32)) if os.environ.get("S3_GEMM_MF16", "1") == "0" else set()
+# S3_GEMM_HALO=0: leave the halo-reuse conv tiles out of the tuner (A/B)
+if os.environ.get("S3_GEMM_HALO", "1") == "0":
+    _EXCLUDED |= {40, 41, 42, 43, 45}
 
 
 # Reduction structure of each tile (net_gemm_t*.hip launch<BM, BN, S, NWM,
