@@ -80,8 +80,9 @@ int s3t_gn_iterations_calib(const float* Xf, const float* Xk, const float* Q,
  *   counts[0] += valid_opt[i];  counts[1] += vm[i] && Q_out[i] > Q_conf;
  *   counts[2] = |{ j : some i with vm[i] has idx[i] == j }| (unique hits).
  * Xf [n,3], Cf / Ck / Qff / Qkf [n] fp32; idx int64 [n]; vm / valid_opt
- * bool bytes [n]; hit: uint32 [n] scratch; counts int64 [3] (zeroed here,
- * as is hit, inside the stream).  Exact (same fp32 ops as the reference). */
+ * bool bytes [n]; hit: uint32 [n + 192] scratch (zeroed here, inside the
+ * stream); counts int64 [3] (written here).  Exact (same fp32 ops as the
+ * reference). */
 int s3t_track_prep(const int64_t* idx, const uint8_t* vm, const float* Xf, const float* Cf,
                    const float* Ck, const float* Qff, const float* Qkf, int64_t n, float C_conf,
                    float Q_conf, float* Xf_out, float* Q_out, uint8_t* valid_opt,

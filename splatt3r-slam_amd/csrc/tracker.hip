@@ -345,10 +345,15 @@ extern "C" int s3t_gn_iterations_calib(const float* Xf, const float* Xk, const f
 // ------------------------------------------------------------ track prep --
 // FrameTracker.track's correspondence filter (include/s3t.h s3t_track_prep):
 // gathers, the three validity masks and the decision counts in one pass.
-// Counts: wave ballots, one 64-bit atomic per wave and count (exact
-// integers, so the result does not depend on the order).  Unique hits: the
-// first writer of hit[j] (atomicExch returns 0) counts it.
+// Counts: wave ballots summed over the workgroup in LDS, then one atomic per
+// workgroup and count into one of 64 spread slots (slot = workgroup mod 64:
+// one address per count took ~9k serialised atomics per frame, ~110 us), and
+// k_track_count sums the slots (exact integers, so the result does not depend
+// on the order).  Unique hits: the first writer of hit[j] (atomicExch returns
+// 0) counts it.  The slots live behind the n hit words.
 namespace {
+
+constexpr int kTrackSlots = 64;
 
 __global__ void __launch_bounds__(kThreads)
 k_track_prep(const int64_t* __restrict__ idx, const uint8_t* __restrict__ vm,
@@ -356,8 +361,8 @@ k_track_prep(const int64_t* __restrict__ idx, const uint8_t* __restrict__ vm,
              const float* __restrict__ Ck, const float* __restrict__ Qff,
              const float* __restrict__ Qkf, int64_t n, float C_conf, float Q_conf,
              float* __restrict__ Xf_out, float* __restrict__ Q_out,
-             uint8_t* __restrict__ valid_opt, uint32_t* __restrict__ hit,
-             unsigned long long* __restrict__ counts) {
+             uint8_t* __restrict__ valid_opt, uint32_t* __restrict__ hit) {
+  __shared__ uint32_t s_cnt[kThreads / 64][3];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool vopt = false, vkf = false, uniq = false;
   if (i < n) {
@@ -375,11 +380,31 @@ k_track_prep(const int64_t* __restrict__ idx, const uint8_t* __restrict__ vm,
     valid_opt[i] = vopt ? 1 : 0;
     if (m) uniq = atomicExch(&hit[j], 1u) == 0u;
   }
+  const int w = threadIdx.x >> 6;
   const unsigned long long b0 = __ballot(vopt), b1 = __ballot(vkf), b2 = __ballot(uniq);
   if ((threadIdx.x & 63) == 0) {
-    if (b0) atomicAdd(&counts[0], (unsigned long long)__popcll(b0));
-    if (b1) atomicAdd(&counts[1], (unsigned long long)__popcll(b1));
-    if (b2) atomicAdd(&counts[2], (unsigned long long)__popcll(b2));
+    s_cnt[w][0] = (uint32_t)__popcll(b0);
+    s_cnt[w][1] = (uint32_t)__popcll(b1);
+    s_cnt[w][2] = (uint32_t)__popcll(b2);
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < kThreads / 64; ++k) t += s_cnt[k][threadIdx.x];
+    if (t) atomicAdd(&hit[n + (blockIdx.x % kTrackSlots) * 3 + threadIdx.x], t);
+  }
+}
+
+// counts[c] = sum of the spread slots of count c (one wave)
+__global__ void __launch_bounds__(64)
+k_track_count(const uint32_t* __restrict__ slots, int64_t* __restrict__ counts) {
+  const int lane = threadIdx.x;
+  for (int c = 0; c < 3; ++c) {
+    unsigned long long v = slots[lane * 3 + c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) counts[c] = (int64_t)v;
   }
 }
 
@@ -391,16 +416,19 @@ extern "C" int s3t_track_prep(const int64_t* idx, const uint8_t* vm, const float
                               float* Xf_out, float* Q_out, uint8_t* valid_opt, uint32_t* hit,
                               int64_t* counts, void* stream) {
   S3_REQUIRE(n >= 0, "s3t_track_prep: bad n");
+  S3_REQUIRE(hit && counts, "s3t_track_prep: null scratch / counts");
   S3_REQUIRE(n == 0 || (idx && vm && Xf && Cf && Ck && Qff && Qkf && Xf_out && Q_out &&
-                        valid_opt && hit && counts),
+                        valid_opt),
              "s3t_track_prep: null operand");
   hipStream_t st = s3::as_stream(stream);
-  if (counts) S3_HIP(hipMemsetAsync(counts, 0, 3 * sizeof(int64_t), st));
-  if (n == 0) return S3_OK;
-  S3_HIP(hipMemsetAsync(hit, 0, (size_t)n * sizeof(uint32_t), st));
-  k_track_prep<<<(unsigned)s3::cdiv(n, kThreads), kThreads, 0, st>>>(
-      idx, vm, Xf, Cf, Ck, Qff, Qkf, n, C_conf, Q_conf, Xf_out, Q_out, valid_opt, hit,
-      reinterpret_cast<unsigned long long*>(counts));
+  // the hit flags and the count slots behind them, zeroed in one fill
+  S3_HIP(hipMemsetAsync(hit, 0, ((size_t)n + kTrackSlots * 3) * sizeof(uint32_t), st));
+  if (n > 0) {
+    k_track_prep<<<(unsigned)s3::cdiv(n, kThreads), kThreads, 0, st>>>(
+        idx, vm, Xf, Cf, Ck, Qff, Qkf, n, C_conf, Q_conf, Xf_out, Q_out, valid_opt, hit);
+    S3_LAUNCH_CHECK();
+  }
+  k_track_count<<<1, 64, 0, st>>>(hit + n, counts);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

@@ -59,7 +59,7 @@ def track_prep(idx, vm, Xf, Cf, Ck, Qff, Qkf, C_conf, Q_conf):
     Xo = torch.empty(n, 3, device=dev)
     Qo = torch.empty(n, 1, device=dev)
     vo = torch.empty(n, 1, device=dev, dtype=torch.bool)
-    hit = torch.empty(n, device=dev, dtype=torch.int32)
+    hit = torch.empty(n + 192, device=dev, dtype=torch.int32)   # flags + count slots (s3t.h)
     cnt = torch.empty(3, device=dev, dtype=torch.int64)
     _lib.call("s3t_track_prep", *(x.data_ptr() for x in t), n, float(C_conf), float(Q_conf),
               Xo.data_ptr(), Qo.data_ptr(), vo.data_ptr(), hit.data_ptr(), cnt.data_ptr(),
