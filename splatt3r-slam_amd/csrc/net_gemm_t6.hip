@@ -222,6 +222,9 @@ int launch_t6(int tile, const GemmP& p, hipStream_t st) {
   if (tile == 42) return launch_halo<128, 128, 2, 2, 32, false>(p, st);
   if (tile == 43) return launch_halo<128, 128, 2, 2, 16, true>(p, st);
   if (tile == 45) return launch_halo<128, 128, 2, 2, 32, true>(p, st);
+  // 8 waves (two per SIMD: one wave's LDS reads hide behind the other's MFMAs)
+  if (tile == 46) return launch_halo<128, 128, 2, 4, 16, false>(p, st);
+  if (tile == 47) return launch_halo<256, 64, 4, 2, 16, false>(p, st);
   return kNotMine;
 }
 int sat_t6(int reset) { return read_sat(reset); }
