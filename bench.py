@@ -179,6 +179,8 @@ def _kernel_trace(units, reps=5):
             m = _KFAM.search(e.name)
             if m:
                 k = "gemm.dense" if m.group(1).split(",")[4].strip() == "0" else "gemm.conv"
+            elif "k_conv3_halo" in e.name:     # the halo-reuse conv tiles (net_gemm_t6.hip)
+                k = "gemm.conv"
             elif "k_splitk_reduce" in e.name:
                 k = "gemm.dense"
             elif "k_attn" in e.name:

@@ -38,6 +38,8 @@ def _family(name: str) -> str:
     m = re.search(r"k_gemm<(\d+), (\d+), \d+, \d+, (\d+),", name)
     if m:
         return "gemm_dense" if m.group(3) == "0" else "gemm_conv"
+    if "k_conv3_halo" in name:        # halo-reuse conv tiles: the conv GEMM family
+        return "gemm_conv"
     m = re.search(r"\b(k_\w+)", name)
     return m.group(1) if m else name[:40]
 
