@@ -89,6 +89,10 @@ def _args():
                     help="decode each frame alone (default: the next frame is decoded "
                          "against the same keyframe in the same Bp=2 pair-plan replay, "
                          "used when no keyframe is added in between)")
+    ap.add_argument("--e2e-loaders", type=int, default=4,
+                    help="end-to-end leg: dataset read + resize_img threads")
+    ap.add_argument("--e2e-writers", type=int, default=3,
+                    help="end-to-end leg: render PNG writer threads")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="encode each frame inside its own step (no side-stream overlap)")
     return ap.parse_args()
@@ -530,6 +534,7 @@ def main():
     result["device_path_fps"] = value
     if rank == 0 and not a.no_e2e:
         e2e = bench_end_to_end(model, dev, a.steps, a.warmup, a.main_priority,
+                               workers=a.e2e_loaders, writers=a.e2e_writers,
                                enc_batch=kb, enc_ahead=a.enc_ahead, decode_ahead=a.decode_ahead)
         result["end_to_end_fps"] = e2e["frames_per_s"]
         result["end_to_end"] = e2e

@@ -225,6 +225,9 @@ int launch_t6(int tile, const GemmP& p, hipStream_t st) {
   // 8 waves (two per SIMD: one wave's LDS reads hide behind the other's MFMAs)
   if (tile == 46) return launch_halo<128, 128, 2, 4, 16, false>(p, st);
   if (tile == 47) return launch_halo<256, 64, 4, 2, 16, false>(p, st);
+  if (tile == 48) return launch_halo<128, 128, 2, 4, 32, false>(p, st);
+  if (tile == 49) return launch_halo<128, 128, 2, 4, 16, true>(p, st);
+  if (tile == 50) return launch_halo<256, 64, 4, 2, 16, true>(p, st);
   return kNotMine;
 }
 int sat_t6(int reset) { return read_sat(reset); }
