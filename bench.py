@@ -85,6 +85,9 @@ def _args():
     ap.add_argument("--enc-ahead", type=int, default=8,
                     help="frames kept queued for encoding ahead of the current one "
                          "(0: the next enc-batch frames once frame i+1 is not queued)")
+    ap.add_argument("--no-render-async", dest="render_async", action="store_false",
+                    help="render + PNG write / read-back on the tracking thread (default: on "
+                         "a render worker thread and stream, slam._RenderWorker)")
     ap.add_argument("--no-decode-ahead", dest="decode_ahead", action="store_false",
                     help="decode each frame alone (default: the next frame is decoded "
                          "against the same keyframe in the same Bp=2 pair-plan replay, "
@@ -325,7 +328,7 @@ def bench_backend(model, dev, steps, rank):
 
 
 def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, writers=3,
-                     enc_batch=1, enc_ahead=None, decode_ahead=False):
+                     enc_batch=1, enc_ahead=None, decode_ahead=False, render_async=False):
     """The reference's FPS definition (main.py:363-535): frames / wall time of
     the whole loop, with the host work inside it -- the dataset read (PNG
     decode of 640x480 TUM-layout frames), create_frame's resize_img (PIL
@@ -346,7 +349,7 @@ def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, wri
         writer = RenderWriter(os.path.join(root, "renders"), workers=writers)
         fe = Frontend(model, device=dev, spatial_stride=4, render=True, render_writer=writer,
                       main_priority=main_priority, enc_batch=enc_batch, enc_ahead=enc_ahead,
-                      decode_ahead=decode_ahead)
+                      decode_ahead=decode_ahead, render_async=render_async)
         look = enc_batch + max(1, enc_ahead or 1)   # lookahead frames, as the headline
         n = warmup + steps + 1 + look
         loader = FrameLoader(ds, dev, workers=workers, depth=max(2 * workers, look + 2))
@@ -354,12 +357,14 @@ def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, wri
         t0 = None
         for i in range(warmup + steps + 1):
             if i == warmup + 1:                  # frame 0 = INIT, W warm-up frames
+                fe.drain()
                 writer.flush()
                 torch.cuda.synchronize()
                 s0 = dict(fe.stats)
                 t0 = time.perf_counter()
             fe.step(i, win[0], next_img=win[1:])
             win = win[1:] + ([next(loader).consume()] if i + look + 1 < n else [])
+        fe.drain()
         torch.cuda.synchronize()
         writer.flush()
         t = time.perf_counter() - t0
@@ -435,11 +440,13 @@ def main():
     frames = tum_like_sequence(nfr + 16, H, W, seed=rank, step_px=2.0, device=dev)
     fe = Frontend(model, device=dev, spatial_stride=4, render=True, enc_batch=kb,
                   main_priority=a.main_priority, late_prefetch=a.late_prefetch,
-                  decode_ahead=a.decode_ahead, enc_ahead=a.enc_ahead)
+                  decode_ahead=a.decode_ahead, enc_ahead=a.enc_ahead,
+                  render_async=a.render_async)
     nxt = (lambda i: None) if a.no_pipeline else (lambda i: [frames[j] for j in range(i + 1, i + 1 + look)])
 
     for i in range(a.warmup + 1):          # frame 0 = INIT, then W tracked frames
         fe.step(i, frames[i], next_img=nxt(i))
+    fe.drain()
     torch.cuda.synchronize()
     s0 = dict(fe.stats)
     model.encoder.events = []
@@ -450,6 +457,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.warmup + 1, nfr):
         fe.step(i, frames[i], next_img=nxt(i))
+    fe.drain()                             # every frame's render issued
     torch.cuda.synchronize()
     _barrier(ws)
     t = time.perf_counter() - t0
@@ -474,7 +482,7 @@ def main():
                    "global_batch": ws, "seq_len": 768,
                    "parallelism": f"replicas x{ws} (tracker path does not shard)",
                    "encoder_batch": kb, "encoder_ahead": a.enc_ahead,
-                   "decode_ahead": a.decode_ahead},
+                   "decode_ahead": a.decode_ahead, "render_async": a.render_async},
         "msplats_per_s": P_frame * st["rendered"] * ws / t_max / 1e6,
         "frame_breakdown": {"network_ms": net_ms,
                             "rest_ms": t_max / a.steps * 1e3 - net_ms,
@@ -535,7 +543,8 @@ def main():
     if rank == 0 and not a.no_e2e:
         e2e = bench_end_to_end(model, dev, a.steps, a.warmup, a.main_priority,
                                workers=a.e2e_loaders, writers=a.e2e_writers,
-                               enc_batch=kb, enc_ahead=a.enc_ahead, decode_ahead=a.decode_ahead)
+                               enc_batch=kb, enc_ahead=a.enc_ahead, decode_ahead=a.decode_ahead,
+                               render_async=a.render_async)
         result["end_to_end_fps"] = e2e["frames_per_s"]
         result["end_to_end"] = e2e
     if not a.no_pairs:

@@ -28,7 +28,10 @@ encoded exactly once from its own image, with M = 768k-row GEMMs.
 """
 from __future__ import annotations
 
+import queue
+import threading
 import time
+import types
 
 import torch
 
@@ -43,12 +46,85 @@ from splatt3r_amd.tracker import FrameTracker
 __all__ = ["Frontend", "should_append_gaussians"]
 
 
+class _RenderTicket:
+    """A render queued on the render worker: `keep(finish)` hands the image
+    to `finish` (run on the worker, on its stream), `drop()` discards it.
+    Every ticket gets exactly one decision; the worker waits for it."""
+
+    def __init__(self):
+        self.decided = threading.Event()
+        self.finish = None
+        self.done = threading.Event()
+
+    def keep(self, finish):
+        self.finish = finish
+        self.decided.set()
+
+    def drop(self):
+        self.decided.set()
+
+
+class _RenderWorker:
+    """splatt3r_render off the tracking thread, on its own HIP stream.
+
+    The rasterizer sizes its binning buffers from num_rendered, a host read
+    (diff_gaussian_rasterization forward): on the tracking thread that read
+    drained the main stream every frame and the host then issued the rest of
+    the frame while the GPU idled (`profiles/r03k_timeline.txt`, 11 % idle in
+    host-issue gaps; `profiles/r03l_host_profile.log`: 4.6 ms per frame of the
+    tracking thread's 6.7 spent inside that forward).  Here the tracking
+    thread records an event and queues the render; the worker's stream waits
+    on the event, renders (the same kernels, so the same image bit for bit),
+    waits for the tracker's keep / drop decision and then runs the frame's
+    PNG write / read-back on its stream.  ctypes releases the GIL during the
+    library's blocking calls, so the tracking thread keeps issuing the next
+    frame meanwhile.  One daemon thread, FIFO: renders finish in frame order."""
+
+    def __init__(self, device):
+        self.stream = torch.cuda.Stream(device=device)
+        self.q: queue.Queue = queue.Queue()
+        self.error = None
+        self.thread = threading.Thread(target=self._loop, name="s3-render", daemon=True)
+        self.thread.start()
+
+    def _loop(self):
+        while True:
+            task = self.q.get()
+            if task is None:
+                return
+            ev, fn, ticket = task
+            try:
+                with torch.cuda.stream(self.stream):
+                    self.stream.wait_event(ev)
+                    img = fn()
+                    # the tracker decides right after its GN sync; a decision
+                    # that never comes (an exception on the tracking thread)
+                    # drops the render instead of blocking the queue
+                    if not ticket.decided.wait(60.0):
+                        img = None
+                    if ticket.finish is not None and img is not None:
+                        ticket.finish(img)
+            except BaseException as e:          # surfaced by drain()
+                self.error = e
+            finally:
+                ticket.done.set()
+
+    def submit(self, fn, tensors) -> _RenderTicket:
+        ev = torch.cuda.Event()
+        ev.record()                          # the tracking thread's stream position
+        for t in tensors:                    # read on the worker stream: keep the blocks
+            t.record_stream(self.stream)
+        ticket = _RenderTicket()
+        self.q.put((ev, fn, ticket))
+        return ticket
+
+
 class Frontend:
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
                  readback=True, enc_batch=1, main_priority=None, late_prefetch=False,
                  viz=False, max_gaussians=4 * 1024 * 1024, backend=None, render_writer=None,
-                 decode_ahead=False, enc_ahead=None):
+                 decode_ahead=False, enc_ahead=None, render_async=False):
         self.model = model
         # dataio.RenderWriter: the per-frame gs_init_* / gs_track_* PNG export
         # (main.py:436-446, 490-506), written off the tracking thread
@@ -113,6 +189,10 @@ class Frontend:
         # keyframe in the same Bp = 2 replay; the result is used when that
         # frame is tracked against the same keyframe
         self.decode_ahead = decode_ahead
+        # render_async: splatt3r_render + its PNG write / read-back on a
+        # worker thread and stream (_RenderWorker); drain() waits for them
+        self._rworker = _RenderWorker(device) if render_async and render else None
+        self._tickets: list = []
         # min(match_frac_k, unique_frac_f) of the frames tracked against the
         # current keyframe, in order: the decode-ahead pairing predictor
         self._kf_fracs: list[float] = []
@@ -195,14 +275,49 @@ class Frontend:
         frame.T_WC = T_WC
         return frame
 
+    def drain(self):
+        """Wait until every queued render (and its PNG write / read-back) has
+        been issued by the render worker (no-op without one)."""
+        for t in self._tickets:
+            t.done.wait()
+        self._tickets = []
+        if self._rworker is not None and self._rworker.error is not None:
+            e, self._rworker.error = self._rworker.error, None
+            raise e
+
     @property
     def last_render(self):
+        self.drain()
         if self._rb_event is not None:
             self._rb_event.synchronize()
         return self._last_render
 
+    def _render_task(self, frame, ref, target):
+        """splatt3r_render of `frame` at pose `target` (None: its own pose)
+        queued on the render worker; returns the ticket."""
+        snap = types.SimpleNamespace(gaussian_pred=frame.gaussian_pred,
+                                     gaussian_pred_cross=frame.gaussian_pred_cross,
+                                     img=frame.img, T_WC=frame.T_WC)
+        rsnap = types.SimpleNamespace(img=ref.img)
+        tgt = frame.T_WC if target is None else target
+        ts = [snap.img, rsnap.img, snap.T_WC.data, tgt.data]
+        for g in (snap.gaussian_pred, snap.gaussian_pred_cross):
+            if g is not None:
+                ts += [v for v in g.values() if torch.is_tensor(v)]
+        model, K = self.model, self.K
+        t = self._rworker.submit(lambda: splatt3r_render(model, snap, rsnap, K=K, target_T_WC=tgt),
+                                 ts)
+        self._tickets = [x for x in self._tickets if not x.done.is_set()] + [t]
+        return t
+
     def _render(self, frame, ref, target, prefix="gs_track"):
         if not self.render:
+            return
+        if self._rworker is not None:
+            idx = frame.frame_id
+            self._stats["rendered"] += 1
+            self._render_task(frame, ref, target).keep(
+                lambda img: self._finish_render(img, idx, prefix, count=False))
             return
         self._finish_render(splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=target),
                             frame.frame_id, prefix)
@@ -218,16 +333,21 @@ class Frontend:
             frame.T_WC = T_WC
             try:
                 recs = self._world_records(frame)
-                img = (splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=T_WC)
-                       if self.render else None)
+                if not self.render:
+                    img = None
+                elif self._rworker is not None:
+                    img = self._render_task(frame, ref, T_WC)      # a ticket
+                else:
+                    img = splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=T_WC)
             finally:
                 frame.T_WC = saved
             return recs, img
         return hook
 
-    def _finish_render(self, img, index=0, prefix="gs_track"):
+    def _finish_render(self, img, index=0, prefix="gs_track", count=True):
         if img is not None:
-            self._stats["rendered"] += 1
+            if count:
+                self._stats["rendered"] += 1
             if self.render_writer is not None:
                 self.render_writer.submit(index, img, prefix)
                 self._last_render, self._rb_event = None, None
@@ -410,6 +530,9 @@ class Frontend:
             # the keyframe (the same object here, a shared-memory copy there)
             T_state = frame.T_WC
             spec = self.tracker.spec if (self.tracker.spec_valid and not try_reloc) else None
+            if (spec is None and self.tracker.spec is not None
+                    and isinstance(self.tracker.spec[1], _RenderTicket)):
+                self.tracker.spec[1].drop()         # speculative render not kept
             for b in pending:
                 self._prefetch(*b)
             self._stats["gn_iters"] += self.tracker.last_iters
@@ -432,7 +555,11 @@ class Frontend:
                 elif self._to_world(frame, len(self.keyframes)) is not None and self.viz:
                     self.last_append_T_WC, self.last_append_idx = frame.T_WC, i
             if not try_reloc:
-                if spec is not None:
+                if spec is not None and isinstance(spec[1], _RenderTicket):
+                    self._stats["rendered"] += 1
+                    spec[1].keep(lambda img, i=i: self._finish_render(img, i, "gs_track",
+                                                                      count=False))
+                elif spec is not None:
                     self._finish_render(spec[1], i, "gs_track")
                 else:
                     self._render(frame, self.keyframes.last_keyframe(), frame.T_WC)

@@ -102,6 +102,62 @@ def test_decode_ahead_frontend_matches_sequential():
 
 
 @pytest.mark.gpu
+def test_render_worker_matches_inline_render(tmp_path):
+    """render_async (slam._RenderWorker: splatt3r_render + read-back / PNG
+    write on a worker thread and HIP stream, keep / drop decided by the
+    tracker) renders the same images bit for bit as the inline path, with
+    the same counters, with and without decode-ahead, and writes the same
+    PNG files."""
+    import numpy as np
+    from PIL import Image
+    from splatt3r_amd.dataio import RenderWriter
+    from splatt3r_amd.slam import Frontend
+    from splatt3r_amd.splatt3r_utils import load_splatt3r
+    from splatt3r_amd.synthetic import tum_like_sequence
+    from splatt3r_amd.weights import FULL
+
+    dev = torch.device("cuda", 0)
+    model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
+    n = 10
+    frames = tum_like_sequence(n + 6, 384, 512, seed=5, step_px=2.0, device=dev)
+
+    def run(async_, ahead):
+        fe = Frontend(model, device=dev, spatial_stride=4, render=True, render_async=async_,
+                      enc_batch=2 if ahead else 1, enc_ahead=3 if ahead else None,
+                      decode_ahead=ahead)
+        renders = []
+        for i in range(n):
+            fe.step(i, frames[i], next_img=[frames[j] for j in range(i + 1, min(n, i + 6))])
+            renders.append(fe.last_render.clone())
+        fe.drain()
+        torch.cuda.synchronize()
+        return renders, dict(fe.stats)
+
+    r0, st0 = run(False, False)
+    for async_, ahead in ((True, False), (True, True)):
+        r1, st1 = run(async_, ahead)
+        assert st0 == st1, (async_, ahead)
+        for a, b in zip(r0, r1):
+            assert torch.equal(a, b), (async_, ahead)
+    # PNG path: the worker submits to the writer
+    outs = []
+    for async_ in (False, True):
+        d = tmp_path / f"png{int(async_)}"
+        w = RenderWriter(str(d), workers=2)
+        fe = Frontend(model, device=dev, spatial_stride=4, render=True, render_async=async_,
+                      render_writer=w)
+        for i in range(6):
+            fe.step(i, frames[i])
+        fe.drain()
+        w.flush()
+        w.close()
+        outs.append({p.name: np.asarray(Image.open(p)) for p in sorted(d.iterdir())})
+    assert outs[0].keys() == outs[1].keys() and len(outs[0]) == 6
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.gpu
 def test_factor_graph_rays_matches_oracle():
     """global_opt.FactorGraph on real frontend keyframes: symmetric pair
     decode + matching -> two-way edges -> device GN; the solve agrees with
