@@ -85,9 +85,9 @@ def _args():
     ap.add_argument("--enc-ahead", type=int, default=8,
                     help="frames kept queued for encoding ahead of the current one "
                          "(0: the next enc-batch frames once frame i+1 is not queued)")
-    ap.add_argument("--no-render-async", dest="render_async", action="store_false",
-                    help="render + PNG write / read-back on the tracking thread (default: on "
-                         "a render worker thread and stream, slam._RenderWorker)")
+    ap.add_argument("--render-async", action="store_true",
+                    help="render + PNG write / read-back on a render worker thread and stream "
+                         "(slam._RenderWorker; measured slower, profiles/r03m_ab.log)")
     ap.add_argument("--no-decode-ahead", dest="decode_ahead", action="store_false",
                     help="decode each frame alone (default: the next frame is decoded "
                          "against the same keyframe in the same Bp=2 pair-plan replay, "

@@ -78,7 +78,11 @@ class _RenderWorker:
     waits for the tracker's keep / drop decision and then runs the frame's
     PNG write / read-back on its stream.  ctypes releases the GIL during the
     library's blocking calls, so the tracking thread keeps issuing the next
-    frame meanwhile.  One daemon thread, FIFO: renders finish in frame order."""
+    frame meanwhile.  One daemon thread, FIFO: renders finish in frame order.
+    Measured (profiles/r03m_ab.log, bench device path, one box): 152.6 /
+    163.1 frames/s with the worker vs 167.0 / 167.6 inline -- the GPU was not
+    idle during the tracking thread's wait, and the worker's Python competes
+    for the GIL -- so it is opt-in (Frontend(render_async=True))."""
 
     def __init__(self, device):
         self.stream = torch.cuda.Stream(device=device)
