@@ -24,8 +24,8 @@
 
 namespace {
 
-template <int BM, int BN, int NWM, int NWN, int MF, bool RELU_IN, bool PIPE>
-__global__ void __launch_bounds__(64 * NWM * NWN, 1) k_conv3_halo(GemmP p) {
+template <int BM, int BN, int NWM, int NWN, int MF, bool RELU_IN, bool PIPE, int S>
+__global__ void __launch_bounds__(64 * NWM * NWN, S == 1 ? 2 : 1) k_conv3_halo(GemmP p) {
   typedef AccT<MF> AT;
   constexpr int NW = NWM * NWN;
   constexpr int NT = 64 * NW;
@@ -40,8 +40,14 @@ __global__ void __launch_bounds__(64 * NWM * NWN, 1) k_conv3_halo(GemmP p) {
   static_assert(BW * 8 * NW == BN, "B rows split over waves");
   constexpr int A_EL = AINS * 8 * BK;
   constexpr int B_EL = BN * BK;
-  constexpr int STAGE = A_EL + 3 * B_EL;
-  __shared__ __attribute__((aligned(1024))) f16 smem[2 * STAGE];
+  constexpr int STAGE0 = A_EL + 3 * B_EL;
+  // S = 1 (one super-stage, two workgroups per CU: one's DMA and epilogue
+  // overlap the other's MFMAs): the stage also holds the epilogue's padded
+  // fp32 tile and the fused tail's weights
+  constexpr int EPI_EL = (BM * (BN + 4) * 4 + 16 * BN * 2) / 2;
+  constexpr int STAGE = S == 1 ? ((STAGE0 > EPI_EL ? STAGE0 : EPI_EL) + 511) / 512 * 512 : STAGE0;
+  static_assert(S == 1 || S == 2, "one or two super-stages");
+  __shared__ __attribute__((aligned(1024))) f16 smem[S * STAGE];
 
   const int g = blockIdx.z;
   const int nwg = p.tiles_m * p.tiles_n;
@@ -115,12 +121,19 @@ __global__ void __launch_bounds__(64 * NWM * NWN, 1) k_conv3_halo(GemmP p) {
   const int SSn = (p.debug & 8) ? 0 : SS;
   if (SSn > 0) issue(0, 0);
   for (int ss = 0; ss < SSn; ++ss) {
+    if constexpr (S == 1) {
+      if (ss > 0) {
+        __builtin_amdgcn_s_barrier();   // every wave is done reading the stage
+        issue(ss, 0);
+      }
+    }
     // this super-step's DMA (the only one outstanding) has landed, and every
     // wave is done reading the stage the next one overwrites
     wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    if (ss + 1 < SSn) issue(ss + 1, (ss + 1) & 1);
-    const f16* As = smem + (ss & 1) * STAGE;
+    if constexpr (S == 2)
+      if (ss + 1 < SSn) issue(ss + 1, (ss + 1) & 1);
+    const f16* As = smem + (S == 2 ? (ss & 1) : 0) * STAGE;
     const f16* Bs = As + A_EL;
     constexpr int NKS = BK / AT::KS;
     // fragments of tap kx: A rows shifted by kx (the halo), B tile kx
@@ -179,14 +192,14 @@ __global__ void __launch_bounds__(64 * NWM * NWN, 1) k_conv3_halo(GemmP p) {
     }
   }
   if (p.debug & 4) return;
-  constexpr int RING = 2 * STAGE * 2;
+  constexpr int RING = S * STAGE * 2;
   constexpr int LDT = BM * (BN + 4) * 4 <= RING ? BN + 4 : BN;
   static_assert(BM * LDT * 4 <= RING, "fp32 tile staged in the LDS ring");
   epilogue_vec<BM, BN, NWM, NWN, FM, FN, LDT, RING, 1, MF>(p, g, m0, n0, acc,
                                                            reinterpret_cast<float*>(smem));
 }
 
-template <int BM, int BN, int NWM, int NWN, int MF, bool PIPE>
+template <int BM, int BN, int NWM, int NWN, int MF, bool PIPE, int S = 2>
 int launch_halo(const GemmP& p, hipStream_t st) {
   S3_REQUIRE(p.a_mode != S3N_A_DENSE && p.ks == 3 && p.st == 1 && p.pad == 1 &&
                  p.cH == p.oH && p.cW == p.oW,
@@ -202,9 +215,9 @@ int launch_halo(const GemmP& p, hipStream_t st) {
   q.split_k = 1;
   dim3 grid(q.tiles_m * q.tiles_n, 1, p.groups);
   if (p.relu_in)
-    k_conv3_halo<BM, BN, NWM, NWN, MF, true, PIPE><<<grid, 64 * NWM * NWN, 0, st>>>(q);
+    k_conv3_halo<BM, BN, NWM, NWN, MF, true, PIPE, S><<<grid, 64 * NWM * NWN, 0, st>>>(q);
   else
-    k_conv3_halo<BM, BN, NWM, NWN, MF, false, PIPE><<<grid, 64 * NWM * NWN, 0, st>>>(q);
+    k_conv3_halo<BM, BN, NWM, NWN, MF, false, PIPE, S><<<grid, 64 * NWM * NWN, 0, st>>>(q);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }
@@ -228,6 +241,10 @@ int launch_t6(int tile, const GemmP& p, hipStream_t st) {
   if (tile == 48) return launch_halo<128, 128, 2, 4, 32, false>(p, st);
   if (tile == 49) return launch_halo<128, 128, 2, 4, 16, true>(p, st);
   if (tile == 50) return launch_halo<256, 64, 4, 2, 16, true>(p, st);
+  // one super-stage, two workgroups per CU
+  if (tile == 51) return launch_halo<128, 128, 2, 2, 16, false, 1>(p, st);
+  if (tile == 52) return launch_halo<128, 128, 2, 2, 32, false, 1>(p, st);
+  if (tile == 53) return launch_halo<256, 64, 2, 2, 16, false, 1>(p, st);
   return kNotMine;
 }
 int sat_t6(int reset) { return read_sat(reset); }

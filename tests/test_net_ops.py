@@ -458,7 +458,9 @@ def test_gemm_conv_fused_1x1_tail(tile, tn, store_c):
     (43, 2, 5, 256, 128, 128, True, True, True), (43, 1, 4, 256, 256, 128, True, False, False),
     (45, 1, 6, 128, 128, 128, False, True, True), (46, 2, 3, 256, 128, 128, True, True, True),
     (47, 1, 4, 256, 256, 128, True, False, False), (48, 1, 5, 128, 128, 128, True, True, True),
-    (49, 2, 4, 128, 256, 128, False, True, True), (50, 1, 3, 256, 128, 64, True, False, False)])
+    (49, 2, 4, 128, 256, 128, False, True, True), (50, 1, 3, 256, 128, 64, True, False, False),
+    (51, 2, 5, 256, 128, 128, True, True, True), (52, 1, 4, 128, 256, 128, False, False, True),
+    (53, 1, 3, 512, 128, 128, True, True, False)])
 def test_gemm_halo_conv_vs_torch(tile, B, H, W, Cin, Cout, relu, res, tail):
     """Halo-reuse 3x3 conv tiles (net_gemm_t6.hip: one input row segment per
     (ky, channel chunk) serves the three kx taps) vs torch fp32: bias, ReLU on
