@@ -38,6 +38,7 @@ int launch_t3(int tile, const GemmP& p, hipStream_t st);
 int launch_t4(int tile, const GemmP& p, hipStream_t st);
 int launch_t5(int tile, const GemmP& p, hipStream_t st);
 int launch_t6(int tile, const GemmP& p, hipStream_t st);
+int launch_t7(int tile, const GemmP& p, hipStream_t st);
 // read (and optionally reset) one translation unit's fp16 saturation flag
 int sat_t1(int reset);
 int sat_t2(int reset);
@@ -45,6 +46,7 @@ int sat_t3(int reset);
 int sat_t4(int reset);
 int sat_t5(int reset);
 int sat_t6(int reset);
+int sat_t7(int reset);
 constexpr int kNotMine = -1000;
 }  // namespace s3gemm
 

@@ -191,6 +191,8 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
                 21: (64, 160), 22: (96, 64), 23: (128, 96), 24: (160, 128), 25: (256, 128),
                 26: (64, 64), 27: (128, 128), 28: (64, 128), 29: (96, 128), 30: (64, 192),
                 31: (64, 64),
+                # 8 / 16 waves per workgroup (net_gemm_t7.hip)
+                32: (128, 128), 34: (256, 128), 35: (128, 256), 36: (256, 128), 37: (128, 128),
                 # 3x3 conv with halo reuse of the input row segment (net_gemm_t6.hip)
                 40: (128, 128), 41: (256, 64), 42: (128, 128), 43: (128, 128), 45: (128, 128),
                 46: (128, 128), 47: (256, 64), 48: (128, 128), 49: (128, 128), 50: (256, 64),
@@ -211,10 +213,11 @@ _TILE_RED = {1: (64, 1, 32), 2: (64, 1, 32), 3: (64, 1, 32), 4: (64, 1, 32), 5: 
              15: (64, 2, 32), 16: (64, 4, 32), 17: (64, 2, 32), 18: (64, 2, 32),
              19: (128, 2, 32), 20: (64, 3, 32),
              **{t: (64, 1, 16) for t in range(21, 31)}, 31: (128, 1, 16),
+             32: (64, 1, 16), 34: (64, 1, 32), 35: (64, 1, 32), 36: (64, 1, 16), 37: (64, 1, 16),
              40: (64, 1, 16), 41: (64, 1, 16), 42: (64, 1, 32), 43: (64, 1, 16),
              45: (64, 1, 32), 46: (64, 1, 16), 47: (64, 1, 16), 48: (64, 1, 32), 49: (64, 1, 16),
              50: (64, 1, 16), 51: (64, 1, 16), 52: (64, 1, 32), 53: (64, 1, 16)}
-_REGS_EPILOGUE = {14}
+_REGS_EPILOGUE = {14, 34, 35}   # the fp32 tile does not fit the LDS ring
 # K tiles in (ky, channel chunk, kx) order instead of (ky, kx, channel chunk)
 _HALO = set(range(40, 54)) - {44}
 # S3_GEMM_HALO=0: leave the halo-reuse conv tiles out of the tuner (A/B)

@@ -58,7 +58,11 @@ def test_gemm_dense_bias_residual(M, N, K, groups):
     (300, 136, 520, 1, 1, 25), (768, 1024, 1024, 1, 1, 26), (64, 64, 136, 1, 2, 26),
     (768, 2304, 768, 2, 1, 27), (130, 96, 2000, 2, 1, 27), (600, 256, 200, 1, 1, 28),
     (768, 768, 3072, 2, 3, 29), (300, 500, 1000, 1, 1, 29), (768, 3072, 1024, 1, 1, 30),
-    (200, 96, 200, 2, 5, 30), (768, 1024, 4096, 1, 2, 31), (130, 300, 968, 1, 1, 31)])
+    (200, 96, 200, 2, 5, 30), (768, 1024, 4096, 1, 2, 31), (130, 300, 968, 1, 1, 31),
+    (1536, 2304, 768, 2, 1, 32), (130, 300, 968, 1, 2, 32), (6144, 1024, 1024, 1, 1, 34),
+    (300, 200, 1000, 2, 3, 34), (1536, 768, 3072, 1, 1, 35), (520, 300, 640, 1, 1, 35),
+    (6144, 4096, 1024, 1, 1, 36), (130, 96, 2000, 2, 2, 36), (1536, 3072, 768, 2, 1, 37),
+    (64, 64, 136, 1, 1, 37)])
 def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
     """Split-K partials + ordered reduce + the full epilogue (bias, GELU,
     fp32 residual, fp16 out + fp16 copy) for every tile shape."""
@@ -83,7 +87,9 @@ def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
                                             (1, 16, 96), (1, 17, 768), (2, 18, 256), (1, 19, 136),
                                             (1, 20, 768), (1, 21, 768), (2, 23, 256),
                                             (1, 24, 96), (1, 25, 136), (1, 27, 768),
-                                            (1, 29, 256), (1, 31, 768)])
+                                            (1, 29, 256), (1, 31, 768), (1, 32, 768),
+                                            (2, 34, 256), (1, 35, 136), (1, 36, 768),
+                                            (1, 37, 96)])
 def test_gemm_implicit_conv_split_k(split, tile, Cin):
     from splatt3r_amd import ops, _lib
     B, H, W, Cout, k, stride, pad = 1, 12, 16, 256, 3, 1, 1
