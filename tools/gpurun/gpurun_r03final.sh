@@ -15,7 +15,7 @@ tail -c 1500 gpurun_out/bench.log
 STEPS=24 WIN_MS=60 GAPS=20 bash tools/gpurun/gpurun_prof.sh || exit 1
 PMC_ARGS="--kb 8 --bp 2" bash tools/gpurun/gpurun_traffic.sh || exit 1
 head -40 gpurun_out/traffic/summary.txt
-S3_GEMM_HALO=0 CONFIGS=" " bash tools/gpurun/gpurun_ab.sh
-CONFIGS="--main-priority 0" bash tools/gpurun/gpurun_ab.sh
-timeout -k 10 300 python -u -m tools.bench_conv_parts --tiles 4,3,28,40,41,42,43,45,46,47 --B 2 > gpurun_out/conv_parts.log 2>&1 || { tail -20 gpurun_out/conv_parts.log; exit 1; }
+
+
+timeout -k 10 300 python -u -m tools.bench_conv_parts --tiles 3,4,48,51,52,53 --B 2 > gpurun_out/conv_parts.log 2>&1 || { tail -20 gpurun_out/conv_parts.log; exit 1; }
 grep conv gpurun_out/conv_parts.log
