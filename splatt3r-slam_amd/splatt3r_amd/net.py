@@ -184,9 +184,10 @@ class EncoderPlan:
     def __init__(self, net: "Splatt3RNet", B: int, H: int, W: int):
         cfg, w, dev = net.cfg, net.w, net.device
         # batch-invariant: image b of a B-image replay equals a one-image
-        # replay bit for bit (ops.gemm batch=B), so the encoder lookahead
-        # batch never changes a frame's features
-        gemm = functools.partial(ops.gemm, batch=B)
+        # replay bit for bit (ops.gemm batch=B, every encoder plan tuned in
+        # the reduction class chosen for net.class_batch[0] images), so the
+        # encoder lookahead batch never changes a frame's features
+        gemm = functools.partial(ops.gemm, batch=B, class_batch=net.class_batch[0])
         E, p = cfg.enc_dim, cfg.patch
         ht, wt = H // p, W // p
         N = ht * wt
@@ -252,11 +253,13 @@ class PairPlan:
     def __init__(self, net: "Splatt3RNet", Bp: int, H: int, W: int, keep_tokens=False,
                  batch_invariant=False):
         cfg, w, dev = net.cfg, net.w, net.device
-        # batch_invariant: every GEMM tuned within the reduction class of the
-        # Bp = 1 shape's choice (ops.reduction_class), so each pair's outputs
-        # equal a Bp = 1 replay bit for bit (the tracker's decode-ahead)
+        # batch_invariant: every GEMM tuned within the reduction class
+        # (ops.reduction_class) chosen for net.class_batch[1] pairs, whatever
+        # Bp, so each pair's outputs equal a Bp = 1 replay bit for bit (the
+        # tracker's decode-ahead)
         self.batch_invariant = batch_invariant
-        self._gemm = functools.partial(ops.gemm, batch=Bp if batch_invariant else 1)
+        self._gemm = (functools.partial(ops.gemm, batch=Bp, class_batch=net.class_batch[1])
+                      if batch_invariant else ops.gemm)
         E, D, p = cfg.enc_dim, cfg.dec_dim, cfg.patch
         ht, wt = H // p, W // p
         N = ht * wt
@@ -550,8 +553,12 @@ class Splatt3RNet:
     (dust3r/dust3r/model.py:121-193) plus fused fast paths."""
 
     def __init__(self, cfg: NetConfig = FULL, state_dict=None, seed: int = 1234, device="cuda",
-                 graphs: bool = True, symmetric: bool = False):
+                 graphs: bool = True, symmetric: bool = False, class_batch=(8, 2)):
         self.cfg = cfg
+        # (encoder images, pairs): the batch whose shapes pick the GEMM
+        # reduction classes of the batch-invariant plans -- the frame loop's
+        # encoder lookahead batch and decode-ahead pair replay
+        self.class_batch = tuple(class_batch)
         self.device = torch.device(device)
         sd = state_dict if state_dict is not None else prng_state_dict(cfg, seed, self.device)
         if symmetric:

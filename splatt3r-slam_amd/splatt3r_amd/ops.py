@@ -323,6 +323,12 @@ def _tuned(a, A, B, bias, rope, rope_pos, split_ok, like=None):
             r = scratch((a.M - 1) * a.ldc2 + a.N, torch.float16)
             keep.append(r)
             t.C2[i] = r.data_ptr()
+        if a.rope_pos[i]:
+            # (y, x) token positions: zeros are in range for any M (the
+            # class_batch shape has more rows than the plan's own pos)
+            r = torch.zeros(int(a.M) * 2, device=dev, dtype=torch.int64)
+            keep.append(r)
+            t.rope_pos[i] = r.data_ptr()
     L = _lib.lib()
     st = _lib.stream(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -369,16 +375,21 @@ def _tuned(a, A, B, bias, rope, rope_pos, split_ok, like=None):
 
 def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1=None,
          ldr1=0, R2=None, ldr2=0, C2=None, ldc2=0, conv=None, store=None, split_k=None,
-         tile=0, rope=None, rope_pos=None, rope_ncols=0, tail=None, batch=1) -> Call:
+         tile=0, rope=None, rope_pos=None, rope_ncols=0, tail=None, batch=1,
+         class_batch=None) -> Call:
     """Grouped GEMM: A, B, C, bias, R1, R2, C2 are lists (one entry per group)
     of tensors / raw pointers.  conv = dict(H, W, C, k, stride, pad, oH, oW,
     relu_in) switches A to implicit im2col of an NHWC image.  store =
     ("convt"|"pixshuf", sH, sW, s, Cout).  tail = (W [tail_n, N] fp16, bias fp32,
     out fp32 [M, ld], tail_n, ld) lists per group: the fused 1x1 tail (s3n.h);
-    C entries may then be None.  batch = b > 1: the M rows are b items of
-    M / b rows (a pair plan's Bp pairs); the launch is tuned among the
-    configurations of the same reduction_class as the one-item shape's
-    choice, so every item's rows equal the one-item launch bit for bit."""
+    C entries may then be None.  batch = b: the M rows are b items of
+    M / b rows (a pair plan's Bp pairs).  With class_batch = h (batch-
+    invariant plans) the launch is tuned among the configurations of one
+    reduction_class, the class of the unconstrained choice for h items (the
+    batch the frame loop mostly replays), so every plan of the same one-item
+    shape -- whatever its b -- computes each item's rows bit for bit alike.
+    With class_batch None and b > 1 the class is the one-item shape's
+    choice."""
     a = GemmArgs()
     groups = len(A)
     a.M, a.N, a.K, a.groups = int(M), int(N), int(K), groups
@@ -432,11 +443,18 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
     if TUNE and not tile and not TILE_OVERRIDE and torch.cuda.is_available():
         split_ok = split_k is None and rope_pos is None
         like = None
-        if batch > 1 and a.M % batch == 0:
+        if a.M % max(1, batch) == 0 and (batch > 1 or (class_batch or 1) > 1):
             a1 = GemmArgs.from_buffer_copy(a)
-            a1.M = a.M // batch
+            a1.M = a.M // max(1, batch) * (class_batch or 1)
             like = _tuned(a1, A, B, bias, rope, rope_pos, split_ok)
-        a.tile, a.split_k = _tuned(a, A, B, bias, rope, rope_pos, split_ok, like)
+        if like is not None and a1.M == a.M:
+            a.tile, a.split_k = like
+        else:
+            a.tile, a.split_k = _tuned(a, A, B, bias, rope, rope_pos, split_ok, like)
+            if like is not None and (reduction_class(a.K, a.tile, a.split_k)
+                                     != reduction_class(a.K, *like)):
+                raise RuntimeError(f"s3n_gemm {a.M}x{a.N}x{a.K}: no launch in the reduction "
+                                   f"class of tile {like[0]} split {like[1]}")
     ws = None
     if a.split_k > 1:
         nbytes = _lib.lib().s3n_gemm_workspace_bytes(ctypes.byref(a))
