@@ -172,6 +172,17 @@ _TUNE_CACHE: dict = {}
 TUNE_LOG = os.environ.get("S3_GEMM_TUNE_LOG", "0") == "1"
 TUNE_COLD = os.environ.get("S3_GEMM_TUNE_COLD", "1") == "1"
 _FLUSH: dict = {}
+# Tuning database: choices of an earlier process, keyed like _TUNE_CACHE and
+# stamped with a digest of the tile tables below (a changed table voids the
+# file).  S3_GEMM_TUNE_DB = path ("" = none; default tune_gfx950.json beside
+# this module); shapes it lacks are timed as usual, so a run with the file
+# makes the same launch choices -- and computes the same bits -- as the run
+# that wrote it.  S3_GEMM_TUNE_DB_SAVE = path: write this process's choices
+# (merged over the loaded file) there at exit.
+TUNE_DB = os.environ.get("S3_GEMM_TUNE_DB",
+                         os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune_gfx950.json"))
+TUNE_DB_SAVE = os.environ.get("S3_GEMM_TUNE_DB_SAVE", "")
+_DB_STATE = {"loaded": False, "entries": {}}
 
 
 def _flush_buffer(dev):
@@ -225,6 +236,58 @@ if os.environ.get("S3_GEMM_HALO", "1") == "0":
     _EXCLUDED |= _HALO
 
 
+def _db_digest() -> str:
+    import hashlib
+    tables = (sorted(_TILE_SHAPES.items()), sorted(_TILE_RED.items()), sorted(_REGS_EPILOGUE),
+              sorted(_HALO), sorted(_TAIL_OK))
+    return hashlib.sha1(repr(tables).encode()).hexdigest()[:16]
+
+
+def _db_decode(k):
+    like = k[-1]
+    return tuple(k[:-1]) + (tuple(like) if like is not None else None,)
+
+
+def _db_load():
+    """Fill _TUNE_CACHE from TUNE_DB once (cold-tuned entries only, none whose
+    tile this process excludes)."""
+    if _DB_STATE["loaded"]:
+        return
+    _DB_STATE["loaded"] = True
+    if not TUNE_DB or not TUNE_COLD or not os.path.isfile(TUNE_DB):
+        return
+    import json
+    with open(TUNE_DB) as f:
+        db = json.load(f)
+    if db.get("digest") != _db_digest():
+        if TUNE_LOG:
+            print(f"[gemm-tune] {TUNE_DB}: tile tables changed, database ignored", flush=True)
+        return
+    for k, v in db["entries"]:
+        key, val = _db_decode(k), (int(v[0]), int(v[1]))
+        if val[0] in _EXCLUDED or (val[0] and val[0] not in _TILE_SHAPES):
+            continue
+        _DB_STATE["entries"][key] = val
+        _TUNE_CACHE.setdefault(key, val)
+
+
+def save_tune_db(path: str):
+    """Write the loaded database merged with this process's choices."""
+    import json
+    merged = dict(_DB_STATE["entries"])
+    merged.update(_TUNE_CACHE)
+    entries = [[list(k[:-1]) + [list(k[-1]) if k[-1] is not None else None], list(v)]
+               for k, v in merged.items()]
+    entries.sort(key=repr)
+    with open(path, "w") as f:
+        json.dump({"digest": _db_digest(), "arch": "gfx950", "entries": entries}, f)
+
+
+if TUNE_DB_SAVE:
+    import atexit
+    atexit.register(lambda: save_tune_db(TUNE_DB_SAVE))
+
+
 def reduction_class(K: int, tile: int, split_k: int):
     """What fixes the summation order of every output element of a launch:
     the MFMA shape, the K-group interleave (K-groups take every KG-th K
@@ -275,6 +338,7 @@ def _tune_candidates(a, split_ok, like=None):
 
 
 def _tuned(a, A, B, bias, rope, rope_pos, split_ok, like=None):
+    _db_load()
     key = _tune_key(a) + (like,)
     if key in _TUNE_CACHE:
         return _TUNE_CACHE[key]

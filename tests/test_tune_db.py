@@ -1,0 +1,69 @@
+"""GEMM tuning database (ops.TUNE_DB): round trip, tile-table digest, the
+exclusion filter, and that a shipped database matches this tree's tables."""
+import json
+import os
+
+import pytest
+
+from splatt3r_amd import ops
+
+
+@pytest.fixture
+def fresh_db_state(monkeypatch):
+    monkeypatch.setattr(ops, "_TUNE_CACHE", {})
+    monkeypatch.setattr(ops, "_DB_STATE", {"loaded": False, "entries": {}})
+    monkeypatch.setattr(ops, "TUNE_COLD", True)
+    yield
+
+
+def _reload(monkeypatch, path):
+    monkeypatch.setattr(ops, "TUNE_DB", str(path))
+    monkeypatch.setattr(ops, "_TUNE_CACHE", {})
+    monkeypatch.setattr(ops, "_DB_STATE", {"loaded": False, "entries": {}})
+    ops._db_load()
+    return dict(ops._TUNE_CACHE)
+
+
+def test_round_trip_keeps_keys_and_like(tmp_path, monkeypatch, fresh_db_state):
+    k1 = (768, 1024, 4096, 1, True, False, None)
+    k2 = (6144, 1024, 4096, 1, True, False, (4, 1))
+    ops._TUNE_CACHE.update({k1: (4, 1), k2: (36, 1)})
+    p = tmp_path / "db.json"
+    ops.save_tune_db(str(p))
+    assert _reload(monkeypatch, p) == {k1: (4, 1), k2: (36, 1)}
+
+
+def test_changed_tile_tables_void_the_file(tmp_path, monkeypatch, fresh_db_state):
+    p = tmp_path / "db.json"
+    p.write_text(json.dumps({"digest": "not-this-tree", "entries": [[[1, 2, 3, None], [4, 1]]]}))
+    assert _reload(monkeypatch, p) == {}
+
+
+def test_excluded_and_unknown_tiles_are_retuned(tmp_path, monkeypatch, fresh_db_state):
+    p = tmp_path / "db.json"
+    ents = [[[1, 1, 1, None], [51, 1]], [[2, 2, 2, None], [999, 1]], [[3, 3, 3, None], [32, 2]]]
+    p.write_text(json.dumps({"digest": ops._db_digest(), "entries": ents}))
+    monkeypatch.setattr(ops, "_EXCLUDED", set(ops._HALO))
+    assert _reload(monkeypatch, p) == {(3, 3, 3, None): (32, 2)}
+
+
+def test_warm_tuning_policy_ignores_the_cold_database(tmp_path, monkeypatch, fresh_db_state):
+    p = tmp_path / "db.json"
+    p.write_text(json.dumps({"digest": ops._db_digest(), "entries": [[[3, 3, 3, None], [32, 1]]]}))
+    monkeypatch.setattr(ops, "TUNE_COLD", False)
+    assert _reload(monkeypatch, p) == {}
+
+
+def test_shipped_database_matches_this_tree():
+    path = os.path.join(os.path.dirname(ops.__file__), "tune_gfx950.json")
+    if not os.path.isfile(path):
+        pytest.skip("no shipped tuning database")
+    with open(path) as f:
+        db = json.load(f)
+    assert db["digest"] == ops._db_digest()
+    for k, v in db["entries"]:
+        assert v[0] == 0 or v[0] in ops._TILE_SHAPES
+        if k[-1] is not None and v[0] and k[-1][0]:
+            # a batch-invariant plan's choice is in the class of its like
+            kk = k[2]
+            assert ops.reduction_class(kk, *v) == ops.reduction_class(kk, *k[-1])
