@@ -150,13 +150,13 @@ __global__ void __launch_bounds__(kThreads) k_upsample2x(UpP p) {
 }
 
 // ------------------------------------------------------ postprocess -------
-__global__ void __launch_bounds__(kThreads)
-k_gauss_post(int64_t n, const float* __restrict__ pts, int ldp, const float* __restrict__ feat,
-             const float* __restrict__ gs, int ldg, int use_offsets, float* pts3d, float* conf,
-             float* desc, f16* desc16, float* desc_conf, float* scales, float* rot, float* sh,
-             float* opac, float* means) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// pts3d / conf, desc_conf and the Gaussian parameters of row i (the
+// descriptor normalisation is the caller's: in registers or through LDS)
+__device__ __forceinline__ void gauss_post_row(int64_t i, const float* __restrict__ pts, int ldp,
+                                               float f24, const float* __restrict__ gs, int ldg,
+                                               int use_offsets, float* pts3d, float* conf,
+                                               float* desc_conf, float* scales, float* rot,
+                                               float* sh, float* opac, float* means) {
   const float* P = pts + i * ldp;
   // reg_dense_depth, mode exp: xyz / clip(|xyz|, 1e-8) * expm1(|xyz|)
   const float x = P[0], y = P[1], z = P[2];
@@ -166,18 +166,7 @@ k_gauss_post(int64_t n, const float* __restrict__ pts, int ldp, const float* __r
   const float px = x / dc * e, py = y / dc * e, pz = z / dc * e;
   pts3d[i * 3 + 0] = px; pts3d[i * 3 + 1] = py; pts3d[i * 3 + 2] = pz;
   conf[i] = 1.0f + expf(P[3]);  // reg_dense_conf exp: vmin + exp(x).clip(max=inf)
-  const float* F = feat + i * 25;
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 24; ++k) s += F[k] * F[k];
-  const float inv = 1.0f / sqrtf(s);
-#pragma unroll
-  for (int k = 0; k < 24; ++k) {
-    const float v = F[k] * inv;
-    desc[i * 24 + k] = v;
-    if (desc16) desc16[i * 24 + k] = (f16)v;
-  }
-  desc_conf[i] = 1.0f + expf(F[24]);
+  desc_conf[i] = 1.0f + expf(f24);
   const float* G = gs + i * ldg;
   // reg_dense_offsets(shift 6): xyz/clip(d,1e-8) * (exp(d-6) - exp(-6))
   const float ox = G[0], oy = G[1], oz = G[2];
@@ -196,6 +185,45 @@ k_gauss_post(int64_t n, const float* __restrict__ pts, int ldp, const float* __r
     means[i * 3 + 2] = pz + oz / odc * of;
   } else {
     means[i * 3 + 0] = px; means[i * 3 + 1] = py; means[i * 3 + 2] = pz;
+  }
+}
+
+// One row per thread, the workgroup's 256 descriptor rows (25 floats: 24 +
+// desc_conf logit) moved through LDS: read as one coalesced range,
+// normalised in registers from the thread's own row (LDS stride 25 is
+// conflict-free), written back into the slot and stored as coalesced desc /
+// desc16 ranges.  A row per lane straight from memory (96-100 B stride)
+// touches ~50 cache lines per load / store instruction.
+__global__ void __launch_bounds__(kThreads)
+k_gauss_post(int64_t n, const float* __restrict__ pts, int ldp, const float* __restrict__ feat,
+             const float* __restrict__ gs, int ldg, int use_offsets, float* pts3d, float* conf,
+             float* desc, f16* desc16, float* desc_conf, float* scales, float* rot, float* sh,
+             float* opac, float* means) {
+  __shared__ float s_f[kThreads * 25];
+  const int64_t r0 = (int64_t)blockIdx.x * kThreads;
+  const int rows = (int)min((int64_t)kThreads, n - r0);
+  const int t = threadIdx.x;
+  for (int e = t; e < rows * 25; e += kThreads) s_f[e] = feat[r0 * 25 + e];
+  __syncthreads();
+  float F[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) F[k] = t < rows ? s_f[t * 25 + k] : 1.0f;
+  __syncthreads();
+  if (t < rows) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 24; ++k) s += F[k] * F[k];
+    const float inv = 1.0f / sqrtf(s);
+#pragma unroll
+    for (int k = 0; k < 24; ++k) s_f[t * 25 + k] = F[k] * inv;
+    gauss_post_row(r0 + t, pts, ldp, F[24], gs, ldg, use_offsets, pts3d, conf, desc_conf,
+                   scales, rot, sh, opac, means);
+  }
+  __syncthreads();
+  for (int e = t; e < rows * 24; e += kThreads) {
+    const float v = s_f[(e / 24) * 25 + e % 24];
+    desc[r0 * 24 + e] = v;
+    if (desc16) desc16[r0 * 24 + e] = (f16)v;
   }
 }
 

@@ -341,16 +341,20 @@ def test_prng_fill_bitexact_vs_numpy():
     np.testing.assert_array_equal(t.cpu().numpy(), prng_numpy(seed, 100_003, 0.0541, 0.0))
 
 
-def test_gaussian_postprocess_vs_torch():
+@pytest.mark.parametrize("n", [5000, 1, 256, 257])
+def test_gaussian_postprocess_vs_torch(n):
     from splatt3r_amd import ops, _lib
-    n = 5000
     pts = _rand(n, 16, dtype=torch.float32, seed=18)
     feat = _rand(n, 25, dtype=torch.float32, seed=19)
     gs = _rand(n, 16, dtype=torch.float32, seed=20)
     out = {k: torch.empty(n, c, device="cuda").squeeze(-1) for k, c in
            dict(pts3d=3, conf=1, desc=24, desc_conf=1, scales=3, rotations=4, sh=3,
                 opacities=1, means=3).items()}
-    ops.gaussian_postprocess(n, pts, 16, feat, gs, 16, True, out)(_lib.stream())
+    desc16 = torch.full((n + 1, 24), 7.0, device="cuda", dtype=torch.float16)
+    ops.gaussian_postprocess(n, pts, 16, feat, gs, 16, True, out, desc16=desc16)(_lib.stream())
+    # the fp16 copy is the fp32 descriptor rounded, and nothing past row n
+    assert torch.equal(desc16[:n], out["desc"].half())
+    assert bool((desc16[n] == 7.0).all())
     xyz = pts[:, :3]
     d = xyz.norm(dim=-1, keepdim=True)
     p3 = xyz / d.clip(min=1e-8) * torch.expm1(d)
