@@ -118,18 +118,22 @@ struct UpP {
   int B, H, W, C, oh, ow;
 };
 
+// Idx = uint32_t when B * oh * ow * C/8 < 2^31 (every frame-loop shape):
+// the per-thread index split is then 32-bit division, not the ~4x longer
+// 64-bit sequences.
+template <typename Idx>
 __global__ void __launch_bounds__(kThreads) k_upsample2x(UpP p) {
   const int g = blockIdx.y;
   const int OH = 2 * p.H, OW = 2 * p.W, C8 = p.C / 8;
-  const int64_t total = (int64_t)p.B * p.oh * p.ow * C8;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const Idx total = (Idx)p.B * p.oh * p.ow * C8;
+  const Idx i = (Idx)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int c8 = (int)(i % C8);
-  int64_t t = i / C8;
-  const int ox = (int)(t % p.ow);
-  t /= p.ow;
-  const int oy = (int)(t % p.oh);
-  const int b = (int)(t / p.oh);
+  const int c8 = (int)(i % (Idx)C8);
+  Idx t = i / (Idx)C8;
+  const int ox = (int)(t % (Idx)p.ow);
+  t /= (Idx)p.ow;
+  const int oy = (int)(t % (Idx)p.oh);
+  const int b = (int)(t / (Idx)p.oh);
   const float sh = OH > 1 ? (float)(p.H - 1) / (float)(OH - 1) : 0.f;
   const float sw = OW > 1 ? (float)(p.W - 1) / (float)(OW - 1) : 0.f;
   const float fy = sh * oy, fx = sw * ox;
@@ -312,7 +316,10 @@ int s3n_upsample2x(int groups, const void* const* in, void* const* out, int B, i
   }
   const int64_t total = (int64_t)B * oh * ow * (C / 8);
   dim3 grid((unsigned)s3::cdiv(total, kThreads), (unsigned)groups);
-  k_upsample2x<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+  if (total < ((int64_t)1 << 31))
+    k_upsample2x<uint32_t><<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+  else
+    k_upsample2x<int64_t><<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }
