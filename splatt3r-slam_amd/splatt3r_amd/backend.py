@@ -41,7 +41,7 @@ class Backend:
         # the retrieval checkpoint is not available offline: synthetic
         # weights of its shapes unless a database is passed in
         self.retrieval = retrieval if retrieval is not None else RetrievalDatabase(
-            synthetic_retrieval_weights(self.device), self.device)
+            synthetic_retrieval_weights(self.device), device=self.device)
         self.stats = dict(optimized=0, edges=0, reloc_attempts=0, reloc_success=0,
                           retrieval_candidates=0, last_reloc_candidates=[])
         self._q = None

@@ -78,9 +78,12 @@ class Frame:
             if s > self.score:
                 self.X_canon, self.C, self.N, self.score = X.clone(), C.clone(), 1, s
         elif mode == "indep_conf":
+            # the reference's masked in-place writes (frame.py:80-83) as new
+            # tensors: a backend snapshot (Keyframes._snapshot) taken before
+            # this update keeps reading the old storage on its own stream
             m = C > self.C
-            self.X_canon[m.repeat(1, 3)] = X[m.repeat(1, 3)]
-            self.C[m] = C[m]
+            self.X_canon = torch.where(m, X, self.X_canon)
+            self.C = torch.where(m, C, self.C)
             self.N = 1
         elif mode == "weighted_pointmap":
             self.X_canon = (self.C * self.X_canon + C * X) / (self.C + C)

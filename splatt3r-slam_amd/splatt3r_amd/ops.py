@@ -183,6 +183,10 @@ TUNE_DB = os.environ.get("S3_GEMM_TUNE_DB",
                          os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune_gfx950.json"))
 TUNE_DB_SAVE = os.environ.get("S3_GEMM_TUNE_DB_SAVE", "")
 _DB_STATE = {"loaded": False, "entries": {}}
+# Bumped whenever a net_gemm_t*.hip launch precondition or kernel changes the
+# meaning of a (tile, split) choice: a database written under another value is
+# ignored (its "abi" field; files without one were written under 1).
+_KERNEL_ABI = 1
 
 
 def _flush_buffer(dev):
@@ -248,9 +252,18 @@ def _db_decode(k):
     return tuple(k[:-1]) + (tuple(like) if like is not None else None,)
 
 
-def _db_load():
+def _device_arch(dev) -> str:
+    """gfx target of `dev` without feature suffixes ("gfx950:sramecc+" -> "gfx950")."""
+    try:
+        return torch.cuda.get_device_properties(dev).gcnArchName.split(":")[0]
+    except Exception:
+        return ""
+
+
+def _db_load(dev=None):
     """Fill _TUNE_CACHE from TUNE_DB once (cold-tuned entries only, none whose
-    tile this process excludes)."""
+    tile this process excludes).  The file is ignored when its tile tables,
+    kernel ABI or gfx target differ from this process's."""
     if _DB_STATE["loaded"]:
         return
     _DB_STATE["loaded"] = True
@@ -259,9 +272,16 @@ def _db_load():
     import json
     with open(TUNE_DB) as f:
         db = json.load(f)
+    why = None
     if db.get("digest") != _db_digest():
+        why = "tile tables changed"
+    elif int(db.get("abi", 1)) != _KERNEL_ABI:
+        why = f"kernel ABI {db.get('abi', 1)} != {_KERNEL_ABI}"
+    elif dev is not None and _device_arch(dev) and db.get("arch") != _device_arch(dev):
+        why = f"written for {db.get('arch')}, device is {_device_arch(dev)}"
+    if why is not None:
         if TUNE_LOG:
-            print(f"[gemm-tune] {TUNE_DB}: tile tables changed, database ignored", flush=True)
+            print(f"[gemm-tune] {TUNE_DB}: {why}, database ignored", flush=True)
         return
     for k, v in db["entries"]:
         key, val = _db_decode(k), (int(v[0]), int(v[1]))
@@ -280,7 +300,8 @@ def save_tune_db(path: str):
                for k, v in merged.items()]
     entries.sort(key=repr)
     with open(path, "w") as f:
-        json.dump({"digest": _db_digest(), "arch": "gfx950", "entries": entries}, f)
+        json.dump({"digest": _db_digest(), "abi": _KERNEL_ABI, "arch": "gfx950",
+                   "entries": entries}, f)
 
 
 if TUNE_DB_SAVE:
@@ -338,11 +359,11 @@ def _tune_candidates(a, split_ok, like=None):
 
 
 def _tuned(a, A, B, bias, rope, rope_pos, split_ok, like=None):
-    _db_load()
+    dev = next(t.device for t in (*A, *B) if isinstance(t, torch.Tensor))
+    _db_load(dev)
     key = _tune_key(a) + (like,)
     if key in _TUNE_CACHE:
         return _TUNE_CACHE[key]
-    dev = next(t.device for t in (*A, *B) if isinstance(t, torch.Tensor))
     g = a.groups
     gen = torch.Generator(device=dev)
     gen.manual_seed(0)

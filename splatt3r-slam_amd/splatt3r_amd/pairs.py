@@ -361,15 +361,18 @@ class PairShard:
 
 
 @torch.inference_mode()
-def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
+def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3, total=None,
+                with_map=True):
     """keyframe-pairs/s of the sharded FactorGraph.add_factors path: rank 0
     creates n_kf keyframes (encoder + broadcast to every rank), then issues
     add_factors over consecutive keyframes plus 3 retrieval-like earlier
     partners per keyframe (main.py:153-173, k = 3), ws * pairs_per_rank pairs
-    per batch; ranks > 0 serve.  Then the global-map refresh on the same
-    keyframes (refresh_map: each keyframe re-inferred against a partner on
-    rank k mod W, gaussians_to_world filters at stride 4, all-gather into
-    every rank's SharedGaussians), timed on its own."""
+    per batch (weak scaling) or `total` pairs whatever ws (strong scaling);
+    ranks > 0 serve.  Then (with_map) the global-map refresh on the same
+    n_kf keyframes, a fixed amount of work at every ws (refresh_map: each
+    keyframe re-inferred against a partner on rank k mod W, gaussians_to_world
+    filters at stride 4, all-gather into every rank's SharedGaussians), timed
+    on its own."""
     from splatt3r_amd.frame import Keyframes, create_frame
     from splatt3r_amd.gaussian_map import SharedGaussians
     from splatt3r_amd.global_opt import FactorGraph
@@ -384,7 +387,7 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
         for d in (2, 3, 4):
             if k - d >= 0:
                 allp.append((k - d, k))
-    total = ws * pairs_per_rank
+    total = ws * pairs_per_rank if total is None else int(total)
     allp = (allp * (total // len(allp) + 1))[:total]
     map_i = list(range(n_kf))
     map_j = [k + 1 if k + 1 < n_kf else k - 1 for k in map_i]
@@ -412,7 +415,8 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
         jj = [p[1] for p in allp]
     else:
         sh.serve()              # receive the keyframes
-    model.encoder.pair_plan(len(shard(allp, ws, rank)), H, W, tag="backend")
+    if shard(allp, ws, rank):
+        model.encoder.pair_plan(len(shard(allp, ws, rank)), H, W, tag="backend")
 
     def pair_batch():
         if rank == 0:
@@ -454,17 +458,18 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3):
         return t
 
     t = timed(pair_batch)
-    t_map = timed(map_refresh)
     out = dict(kf_pairs_per_s=total / t, pairs=total, pairs_per_rank=len(shard(allp, ws, rank)),
                ms_per_batch=t * 1e3,
                path="FactorGraph.add_factors -> PairShard (pair p on rank p mod W) -> "
-                    "gather to rank 0",
-               map_refresh={"ms": t_map * 1e3, "keyframes": n_kf,
-                            "map_gaussians": sh.gmap.n_gaussians,
-                            "path": "PairShard.refresh_map: keyframe k re-inferred on rank k mod "
-                                    "W, gaussians_to_world filters (stride 4, q 0.98, max scale "
-                                    "1, conf 1.5) -> all-gather -> SharedGaussians (opacity "
-                                    "threshold 0 with PRNG weights; reference 0.3)"})
+                    "gather to rank 0")
+    if with_map:
+        t_map = timed(map_refresh)
+        out["map_refresh"] = {"ms": t_map * 1e3, "keyframes": n_kf, "scaling": "strong",
+                              "map_gaussians": sh.gmap.n_gaussians,
+                              "path": "PairShard.refresh_map: keyframe k re-inferred on rank k "
+                                      "mod W, gaussians_to_world filters (stride 4, q 0.98, max "
+                                      "scale 1, conf 1.5) -> all-gather -> SharedGaussians "
+                                      "(opacity threshold 0 with PRNG weights; reference 0.3)"}
     if ws > 1:
         out["keyframe_broadcast_ms"] = t_bc / n_kf * 1e3
     return out

@@ -58,13 +58,91 @@ ASMK_PARAMS = {"build_ivf": {"kernel": {"binary": True}, "ivf": {"use_idf": Fals
 
 @dataclasses.dataclass
 class RetrievalWeights:
-    proj_W: torch.Tensor                    # [dim, 1024] f32 (nn.Linear weight)
-    proj_b: torch.Tensor                    # [dim] f32
+    proj_W: Optional[torch.Tensor]          # [dim, 1024] f32 (last nn.Linear); None = Identity
+    proj_b: Optional[torch.Tensor]          # [dim] f32
     centroids: torch.Tensor                 # [n_clusters, dim] f32 (ASMK codebook)
     prewhiten: Optional[Tuple[torch.Tensor, torch.Tensor]] = None    # (m [1,1024] f64, P f64)
     postwhiten: Optional[Tuple[torch.Tensor, torch.Tensor]] = None   # (m [1,dim] f64, P f64)
     residual: bool = False
     nfeat: int = 300
+    # hidden projector layers before the last Linear (build_projector,
+    # model.py:144-157: Linear -> LayerNorm -> GELU per entry of hdims[:-1]):
+    # [(W [h, d] f32, b [h], ln_w [h], ln_b [h])]
+    hidden: tuple = ()
+    imsize: int = 512
+
+
+def _load_retrieval_ckpt(path: str):
+    """torch.load(weights_only=True) of the retrieval .pth (processor.py:66-70):
+    the training Namespace under 'args' is the one non-tensor global it holds
+    and is allowed explicitly; nothing else in the file is executed."""
+    import argparse
+    with torch.serialization.safe_globals([argparse.Namespace]):
+        return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def _codebook_path(modelname: str) -> str:
+    """The ASMK codebook beside the checkpoint (processor.py:80-83 names it
+    <prefix>_codebook.pkl).  A pickle is never loaded here: the centroids
+    array [n_clusters, dim] is read from <prefix>_codebook.npy (numpy,
+    allow_pickle=False) or <prefix>_codebook.safetensors (key 'centroids')."""
+    import os
+    d, b = os.path.split(modelname)
+    stem = os.path.join(d, "_".join(b.split("_")[:-1]) + "_codebook")
+    for ext in (".npy", ".safetensors"):
+        if os.path.isfile(stem + ext):
+            return stem + ext
+    if os.path.isfile(stem + ".pkl"):
+        raise RuntimeError(
+            f"{stem}.pkl is a pickle (the asmk codebook cache); it is not loaded by this build. "
+            f"Export its centroids once, where the asmk package is installed, e.g. "
+            f"numpy.save('{stem}.npy', asmk_method.codebook.centroids), and place the .npy "
+            f"beside the checkpoint")
+    raise FileNotFoundError(f"codebook not found: {stem}.npy / .safetensors")
+
+
+def _load_centroids(path: str) -> torch.Tensor:
+    if path.endswith(".npy"):
+        import numpy as np
+        return torch.from_numpy(np.load(path, allow_pickle=False)).float()
+    from safetensors.torch import load_file
+    return load_file(path)["centroids"].float()
+
+
+def load_retrieval_weights(modelname: str, device="cuda") -> RetrievalWeights:
+    """Retriever.__init__ (processor.py:66-91): the retrieval head's weights
+    from the checkpoint's 'model' state dict (prewhiten.m / .p, projector.*,
+    postwhiten.m / .p; backbone.* ignored, the SLAM model's encoder is the
+    backbone) and its 'args' (hdims, residual, nfeat, featweights), plus the
+    ASMK codebook centroids."""
+    import os
+    if not os.path.isfile(modelname):
+        raise FileNotFoundError(modelname)
+    print(f"Loading retrieval model from {modelname}")
+    ck = _load_retrieval_ckpt(modelname)
+    args, sd = ck["args"], ck["model"]
+    fw = getattr(args, "featweights", "l2norm")
+    if fw != "l2norm":
+        raise NotImplementedError(fw)            # model.py:131-134 raises the same
+    hd = getattr(args, "hdims", "1024")
+    hdims = [int(x) for x in hd.split("_")] if isinstance(hd, str) and len(hd) > 0 else list(hd or [])
+    f32 = lambda k: sd[k].to(device=device, dtype=torch.float32).contiguous()
+    f64 = lambda k: sd[k].to(device=device, dtype=torch.float64).contiguous()
+    white = lambda n: (f64(f"{n}.m"), f64(f"{n}.p")) if f"{n}.p" in sd else None
+    hidden, W, b = [], None, None
+    if hdims:
+        # nn.Sequential: Linear (3 i), LayerNorm (3 i + 1), GELU per hidden dim
+        for i in range(len(hdims) - 1):
+            j = 3 * i
+            hidden.append((f32(f"projector.{j}.weight"), f32(f"projector.{j}.bias"),
+                           f32(f"projector.{j + 1}.weight"), f32(f"projector.{j + 1}.bias")))
+        j = 3 * (len(hdims) - 1)
+        W, b = f32(f"projector.{j}.weight"), f32(f"projector.{j}.bias")
+    cen = _load_centroids(_codebook_path(modelname)).to(device)
+    return RetrievalWeights(W, b, cen, white("prewhiten"), white("postwhiten"),
+                            residual=bool(getattr(args, "residual", False)),
+                            nfeat=getattr(args, "nfeat", 300), hidden=tuple(hidden),
+                            imsize=int(getattr(args, "imsize", 512)))
 
 
 def _chk(t, dtype, name):
@@ -204,7 +282,15 @@ class RetrievalDatabase:
     """retrieval_database.py:9-134: prep_features / quantize_custom on the
     device kernels above, the ASMK inverted file restated on the device."""
 
-    def __init__(self, weights: RetrievalWeights, device="cuda"):
+    def __init__(self, modelname, backbone=None, device="cuda"):
+        """retrieval_database.py:9-22: `modelname` is the retrieval checkpoint
+        path (weights + ASMK codebook beside it, load_retrieval_weights) or
+        already-loaded RetrievalWeights; `backbone` is the SLAM model's
+        encoder (load_retriever passes model.encoder), whose features the
+        caller hands to update() (frame.feat)."""
+        weights = (modelname if isinstance(modelname, RetrievalWeights)
+                   else load_retrieval_weights(str(modelname), device))
+        self.backbone = backbone
         self.w = weights
         self.kf_counter = 0
         self.kf_ids = []
@@ -223,7 +309,16 @@ class RetrievalDatabase:
         x = backbone_feat.float().contiguous()
         if w.prewhiten is not None:
             x = whiten(x, *w.prewhiten)
-        proj = linear(x, w.proj_W, w.proj_b, w.residual)
+        h = x
+        for Wh, bh, lw, lb in w.hidden:      # build_projector's hidden layers
+            h = linear(h, Wh, bh)
+            h = torch.nn.functional.gelu(torch.nn.functional.layer_norm(h, h.shape[-1:], lw, lb))
+        if w.proj_W is None:                 # hdims empty: nn.Identity
+            proj = h + x if w.residual else h
+        elif w.residual and w.hidden:
+            proj = linear(h, w.proj_W, w.proj_b) + x
+        else:
+            proj = linear(h, w.proj_W, w.proj_b, w.residual)
         post = whiten(proj, *w.postwhiten) if w.postwhiten is not None else proj
         feats, _, _ = how_select_local(post, proj, w.nfeat)
         return feats

@@ -43,7 +43,35 @@ from splatt3r_amd.splatt3r_utils import (_sim3_to_4x4, splatt3r_inference_mono,
                                          splatt3r_render, world_records)
 from splatt3r_amd.tracker import FrameTracker
 
-__all__ = ["Frontend", "should_append_gaussians"]
+__all__ = ["Frontend", "should_append_gaussians", "lookahead_batches"]
+
+
+def _clear_ahead_slot(model):
+    enc = getattr(model, "encoder", None)
+    if enc is not None and getattr(enc, "_ahead_slot", None) is not None:
+        enc._ahead_slot = None
+
+
+def lookahead_batches(i: int, next_enc: int, n_next: int, enc_batch: int, enc_ahead=None):
+    """The encoder batches frame i queues: [(first frame, count)].
+
+    `next_enc` is the lowest frame index not yet queued, `n_next` the number
+    of lookahead images handed to the step (frames i + 1 .. i + n_next).
+    Frames are queued in batches of at most `enc_batch` until every frame up
+    to i + enc_ahead (None: i + 1) is queued; the last batch is partial when
+    fewer images are available.  Pure host logic: Frontend._step and the
+    bench's timed-region plan (bench.py plan_encodes) share it."""
+    kb = max(1, int(enc_batch))
+    want = i + max(1, enc_ahead or 1)
+    out = []
+    while next_enc <= want:
+        off = next_enc - (i + 1)
+        c = min(kb, n_next - off)
+        if off < 0 or c <= 0:
+            break
+        out.append((next_enc, c))
+        next_enc += c
+    return out
 
 
 class _RenderTicket:
@@ -84,12 +112,20 @@ class _RenderWorker:
     idle during the tracking thread's wait, and the worker's Python competes
     for the GIL -- so it is opt-in (Frontend(render_async=True))."""
 
+    DECISION_TIMEOUT_S = 60.0
+
     def __init__(self, device):
         self.stream = torch.cuda.Stream(device=device)
         self.q: queue.Queue = queue.Queue()
         self.error = None
+        self.timeouts = 0          # renders dropped for want of a decision (drain raises)
         self.thread = threading.Thread(target=self._loop, name="s3-render", daemon=True)
         self.thread.start()
+
+    def close(self):
+        """Stop the worker thread after the queued renders."""
+        self.q.put(None)
+        self.thread.join()
 
     def _loop(self):
         while True:
@@ -103,9 +139,11 @@ class _RenderWorker:
                     img = fn()
                     # the tracker decides right after its GN sync; a decision
                     # that never comes (an exception on the tracking thread)
-                    # drops the render instead of blocking the queue
-                    if not ticket.decided.wait(60.0):
+                    # drops the render instead of blocking the queue, and is
+                    # counted (Frontend.drain raises)
+                    if not ticket.decided.wait(self.DECISION_TIMEOUT_S):
                         img = None
+                        self.timeouts += 1
                     if ticket.finish is not None and img is not None:
                         ticket.finish(img)
             except BaseException as e:          # surfaced by drain()
@@ -193,7 +231,11 @@ class Frontend:
         # keyframe in the same Bp = 2 replay; the result is used when that
         # frame is tracked against the same keyframe
         self.decode_ahead = decode_ahead
-        # render_async: splatt3r_render + its PNG write / read-back on a
+        # a decode-ahead slot left on the shared model by an earlier session
+        # (frame ids restart, the allocator reuses addresses) is never valid
+        # for this one
+        _clear_ahead_slot(model)
+        # render_async:splatt3r_render + its PNG write / read-back on a
         # worker thread and stream (_RenderWorker); drain() waits for them
         self._rworker = _RenderWorker(device) if render_async and render else None
         self._tickets: list = []
@@ -285,9 +327,26 @@ class Frontend:
         for t in self._tickets:
             t.done.wait()
         self._tickets = []
-        if self._rworker is not None and self._rworker.error is not None:
-            e, self._rworker.error = self._rworker.error, None
-            raise e
+        if self._rworker is not None:
+            if self._rworker.timeouts:
+                n, self._rworker.timeouts = self._rworker.timeouts, 0
+                raise RuntimeError(f"{n} render(s) dropped: no keep/drop decision within "
+                                   f"{_RenderWorker.DECISION_TIMEOUT_S} s")
+            if self._rworker.error is not None:
+                e, self._rworker.error = self._rworker.error, None
+                raise e
+
+    def close(self):
+        """End the session: wait for queued renders, stop the render worker
+        thread and release the decode-ahead slot this session left on the
+        shared model (its views keep the pair plan's outputs alive)."""
+        try:
+            self.drain()
+        finally:
+            if self._rworker is not None:
+                self._rworker.close()
+                self._rworker = None
+            _clear_ahead_slot(self.model)
 
     @property
     def last_render(self):
@@ -488,15 +547,10 @@ class Frontend:
             # images (lookahead); up to enc_batch of them are encoded together,
             # until frames up to i + enc_ahead are queued
             nxt = list(next_img) if isinstance(next_img, (list, tuple)) else [next_img]
-            kb = max(1, self.enc_batch)
-            want = i + max(1, self.enc_ahead or 1)
-            while self._next_enc <= want:
-                off = self._next_enc - (i + 1)
-                imgs = nxt[off:off + kb]
-                if not imgs:
-                    break
-                pending.append((self._next_enc, imgs))
-                self._next_enc += len(imgs)
+            for s, c in lookahead_batches(i, self._next_enc, len(nxt), self.enc_batch,
+                                          self.enc_ahead):
+                pending.append((s, nxt[s - (i + 1):s - (i + 1) + c]))
+                self._next_enc = s + c
             # late prefetch: a tracked frame queues the next encoder after
             # its GN sync, so the encoder fills the device while the host
             # issues the post-GN launches (pose update, map, render)

@@ -72,6 +72,18 @@ def load_splatt3r(path=None, device="cuda", cfg=None, seed: int = 1234, graphs: 
     return Splatt3RModel(net, DecoderSplattingCUDA([0.0, 0.0, 0.0]).to(device))
 
 
+def load_retriever(splatt3r_model, retriever_path=None, device="cuda"):
+    """splatt3r_utils.py:69-89: the keyframe retrieval database over the
+    SLAM model's encoder, from the MASt3R retrieval checkpoint (default path
+    as the reference) and the ASMK codebook beside it (.npy / .safetensors;
+    retrieval_database.load_retrieval_weights)."""
+    from splatt3r_amd.retrieval_database import RetrievalDatabase
+    retriever_path = (
+        "checkpoints/MASt3R_ViTLarge_BaseDecoder_512_catmlpdpt_metric_retrieval_trainingfree.pth"
+        if retriever_path is None else retriever_path)
+    return RetrievalDatabase(retriever_path, backbone=splatt3r_model.encoder, device=device)
+
+
 # ------------------------------------------------------------- inference ---
 @torch.inference_mode()
 def decoder(model, feat1, feat2, pos1, pos2, shape1, shape2):

@@ -200,7 +200,7 @@ def test_hip_retrieval_database_update_matches_oracle():
     g = torch.Generator().manual_seed(3)
     cen = torch.nn.functional.normalize(torch.randn(C, D, generator=g), dim=1)
     W = RetrievalWeights(torch.eye(D, 1024)[:D].cuda(), torch.zeros(D).cuda(), cen.cuda(), nfeat=100)
-    db = RetrievalDatabase(W, "cuda")
+    db = RetrievalDatabase(W, device="cuda")
     ref = RetrievalDBRef(cen.numpy())
     places = [torch.nn.functional.normalize(torch.randn(100, D, generator=g), dim=1)
               for _ in range(5)]
@@ -223,3 +223,122 @@ def test_hip_retrieval_database_update_matches_oracle():
         assert inds == want, (t, inds, want)
         got_all.append(inds)
     assert got_all[5][0] == 2 and got_all[6][0] == 0
+
+
+# ------------------------------------------- checkpoint-backed constructor ---
+def _write_retrieval_ckpt(tmp_path, hdims="1024", residual=False, C=64, seed=5):
+    """A file with the layout of the MASt3R retrieval checkpoint
+    (processor.py:66-78: {'args': Namespace, 'model': state dict without the
+    frozen backbone}) and the codebook beside it as .npy (the reference's
+    <prefix>_codebook.pkl is a pickle, not read by this build)."""
+    import argparse
+    g = torch.Generator().manual_seed(seed)
+    dims = [int(x) for x in hdims.split("_")] if hdims else []
+    sd = {"prewhiten.m": torch.randn(1, 1024, generator=g, dtype=torch.float64) * 0.1,
+          "prewhiten.p": torch.randn(1024, 1024, generator=g, dtype=torch.float64) / 32}
+    d = 1024
+    for i, h in enumerate(dims):
+        sd[f"projector.{3 * i}.weight"] = torch.randn(h, d, generator=g) / d ** 0.5
+        sd[f"projector.{3 * i}.bias"] = torch.randn(h, generator=g) * 0.01
+        if i < len(dims) - 1:
+            sd[f"projector.{3 * i + 1}.weight"] = 1 + 0.1 * torch.randn(h, generator=g)
+            sd[f"projector.{3 * i + 1}.bias"] = 0.1 * torch.randn(h, generator=g)
+        d = h
+    sd["postwhiten.m"] = torch.randn(1, d, generator=g, dtype=torch.float64) * 0.1
+    sd["postwhiten.p"] = torch.randn(d, d, generator=g, dtype=torch.float64) / d ** 0.5
+    args = argparse.Namespace(pretrained="x", freeze_backbone=1, prewhiten=-1, hdims=hdims,
+                              residual=residual, postwhiten=-1, featweights="l2norm", nfeat=300,
+                              nclusters=C, imsize=512)
+    path = tmp_path / "MASt3R_ViTLarge_BaseDecoder_512_catmlpdpt_metric_retrieval_trainingfree.pth"
+    torch.save({"args": args, "model": sd}, str(path))
+    cen = torch.nn.functional.normalize(torch.randn(C, d, generator=g), dim=1).numpy()
+    np.save(str(tmp_path / "MASt3R_ViTLarge_BaseDecoder_512_catmlpdpt_metric_retrieval_codebook.npy"),
+            cen)
+    return str(path), sd, cen
+
+
+def test_retrieval_checkpoint_maps_onto_weights(tmp_path):
+    from splatt3r_amd.retrieval_database import load_retrieval_weights
+    path, sd, cen = _write_retrieval_ckpt(tmp_path, hdims="512_1024")
+    w = load_retrieval_weights(path, device="cpu")
+    assert torch.equal(w.prewhiten[1], sd["prewhiten.p"]) and w.prewhiten[1].dtype == torch.float64
+    assert torch.equal(w.postwhiten[0], sd["postwhiten.m"])
+    assert len(w.hidden) == 1 and torch.equal(w.hidden[0][0], sd["projector.0.weight"])
+    assert torch.equal(w.hidden[0][2], sd["projector.1.weight"])
+    assert torch.equal(w.proj_W, sd["projector.3.weight"])
+    assert torch.equal(w.centroids, torch.from_numpy(cen))
+    assert w.nfeat == 300 and not w.residual
+
+
+def test_retrieval_codebook_pickle_is_refused(tmp_path):
+    from splatt3r_amd.retrieval_database import load_retrieval_weights
+    path, _, _ = _write_retrieval_ckpt(tmp_path)
+    npy = tmp_path / "MASt3R_ViTLarge_BaseDecoder_512_catmlpdpt_metric_retrieval_codebook.npy"
+    npy.rename(npy.with_suffix(".pkl"))
+    with pytest.raises(RuntimeError, match="pickle"):
+        load_retrieval_weights(path, device="cpu")
+
+
+def test_retrieval_missing_checkpoint_raises(tmp_path):
+    from splatt3r_amd.retrieval_database import load_retrieval_weights
+    with pytest.raises(FileNotFoundError):
+        load_retrieval_weights(str(tmp_path / "nope.pth"), device="cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hdims,residual", [("1024", False), ("1024", True), ("512_1024", False)])
+def test_hip_load_retriever_from_checkpoint_vs_torch(tmp_path, hdims, residual):
+    """load_retriever(model, path) (splatt3r_utils.py:69-89) -> prep_features
+    on the device == RetrievalModel.extract_features_and_attention +
+    how_select_local (model.py:62-157, 89-103) in torch fp64/fp32 on the CPU."""
+    from types import SimpleNamespace
+    from splatt3r_amd.splatt3r_utils import load_retriever
+    path, sd, cen = _write_retrieval_ckpt(tmp_path, hdims=hdims, residual=residual)
+    db = load_retriever(SimpleNamespace(encoder="enc"), path, device="cuda")
+    assert db.backbone == "enc" and db.centroids.shape == (64, 1024)
+    feat = torch.randn(1, 768, 1024, generator=torch.Generator().manual_seed(2))
+    x = R.whiten(feat, sd["prewhiten.m"], sd["prewhiten.p"])
+    h = x
+    dims = hdims.split("_")
+    for i in range(len(dims) - 1):
+        h = torch.nn.functional.linear(h, sd[f"projector.{3 * i}.weight"], sd[f"projector.{3 * i}.bias"])
+        h = torch.nn.functional.gelu(torch.nn.functional.layer_norm(
+            h, h.shape[-1:], sd[f"projector.{3 * i + 1}.weight"], sd[f"projector.{3 * i + 1}.bias"]))
+    j = 3 * (len(dims) - 1)
+    proj = torch.nn.functional.linear(h, sd[f"projector.{j}.weight"], sd[f"projector.{j}.bias"])
+    if residual:
+        proj = proj + x
+    post = R.whiten(proj, sd["postwhiten.m"], sd["postwhiten.p"])
+    attn = proj.norm(dim=-1)
+    got = db.prep_features(feat.cuda()).cpu()
+    ta, ti = torch.topk(attn, 300, dim=1)
+    # rows at the reference's top-300 attention order, up to near-ties
+    sel = post[0, ti[0]]
+    ok = torch.isclose(got[0], sel, rtol=2e-4, atol=2e-4).all(-1)
+    gap = (ta[0, :-1] - ta[0, 1:]).abs()
+    for c in (~ok).nonzero().flatten().tolist():
+        near = min(float(gap[c - 1]) if c > 0 else 1.0, float(gap[c]) if c < 299 else 1.0)
+        assert near < 1e-3, c
+
+
+def test_every_name_the_reference_imports_from_splatt3r_utils():
+    """main.py:41-47, tracker.py:12, global_opt.py:8, frame.py:6,
+    dataloader.py:10 import these from splatt3r_slam.splatt3r_utils."""
+    import importlib
+    names = {"load_splatt3r", "load_retriever", "splatt3r_inference_mono", "splatt3r_render",
+             "gaussians_to_world", "splatt3r_match_asymmetric", "splatt3r_match_symmetric",
+             "resize_img"}
+    import os
+    ref = "/root/reference"
+    if os.path.isdir(ref):                     # cross-check the list where the reference is
+        import re
+        for f in ("main.py", "splatt3r_slam/tracker.py", "splatt3r_slam/global_opt.py",
+                  "splatt3r_slam/frame.py", "splatt3r_slam/dataloader.py"):
+            src = open(os.path.join(ref, f)).read()
+            for m in re.finditer(r"from splatt3r_slam\.splatt3r_utils import \(?([^)]*?)\)?\n"
+                                 r"(?=\S|$)", src, re.S):
+                got = {n.strip() for n in m.group(1).replace("\n", ",").split(",") if n.strip()}
+                assert got <= names, got - names
+    mod = importlib.import_module("splatt3r_amd.splatt3r_utils")
+    for n in sorted(names):
+        assert callable(getattr(mod, n)), n

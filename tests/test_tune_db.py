@@ -67,3 +67,28 @@ def test_shipped_database_matches_this_tree():
             # a batch-invariant plan's choice is in the class of its like
             kk = k[2]
             assert ops.reduction_class(kk, *v) == ops.reduction_class(kk, *k[-1])
+
+
+def _reload_dev(monkeypatch, path, arch):
+    monkeypatch.setattr(ops, "_device_arch", lambda dev: arch)
+    monkeypatch.setattr(ops, "TUNE_DB", str(path))
+    monkeypatch.setattr(ops, "_TUNE_CACHE", {})
+    monkeypatch.setattr(ops, "_DB_STATE", {"loaded": False, "entries": {}})
+    ops._db_load("cuda:0")
+    return dict(ops._TUNE_CACHE)
+
+
+def test_foreign_arch_voids_the_file(tmp_path, monkeypatch, fresh_db_state):
+    p = tmp_path / "db.json"
+    ents = [[[3, 3, 3, None], [32, 1]]]
+    p.write_text(json.dumps({"digest": ops._db_digest(), "arch": "gfx950", "entries": ents}))
+    assert _reload_dev(monkeypatch, p, "gfx942") == {}
+    assert _reload_dev(monkeypatch, p, "gfx950") == {(3, 3, 3, None): (32, 1)}
+
+
+def test_other_kernel_abi_voids_the_file(tmp_path, monkeypatch, fresh_db_state):
+    p = tmp_path / "db.json"
+    ents = [[[3, 3, 3, None], [32, 1]]]
+    p.write_text(json.dumps({"digest": ops._db_digest(), "abi": ops._KERNEL_ABI + 1,
+                             "arch": "gfx950", "entries": ents}))
+    assert _reload_dev(monkeypatch, p, "gfx950") == {}
