@@ -248,10 +248,18 @@ def test_hip_forward_c3_full_size_bitexact_vs_oracle(parity):
 
 
 @pytest.mark.gpu
-def test_hip_backward_1m_splats_c3_resolution_vs_oracle(parity):
-    """Backward at C3 resolution (960x540) with 2^20 splats."""
-    sc = raster_microbench_scene(1 << 20, seed=2)
-    g = raster_grad(sc["H"], sc["W"], seed=3)
+@pytest.mark.parametrize("case", ["1M", "c3_full"])
+def test_hip_backward_1m_splats_c3_resolution_vs_oracle(parity, case):
+    """Backward at C3 resolution (960x540): 2^20 splats, and the full C3
+    microbench case (4,194,304 splats, scene seed 0, dL/dimage seed 1 as
+    SURVEY §8(d) C3 and bench.py's raster_c3 leg)."""
+    from splatt3r_amd.synthetic import C3_P
+    if case == "1M":
+        sc = raster_microbench_scene(1 << 20, seed=2)
+        g = raster_grad(sc["H"], sc["W"], seed=3)
+    else:
+        sc = raster_microbench_scene(C3_P, seed=0)
+        g = raster_grad(sc["H"], sc["W"], seed=1)
     rs, scale, img, radii, kw = _gpu_render(sc, "shs", grad=g)
     ref = oracle.raster(settings_to_dict(rs), sc["means"] * scale, sc["opacities"], shs=sc["shs"],
                         cov3D_precomp=sc["cov6"] * scale * scale, dL_dout=g, nthreads=16)
@@ -264,7 +272,7 @@ def test_hip_backward_1m_splats_c3_resolution_vs_oracle(parity):
         a = a.detach().cpu().numpy().reshape(b.shape).astype(np.float64)
         d = np.abs(a - b)
         sc_ = np.abs(b).max() + 1e-12
-        parity(f"c3_bwd_1M_{name}", max_rel=d.max() / sc_, p999_rel=np.percentile(d, 99.9) / sc_,
+        parity(f"c3_bwd_{case}_{name}", max_rel=d.max() / sc_, p999_rel=np.percentile(d, 99.9) / sc_,
                tol=BWD_TOL)
         assert d.max() <= BWD_TOL * sc_ + 1e-6, (name, d.max() / sc_)
 

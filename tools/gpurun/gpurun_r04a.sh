@@ -8,3 +8,5 @@ tail -3 gpurun_out/r04a_tests.log
 /usr/bin/time -v timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r04a_bench.log 2> gpurun_out/r04a_bench.err || { tail -30 gpurun_out/r04a_bench.err; exit 1; }
 tail -c 3000 gpurun_out/r04a_bench.log
 grep -E "Elapsed|Maximum resident" gpurun_out/r04a_bench.err
+timeout -k 10 300 python -u -m tools.gemm_ceiling > gpurun_out/r04a_gemm_ceiling.log 2>&1 || { tail -20 gpurun_out/r04a_gemm_ceiling.log; exit 1; }
+cat gpurun_out/r04a_gemm_ceiling.log | grep -v "^  t"
