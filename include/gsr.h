@@ -70,6 +70,25 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t num_rendered,
                const int32_t* radii, void* geom, void* binning, void* image,
                float* out_color, void* stream);
 
+/* Sync-free forward (preprocess + binning + blend with no host read):
+ * the instance count and depth-key range stay on the device.  The binning
+ * workspace holds gsr_binning_bytes(capacity) and the depth sort runs over
+ * key_bits bits.  info (device int64[3]) receives {status, num_rendered,
+ * live key bits}: status 0 = out_color is the frame (bit-identical to
+ * gsr_preprocess + gsr_render); bit 0 = more instances than capacity, bit 1
+ * = a depth-key range wider than key_bits -- the image is then not valid and
+ * the caller re-renders with the two-call protocol (sizing the next frame
+ * from info).  For callers that consume the image later than it is produced
+ * (the SLAM frame loop: splatt3r_amd/slam.py), so the stream never waits on
+ * the host.  No backward from this path. */
+int gsr_forward_deferred(const gsr_settings* s, int64_t P, int M, const float* means3D,
+                         const float* scales, const float* rotations,
+                         const float* cov3D_precomp, const float* shs,
+                         const float* colors_precomp, const float* opacities,
+                         int32_t* radii, void* geom, void* binning, int64_t capacity,
+                         int key_bits, void* image, float* out_color, int64_t* info,
+                         void* stream);
+
 /* Backward.  Outputs (caller-zeroed not required; every output is written):
  *   dL_dmeans2D [P,3] (x,y used), dL_dconic [P,4] (scratch),
  *   dL_dopacity [P,1], dL_dcolors [P,3], dL_dmeans3D [P,3],

@@ -46,6 +46,7 @@ SOURCES = {
     "net_gemm_t5.hip": FAST,
     "net_gemm_t6.hip": FAST,
     "net_gemm_t7.hip": FAST,
+    "net_gemm_t8.hip": FAST,
     "net_attn.hip": FAST,
     "net_ops.hip": STRICT,
     "gn_backend.hip": STRICT,

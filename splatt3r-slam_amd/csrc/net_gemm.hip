@@ -15,7 +15,7 @@ int s3n_ln_f16_saturations(int reset);   // net_ops.hip
 extern "C" int s3n_f16_saturations(int reset) {
   int any = 0;
   for (auto fn : {s3gemm::sat_t1, s3gemm::sat_t2, s3gemm::sat_t3, s3gemm::sat_t4, s3gemm::sat_t5,
-                  s3gemm::sat_t6, s3gemm::sat_t7}) {
+                  s3gemm::sat_t6, s3gemm::sat_t7, s3gemm::sat_t8}) {
     const int v = fn(reset);
     if (v < 0) return -1;
     any |= v;
@@ -122,7 +122,8 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   hipStream_t st = s3::as_stream(stream);
   // tile families live in their own translation units (net_gemm_t*.hip)
   for (auto fn : {s3gemm::launch_t1, s3gemm::launch_t2, s3gemm::launch_t3, s3gemm::launch_t4,
-                  s3gemm::launch_t5, s3gemm::launch_t6, s3gemm::launch_t7}) {
+                  s3gemm::launch_t5, s3gemm::launch_t6, s3gemm::launch_t7,
+                  s3gemm::launch_t8}) {
     const int r = fn(a->tile, p, st);
     if (r != s3gemm::kNotMine) return r;
   }

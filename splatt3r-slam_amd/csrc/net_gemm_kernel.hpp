@@ -39,6 +39,7 @@ int launch_t4(int tile, const GemmP& p, hipStream_t st);
 int launch_t5(int tile, const GemmP& p, hipStream_t st);
 int launch_t6(int tile, const GemmP& p, hipStream_t st);
 int launch_t7(int tile, const GemmP& p, hipStream_t st);
+int launch_t8(int tile, const GemmP& p, hipStream_t st);
 // read (and optionally reset) one translation unit's fp16 saturation flag
 int sat_t1(int reset);
 int sat_t2(int reset);
@@ -47,6 +48,7 @@ int sat_t4(int reset);
 int sat_t5(int reset);
 int sat_t6(int reset);
 int sat_t7(int reset);
+int sat_t8(int reset);
 constexpr int kNotMine = -1000;
 }  // namespace s3gemm
 
@@ -909,17 +911,9 @@ __global__ void __launch_bounds__(kThreads) k_splitk_reduce(GemmP p) {
   }
 }
 
-template <int BM, int BN, int S, int NWM = 2, int NWN = 2, int BK = 64, int KG = 1, int MF = 32>
-int launch(const GemmP& p, hipStream_t st) {
-  S3_REQUIRE(MF == 32 || p.vec_epi, "s3n_gemm: 16x16 MFMA tiles need the vector epilogue");
-  static_assert(MF == 32 || BM * BN * 4 <= S * (BM + BN) * BK * 2,
-                "16x16 MFMA tiles stage their fp32 tile in the LDS ring");
-  S3_REQUIRE(!p.tail_w[0] || p.N == BN,
-             "s3n_gemm: the fused tail needs N == the tile width (%d, N = %d)", BN, p.N);
-  S3_REQUIRE(!p.tail_w[0] || BM * BN * 4 <= S * (BM + BN) * BK * 2,
-             "s3n_gemm: the fused tail needs a tile whose fp32 image fits its LDS ring");
-  S3_REQUIRE(KG == 1 || !p.tail_w[0], "s3n_gemm: the fused tail runs with one K-group");
-  constexpr int NT = 64 * NWM * NWN * KG;
+// Launch geometry shared by the kernel templates: tile counts, split-K
+// ranges (no empty splits), tile order and the 2-D XCD partition.
+__attribute__((unused)) static GemmP plan_grid(const GemmP& p, int BM, int BN, int BK) {
   GemmP q = p;
   q.tiles_m = (p.M + BM - 1) / BM;
   q.tiles_n = (p.N + BN - 1) / BN;
@@ -944,6 +938,36 @@ int launch(const GemmP& p, hipStream_t st) {
       if (c < best) { best = c; q.xcd_px = px; }
     }
   }
+  return q;
+}
+
+// The split-K combine launch after a split kernel.
+__attribute__((unused)) static int launch_splitk_reduce(const GemmP& q, hipStream_t st) {
+  if (q.split_k > 1) {
+    if (q.N % 4 == 0) {
+      dim3 rg((unsigned)s3::cdiv((int64_t)q.M * q.N / 4, kThreads), q.groups);
+      k_splitk_reduce<4><<<rg, kThreads, 0, st>>>(q);
+    } else {
+      dim3 rg((unsigned)s3::cdiv((int64_t)q.M * q.N, kThreads), q.groups);
+      k_splitk_reduce<1><<<rg, kThreads, 0, st>>>(q);
+    }
+    S3_LAUNCH_CHECK();
+  }
+  return S3_OK;
+}
+
+template <int BM, int BN, int S, int NWM = 2, int NWN = 2, int BK = 64, int KG = 1, int MF = 32>
+int launch(const GemmP& p, hipStream_t st) {
+  S3_REQUIRE(MF == 32 || p.vec_epi, "s3n_gemm: 16x16 MFMA tiles need the vector epilogue");
+  static_assert(MF == 32 || BM * BN * 4 <= S * (BM + BN) * BK * 2,
+                "16x16 MFMA tiles stage their fp32 tile in the LDS ring");
+  S3_REQUIRE(!p.tail_w[0] || p.N == BN,
+             "s3n_gemm: the fused tail needs N == the tile width (%d, N = %d)", BN, p.N);
+  S3_REQUIRE(!p.tail_w[0] || BM * BN * 4 <= S * (BM + BN) * BK * 2,
+             "s3n_gemm: the fused tail needs a tile whose fp32 image fits its LDS ring");
+  S3_REQUIRE(KG == 1 || !p.tail_w[0], "s3n_gemm: the fused tail runs with one K-group");
+  constexpr int NT = 64 * NWM * NWN * KG;
+  const GemmP q = plan_grid(p, BM, BN, BK);
   dim3 grid(q.tiles_m * q.tiles_n, q.split_k, p.groups);
   if (p.a_mode == S3N_A_DENSE)
     k_gemm<BM, BN, NWM, NWN, kDense, S, BK, KG, MF><<<grid, NT, 0, st>>>(q);
@@ -952,17 +976,7 @@ int launch(const GemmP& p, hipStream_t st) {
   else
     k_gemm<BM, BN, NWM, NWN, kConv, S, BK, KG, MF><<<grid, NT, 0, st>>>(q);
   S3_LAUNCH_CHECK();
-  if (q.split_k > 1) {
-    if (p.N % 4 == 0) {
-      dim3 rg((unsigned)s3::cdiv((int64_t)p.M * p.N / 4, kThreads), p.groups);
-      k_splitk_reduce<4><<<rg, kThreads, 0, st>>>(q);
-    } else {
-      dim3 rg((unsigned)s3::cdiv((int64_t)p.M * p.N, kThreads), p.groups);
-      k_splitk_reduce<1><<<rg, kThreads, 0, st>>>(q);
-    }
-    S3_LAUNCH_CHECK();
-  }
-  return S3_OK;
+  return launch_splitk_reduce(q, st);
 }
 
 

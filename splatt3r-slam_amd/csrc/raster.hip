@@ -84,6 +84,7 @@ struct GeomState {
   uint32_t* dtot;   // [bins]
   uint4* dup_sorted;  // dup records in depth order (k_order_gather)
   uint32_t* cnt_seg;  // [P / kDupRanks]: instances per depth-rank segment -> offsets
+  uint32_t* dyn;      // [4] sync-free forward: kmin, span, instances kept
 };
 
 // One layout routine serves both sizing (base == nullptr) and carving.
@@ -105,6 +106,7 @@ GeomState carve_geom(void* base, int64_t P, size_t* total = nullptr) {
   g.dtot = c.take<uint32_t>(kMaxBins);
   g.dup_sorted = c.take<uint4>(P);
   g.cnt_seg = c.take<uint32_t>(std::max<int64_t>(1, s3::cdiv(P, kDupRanks)));
+  g.dyn = c.take<uint32_t>(4);
   if (total) *total = c.off;
   return g;
 }
@@ -459,18 +461,33 @@ k_row_scan(uint32_t* __restrict__ hist, int64_t cols, uint32_t* __restrict__ tot
 struct Digit {
   uint32_t kmin, span;
   int shift, bits;
+  // device (kmin, span) of the sync-free forward (gsr_forward_deferred);
+  // null: the host values above
+  const uint32_t* dyn;
   __device__ __forceinline__ uint32_t operator()(uint32_t key) const {
     uint32_t k = key - kmin;
     k = k < span ? k : span;
     return (k >> shift) & ((1u << bits) - 1u);
   }
+  __device__ __forceinline__ Digit live() const {
+    Digit d = *this;
+    if (dyn) { d.kmin = dyn[0]; d.span = dyn[1]; }
+    return d;
+  }
 };
+
+// item count of a pass: the host bound, or the device count when given
+__device__ __forceinline__ int64_t live_n(int64_t n, const uint32_t* dn) {
+  return dn ? min(n, (int64_t)*dn) : n;
+}
 
 template <typename K>
 __global__ void __launch_bounds__(kSortThreads)
-k_rs_hist(int64_t n, const K* __restrict__ keys, Digit dg, int64_t nseg,
-          uint32_t* __restrict__ hist) {
+k_rs_hist(int64_t n, const K* __restrict__ keys, Digit dg_in, int64_t nseg,
+          uint32_t* __restrict__ hist, const uint32_t* __restrict__ dn) {
   __shared__ uint32_t cnt[kMaxBins];
+  const Digit dg = dg_in.live();
+  n = live_n(n, dn);
   const int bins = 1 << dg.bits;
   for (int d = threadIdx.x; d < bins; d += kSortThreads) cnt[d] = 0u;
   __syncthreads();
@@ -500,9 +517,12 @@ k_rs_hist(int64_t n, const K* __restrict__ keys, Digit dg, int64_t nseg,
 template <typename K, typename V>
 __global__ void __launch_bounds__(kSortThreads)
 k_rs_scatter(int64_t n, const K* __restrict__ kin, const V* __restrict__ vin,
-             K* __restrict__ kout, V* __restrict__ vout, Digit dg, int64_t nseg,
-             const uint32_t* __restrict__ hist, const uint32_t* __restrict__ tot) {
+             K* __restrict__ kout, V* __restrict__ vout, Digit dg_in, int64_t nseg,
+             const uint32_t* __restrict__ hist, const uint32_t* __restrict__ tot,
+             const uint32_t* __restrict__ dn) {
   constexpr int NW = kSortThreads / 64;
+  const Digit dg = dg_in.live();
+  n = live_n(n, dn);
   __shared__ uint32_t cnt[NW][kMaxBins];  // per-wave counts -> local slots
   __shared__ uint32_t gdelta[kMaxBins];   // global slot - local slot, per digit
   __shared__ uint32_t s_w[NW];
@@ -666,7 +686,7 @@ __global__ void __launch_bounds__(kThreads)
 k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ order,
             const uint4* __restrict__ dsorted,
             const uint32_t* __restrict__ seg_off, int64_t nwseg, K* __restrict__ keys,
-            uint32_t* __restrict__ vals) {
+            uint32_t* __restrict__ vals, uint32_t cap) {
   __shared__ K s_key[kThreads / 64][DCH];
   __shared__ uint32_t s_val[kThreads / 64][DCH];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -728,7 +748,9 @@ k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ order,
         }
       }
       wave_lds_sync();
-      for (uint32_t t = lane; t < c1 - c0; t += 64) {
+      // cap: the instance capacity of the sync-free forward (instances past
+      // it are dropped and the frame is flagged by k_red_finalize)
+      for (uint32_t t = lane; t < c1 - c0 && c0 + t < cap; t += 64) {
         keys[c0 + t] = sk[t];
         vals[c0 + t] = sv[t];
       }
@@ -739,7 +761,9 @@ k_duplicate(int64_t P, int gx, const uint32_t* __restrict__ order,
 
 template <typename K>
 __global__ void __launch_bounds__(kThreads)
-k_ranges(int64_t R, const K* __restrict__ keys, uint2* __restrict__ ranges) {
+k_ranges(int64_t R, const K* __restrict__ keys, uint2* __restrict__ ranges,
+         const uint32_t* __restrict__ dn) {
+  R = live_n(R, dn);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R) return;
   const uint32_t cur = keys[i];
@@ -764,26 +788,59 @@ inline int tile_sort_buffer(int ntiles) {
   return sort_passes(bit_length((uint64_t)(ntiles - 1))) & 1;
 }
 
+// dyn / dn: device (kmin, span) and item count of the sync-free forward
+// (kernels sized for the host bound n, items past *dn ignored).
 template <typename K, typename V>
 int radix_sort(int64_t n, K* keys[2], V* vals[2], uint32_t kmin, uint32_t span, int bits,
                bool keep_keys, uint32_t* hist, uint32_t* tot, hipStream_t st,
-               bool index_vals = false) {
+               bool index_vals = false, const uint32_t* dyn = nullptr,
+               const uint32_t* dn = nullptr) {
   const int passes = sort_passes(bits);
   const int width = (bits + passes - 1) / passes;
   const int64_t nseg = nsegs(n);
   int src = 0;
   for (int p = 0; p < passes; ++p) {
     const int hi = std::min(bits, (p + 1) * width);
-    const Digit dg{kmin, span, p * width, std::max(1, hi - p * width)};
-    k_rs_hist<K><<<(unsigned)nseg, kSortThreads, 0, st>>>(n, keys[src], dg, nseg, hist);
+    const Digit dg{kmin, span, p * width, std::max(1, hi - p * width), dyn};
+    k_rs_hist<K><<<(unsigned)nseg, kSortThreads, 0, st>>>(n, keys[src], dg, nseg, hist, dn);
     k_row_scan<<<1u << dg.bits, kThreads, 0, st>>>(hist, nseg, tot);
     const bool last = p == passes - 1;
     k_rs_scatter<K, V><<<(unsigned)nseg, kSortThreads, 0, st>>>(
         n, keys[src], (p == 0 && index_vals) ? nullptr : vals[src], (!last || keep_keys) ? keys[src ^ 1] : nullptr, vals[src ^ 1],
-        dg, nseg, hist, tot);
+        dg, nseg, hist, tot, dn);
     src ^= 1;
   }
   return src;
+}
+
+// The sync-free forward's bookkeeping (one wave, after k_preprocess): the
+// reduction slots -> instance total and depth-key range; dyn = {kmin, span,
+// instances kept (<= cap)}; info = {status, instances, live key bits}, status
+// bit 0 = more instances than the binning capacity, bit 1 = a key range wider
+// than the depth sort's passes cover (the image is then not valid).
+__global__ void __launch_bounds__(64)
+k_red_finalize(const Reduce* __restrict__ red, uint32_t cap, int key_bits,
+               uint32_t* __restrict__ dyn, int64_t* __restrict__ info) {
+  const int lane = threadIdx.x;
+  unsigned long long total = red->slot[lane].total;
+  uint32_t kmax = red->slot[lane].kmax, kmin_inv = red->slot[lane].kmin_inv;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    total += __shfl_xor(total, o, 64);
+    kmax = max(kmax, (uint32_t)__shfl_xor(kmax, o, 64));
+    kmin_inv = max(kmin_inv, (uint32_t)__shfl_xor(kmin_inv, o, 64));
+  }
+  if (lane != 0) return;
+  const uint32_t kmin = total ? ~kmin_inv : 0u;
+  const uint32_t span = total ? kmax - kmin + 1u : 1u;
+  const int bits = 32 - __clz(span);
+  const int status = (total > cap ? 1 : 0) | (bits > key_bits ? 2 : 0);
+  dyn[0] = kmin;
+  dyn[1] = span;
+  dyn[2] = (uint32_t)min(total, (unsigned long long)cap);
+  info[0] = status;
+  info[1] = (int64_t)total;
+  info[2] = bits;
 }
 
 // --------------------------------------------------------------- blend ----
@@ -1336,12 +1393,16 @@ int gsr_preprocess(const gsr_settings* s, int64_t P, int M, const float* means3D
   return S3_OK;
 }
 
-int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii,
-               void* geom, void* binning, void* image, float* out_color, void* stream) {
-  S3_REQUIRE(s && P >= 0 && R >= 0, "gsr_render: bad arguments");
-  S3_REQUIRE(R < ((int64_t)1 << 32), "gsr_render: too many tile instances");
-  (void)radii;
-  hipStream_t st = s3::as_stream(stream);
+}  // extern "C"
+
+namespace {
+// Binning + blend of gsr_render.  R: instances (host count; the binning
+// capacity in the sync-free forward).  kmin / span / bits: the depth sort's
+// key range and pass width.  dyn (sync-free): device {kmin, span, instances}
+// that override kmin / span and bound the instance passes.
+int render_impl(const gsr_settings* s, int64_t P, int64_t R, void* geom, void* binning,
+                void* image, float* out_color, hipStream_t st, uint32_t kmin, uint32_t span,
+                int bits, const uint32_t* dyn) {
   const int W = s->image_width, H = s->image_height;
   const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY, ntiles = gx * gy;
   if (P == 0) {
@@ -1354,19 +1415,11 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
   tmark(3, st);
   S3_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * ntiles, st));
   const uint32_t* point_list = b.vals[0];
+  const uint32_t* dn = dyn ? dyn + 2 : nullptr;
+  const uint32_t cap = dyn ? (uint32_t)R : 0xFFFFFFFFu;
   if (R > 0) {
-    // the depth-key range of this geometry buffer, from gsr_preprocess's
-    // read-back (full 32-bit width if the buffer was filled elsewhere)
-    uint32_t kmin = 0, kmax = 0xFFFFFFFEu;
-    if (g_keyrange.geom == geom && g_keyrange.P == P) {
-      kmin = g_keyrange.kmin;
-      kmax = g_keyrange.kmax;
-    }
-    // visible keys map to [0, kmax - kmin], culled ones (~0u) to span
-    const uint32_t span = kmax - kmin + 1u;
-    const int dsrc = radix_sort<uint32_t, uint32_t>(P, g.dkey, g.dval, kmin, span,
-                                                    bit_length(span), false, g.dhist, g.dtot, st,
-                                                    true);
+    const int dsrc = radix_sort<uint32_t, uint32_t>(P, g.dkey, g.dval, kmin, span, bits, false,
+                                                    g.dhist, g.dtot, st, true, dyn);
     const uint32_t* order = g.dval[dsrc];
     tmark(4, st);
     const int64_t nwseg = s3::cdiv(P, kDupRanks);
@@ -1382,18 +1435,20 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
       uint16_t* k16[2] = {reinterpret_cast<uint16_t*>(b.keys[0]),
                           reinterpret_cast<uint16_t*>(b.keys[1])};
       k_duplicate<uint16_t><<<dup_blocks, kThreads, 0, st>>>(P, gx, order, g.dup_sorted,
-                                                             g.cnt_seg, nwseg, k16[0], b.vals[0]);
+                                                             g.cnt_seg, nwseg, k16[0], b.vals[0],
+                                                             cap);
       tsrc = radix_sort<uint16_t, uint32_t>(R, k16, b.vals, 0u, 0xFFFFFFFFu, tbits, true, b.hist,
-                                            b.tot, st);
+                                            b.tot, st, false, nullptr, dn);
       k_ranges<uint16_t><<<(unsigned)s3::cdiv(R, kThreads), kThreads, 0, st>>>(R, k16[tsrc],
-                                                                             im.ranges);
+                                                                             im.ranges, dn);
     } else {
       k_duplicate<uint32_t><<<dup_blocks, kThreads, 0, st>>>(P, gx, order, g.dup_sorted,
-                                                             g.cnt_seg, nwseg, b.keys[0], b.vals[0]);
+                                                             g.cnt_seg, nwseg, b.keys[0], b.vals[0],
+                                                             cap);
       tsrc = radix_sort<uint32_t, uint32_t>(R, b.keys, b.vals, 0u, 0xFFFFFFFFu, tbits, true,
-                                            b.hist, b.tot, st);
+                                            b.hist, b.tot, st, false, nullptr, dn);
       k_ranges<uint32_t><<<(unsigned)s3::cdiv(R, kThreads), kThreads, 0, st>>>(R, b.keys[tsrc],
-                                                                             im.ranges);
+                                                                             im.ranges, dn);
     }
     S3_REQUIRE(tsrc == tile_sort_buffer(ntiles), "gsr_render: tile sort buffer mismatch");
     point_list = b.vals[tsrc];
@@ -1407,6 +1462,66 @@ int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii
   S3_LAUNCH_CHECK();
   tmark(6, st);
   return S3_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gsr_render(const gsr_settings* s, int64_t P, int64_t R, const int32_t* radii,
+               void* geom, void* binning, void* image, float* out_color, void* stream) {
+  S3_REQUIRE(s && P >= 0 && R >= 0, "gsr_render: bad arguments");
+  S3_REQUIRE(R < ((int64_t)1 << 32), "gsr_render: too many tile instances");
+  (void)radii;
+  // the depth-key range of this geometry buffer, from gsr_preprocess's
+  // read-back (full 32-bit width if the buffer was filled elsewhere)
+  uint32_t kmin = 0, kmax = 0xFFFFFFFEu;
+  if (g_keyrange.geom == geom && g_keyrange.P == P) {
+    kmin = g_keyrange.kmin;
+    kmax = g_keyrange.kmax;
+  }
+  // visible keys map to [0, kmax - kmin], culled ones (~0u) to span
+  const uint32_t span = kmax - kmin + 1u;
+  return render_impl(s, P, R, geom, binning, image, out_color, s3::as_stream(stream), kmin, span,
+                     bit_length(span), nullptr);
+}
+
+int gsr_forward_deferred(const gsr_settings* s, int64_t P, int M, const float* means3D,
+                         const float* scales, const float* rotations, const float* cov3D_precomp,
+                         const float* shs, const float* colors_precomp, const float* opacities,
+                         int32_t* radii, void* geom, void* binning, int64_t capacity,
+                         int key_bits, void* image, float* out_color, int64_t* info,
+                         void* stream) {
+  S3_REQUIRE(s && info && P >= 0, "gsr_forward_deferred: bad arguments");
+  S3_REQUIRE(P < (int64_t)1 << 31, "gsr_forward_deferred: P too large");
+  S3_REQUIRE(capacity >= 1 && capacity < ((int64_t)1 << 32) && key_bits >= 1 && key_bits <= 32,
+             "gsr_forward_deferred: capacity 1..2^32-1, key_bits 1..32");
+  S3_REQUIRE((shs == nullptr) != (colors_precomp == nullptr),
+             "Please provide excatly one of either SHs or precomputed colors!");
+  S3_REQUIRE((cov3D_precomp == nullptr) != (scales == nullptr || rotations == nullptr),
+             "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+  S3_REQUIRE(s->sh_degree >= 0 && s->sh_degree <= 3, "gsr_forward_deferred: sh_degree 0..3");
+  S3_REQUIRE(shs == nullptr || M >= (s->sh_degree + 1) * (s->sh_degree + 1),
+             "gsr_forward_deferred: M=%d too small for sh_degree %d", M, s->sh_degree);
+  hipStream_t st = s3::as_stream(stream);
+  if (P == 0) {
+    S3_HIP(hipMemsetAsync(info, 0, 3 * sizeof(int64_t), st));
+    return render_impl(s, 0, 0, geom, binning, image, out_color, st, 0, 1, 1, nullptr);
+  }
+  Cam cam = make_cam(s, M);
+  GeomState g = carve_geom(geom, P);
+  tmark(0, st);
+  S3_HIP(hipMemsetAsync(g.red, 0, sizeof(Reduce), st));
+  k_preprocess<<<(unsigned)s3::cdiv(P, kThreads), kThreads, 0, st>>>(
+      P, cam, means3D, scales, rotations, cov3D_precomp, shs, colors_precomp, opacities,
+      s->viewmatrix, s->projmatrix, s->campos, radii, g);
+  S3_LAUNCH_CHECK();
+  k_red_finalize<<<1, 64, 0, st>>>(g.red, (uint32_t)capacity, key_bits, g.dyn, info);
+  S3_LAUNCH_CHECK();
+  tmark(1, st);
+  tmark(2, st);
+  const uint32_t span_bound = key_bits >= 32 ? 0xFFFFFFFFu : ((1u << key_bits) - 1u);
+  return render_impl(s, P, capacity, geom, binning, image, out_color, st, 0u, span_bound,
+                     key_bits, g.dyn);
 }
 
 int gsr_backward(const gsr_settings* s, int64_t P, int M, int64_t R, const float* means3D,

@@ -60,6 +60,8 @@ _lib.register({
     "gsr_backward": (ctypes.c_int, [_SP, ctypes.c_int64, ctypes.c_int, ctypes.c_int64] +
                      [P_] * 8 + [P_, P_, P_, P_] + [P_] * 9 + [P_]),
     "gsr_mark_visible": (ctypes.c_int, [ctypes.c_int64, P_, P_, P_, P_, P_]),
+    "gsr_forward_deferred": (ctypes.c_int, [_SP, ctypes.c_int64, ctypes.c_int] + [P_] * 7 +
+                             [P_, P_, P_, ctypes.c_int64, ctypes.c_int, P_, P_, P_, P_]),
     "gsr_set_timing": (None, [ctypes.c_int]),
     "gsr_last_timing": (ctypes.c_int, [P_, ctypes.c_int]),
 })
@@ -233,6 +235,48 @@ class GaussianRasterizer(nn.Module):
 
 # tile instances (num_rendered) of the most recent forward (bench/diagnostics)
 last_num_rendered = 0
+
+
+def rasterize_deferred(raster_settings, means3D, opacities, shs=None, colors_precomp=None,
+                       cov3D_precomp=None, scales=None, rotations=None, capacity=1 << 20,
+                       key_bits=32):
+    """Forward only, with no host read on the stream (include/gsr.h
+    gsr_forward_deferred): binning capacity `capacity` instances, depth sort
+    over `key_bits` bits.  Returns (color [3,H,W], radii [P], info) where
+    info is a device int64[3] {status, num_rendered, live key bits}; the
+    image is the frame only when status == 0 (otherwise re-render with
+    GaussianRasterizer and size the next call from info).  An extension of
+    this module for callers that consume the image later (the SLAM frame
+    loop, splatt3r_amd.slam); the reference API above is unchanged."""
+    if (shs is None) == (colors_precomp is None):
+        raise Exception("Please provide excatly one of either SHs or precomputed colors!")
+    if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+            ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+        raise Exception("Please provide exactly one of either scale/rotation pair or "
+                        "precomputed 3D covariance!")
+    _lib.require_cuda(means3D)
+    dev = means3D.device
+    P = means3D.shape[0]
+    H, W = int(raster_settings.image_height), int(raster_settings.image_width)
+    m3 = _f32c(means3D)
+    shc = _f32c(shs)
+    M = 0 if shc is None else (shc.shape[1] if shc.dim() == 3 else shc.shape[-1] // 3)
+    col, op = _f32c(colors_precomp), _f32c(opacities)
+    sc, rot, cov = _f32c(scales), _f32c(rotations), _f32c(cov3D_precomp)
+    s, keep = _settings_struct(raster_settings, dev)
+    L = _lib.lib()
+    color = torch.empty(3, H, W, device=dev, dtype=torch.float32)
+    radii = torch.empty(P, device=dev, dtype=torch.int32)
+    geom = torch.empty(int(L.gsr_geom_bytes(P)), device=dev, dtype=torch.uint8)
+    img = torch.empty(int(L.gsr_image_bytes(H, W)), device=dev, dtype=torch.uint8)
+    binning = torch.empty(int(L.gsr_binning_bytes(int(capacity))), device=dev, dtype=torch.uint8)
+    info = torch.empty(3, device=dev, dtype=torch.int64)
+    _lib.check(L.gsr_forward_deferred(
+        ctypes.byref(s), P, M, m3.data_ptr(), _lib.ptr(sc), _lib.ptr(rot), _lib.ptr(cov),
+        _lib.ptr(shc), _lib.ptr(col), _lib.ptr(op), radii.data_ptr(), geom.data_ptr(),
+        binning.data_ptr(), int(capacity), int(key_bits), img.data_ptr(), color.data_ptr(),
+        info.data_ptr(), _lib.stream(dev)), "gsr_forward_deferred")
+    return color, radii, info
 
 
 def set_timing(enabled: bool) -> None:

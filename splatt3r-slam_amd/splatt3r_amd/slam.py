@@ -39,7 +39,7 @@ import lietorch
 from splatt3r_amd.config import config
 from splatt3r_amd.frame import Frame, Keyframes, Mode, create_frame
 from splatt3r_amd.gaussian_map import SharedGaussians, should_append_gaussians
-from splatt3r_amd.splatt3r_utils import (_sim3_to_4x4, splatt3r_inference_mono,
+from splatt3r_amd.splatt3r_utils import (RasterSizing, _sim3_to_4x4, splatt3r_inference_mono,
                                          splatt3r_render, world_records)
 from splatt3r_amd.tracker import FrameTracker
 
@@ -166,7 +166,7 @@ class Frontend:
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
                  readback=True, enc_batch=1, main_priority=None, late_prefetch=False,
                  viz=False, max_gaussians=4 * 1024 * 1024, backend=None, render_writer=None,
-                 decode_ahead=False, enc_ahead=None, render_async=False):
+                 decode_ahead=False, enc_ahead=None, render_async=False, deferred_render=True):
         self.model = model
         # dataio.RenderWriter: the per-frame gs_init_* / gs_track_* PNG export
         # (main.py:436-446, 490-506), written off the tracking thread
@@ -208,7 +208,7 @@ class Frontend:
         self.new_kf_frames: list[int] = []
         self._gw_count = None   # device count of world records (no-viz path)
         self._stats = dict(frames=0, tracked=0, reloc=0, keyframes=0, gn_iters=0,
-                          gaussians_world=0, rendered=0)
+                          gaussians_world=0, rendered=0, rerendered=0)
         self._last_render = None
         # host read-back of the render: double-buffered pinned images filled by
         # async D2H copies; `last_render` waits for the copy on access, so the
@@ -238,6 +238,13 @@ class Frontend:
         # render_async:splatt3r_render + its PNG write / read-back on a
         # worker thread and stream (_RenderWorker); drain() waits for them
         self._rworker = _RenderWorker(device) if render_async and render else None
+        # sync-free renders (diff_gaussian_rasterization.rasterize_deferred):
+        # the tracked frame's render never waits for the host; each image is
+        # delivered (PNG writer / read-back) once its validity flag, copied
+        # to the host behind it, shows it fitted the binning capacity
+        # (re-rendered with the two-call path otherwise), in frame order
+        self.sizing = RasterSizing() if deferred_render else None
+        self._pending: list = []
         self._tickets: list = []
         # min(match_frac_k, unique_frac_f) of the frames tracked against the
         # current keyframe, in order: the decode-ahead pairing predictor
@@ -327,6 +334,12 @@ class Frontend:
         for t in self._tickets:
             t.done.wait()
         self._tickets = []
+        if self._pending:
+            # on the stream the renders were issued on (their buffers belong to it)
+            st = self.main_stream if self.main_stream is not None else \
+                torch.cuda.current_stream(self.device)
+            with torch.cuda.stream(st):
+                self._deliver(block=True)
         if self._rworker is not None:
             if self._rworker.timeouts:
                 n, self._rworker.timeouts = self._rworker.timeouts, 0
@@ -382,7 +395,8 @@ class Frontend:
             self._render_task(frame, ref, target).keep(
                 lambda img: self._finish_render(img, idx, prefix, count=False))
             return
-        self._finish_render(splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=target),
+        self._finish_render(splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=target,
+                                            sizing=self.sizing),
                             frame.frame_id, prefix)
 
     def _speculate(self, frame, ref):
@@ -401,16 +415,47 @@ class Frontend:
                 elif self._rworker is not None:
                     img = self._render_task(frame, ref, T_WC)      # a ticket
                 else:
-                    img = splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=T_WC)
+                    img = splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=T_WC,
+                                          sizing=self.sizing)
             finally:
                 frame.T_WC = saved
             return recs, img
         return hook
 
     def _finish_render(self, img, index=0, prefix="gs_track", count=True):
+        if img is not None and count:
+            self._stats["rendered"] += 1
+        chk = getattr(img, "_gsr_check", None)
+        if chk is not None:
+            info = torch.empty(3, dtype=torch.int64, pin_memory=True)
+            info.copy_(chk.info, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending.append((img, chk, info, ev, index, prefix))
+            return
+        self._deliver_image(img, index, prefix)
+
+    def _deliver(self, block: bool):
+        """Hand the validated sync-free renders to the writer / read-back in
+        frame order: each one once its flag copy has landed (without waiting
+        for it unless `block`), re-rendered by the two-call path if it did
+        not fit."""
+        while self._pending:
+            img, chk, info, ev, index, prefix = self._pending[0]
+            if not block and not ev.query():
+                return
+            ev.synchronize()
+            self._pending.pop(0)
+            status, total, bits = (int(v) for v in info.tolist())
+            chk.sizing.update(total, bits)
+            if status != 0:
+                chk.sizing.rerenders += 1
+                self._stats["rerendered"] += 1
+                img = chk.rerender()
+            self._deliver_image(img, index, prefix)
+
+    def _deliver_image(self, img, index, prefix):
         if img is not None:
-            if count:
-                self._stats["rendered"] += 1
             if self.render_writer is not None:
                 self.render_writer.submit(index, img, prefix)
                 self._last_render, self._rb_event = None, None
@@ -527,6 +572,8 @@ class Frontend:
     def _step(self, i: int, img, next_img=None, e0=None) -> Frame:
         if self.fps_timer is None:
             self.fps_timer = time.time()
+        # renders of earlier frames whose validity flags have landed
+        self._deliver(block=False)
         # keyframe poses the backend worker has finished optimising
         # (SharedKeyframes' in-place writes, frame.py:269-330)
         self.keyframes.apply_pending()

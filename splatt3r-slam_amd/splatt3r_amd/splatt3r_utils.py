@@ -325,8 +325,44 @@ def _estimate_default_intrinsics(h, w, device="cuda"):
 
 
 @torch.inference_mode()
-def splatt3r_render(model, frame, ref_frame, K=None, target_T_WC=None):
-    """splatt3r_utils.py:332-432 -> [1,1,3,H,W]."""
+class RasterSizing:
+    """Binning capacity and depth-key width for the sync-free render
+    (diff_gaussian_rasterization.rasterize_deferred), learnt from the frames
+    already validated: capacity 1.25 x the most instances seen + 64k, key
+    width the widest seen + 1 bit.  Before the first validated frame the
+    render takes the two-call path (one host read)."""
+
+    def __init__(self):
+        self.capacity = None
+        self.key_bits = 32
+        self.max_total = 0
+        self.max_bits = 0
+        self.rerenders = 0
+
+    def update(self, total: int, bits=None):
+        self.max_total = max(self.max_total, int(total))
+        self.capacity = int(self.max_total * 1.25) + 65536
+        if bits is not None:
+            self.max_bits = max(self.max_bits, int(bits))
+            self.key_bits = min(32, self.max_bits + 1)
+
+
+class RenderCheck:
+    """The validity of a sync-free render: `info` (device int64[3] {status,
+    instances, key bits}) and the two-call re-render to use when the frame
+    did not fit.  Attached to the returned image as `_gsr_check`."""
+
+    def __init__(self, info, rerender, sizing):
+        self.info, self.rerender, self.sizing = info, rerender, sizing
+
+
+def splatt3r_render(model, frame, ref_frame, K=None, target_T_WC=None, sizing=None):
+    """splatt3r_utils.py:332-432 -> [1,1,3,H,W].
+
+    sizing (RasterSizing, the frame loop): render without a host read of
+    the instance count (rasterize_deferred); the image then carries a
+    RenderCheck (`image._gsr_check`) that its consumer resolves
+    (Frontend._deliver) before using it."""
     if frame.gaussian_pred is None or frame.gaussian_pred_cross is None:
         print("[splatt3r_render] No Gaussian predictions available – skipping.")
         return None
@@ -349,12 +385,25 @@ def splatt3r_render(model, frame, ref_frame, K=None, target_T_WC=None):
                           opacities=g["opacities"].reshape(-1, 1),
                           img=img.to(dev)))
     means, cov6, shs, opac = pack_splats(views, float(scale[0]), img_chw_normalized=True)
-    from diff_gaussian_rasterization import GaussianRasterizer
-    means2D = torch.zeros_like(means)
-    image, _ = GaussianRasterizer(settings[0])(means3D=means, means2D=means2D, shs=shs,
-                                               colors_precomp=None, opacities=opac,
-                                               cov3D_precomp=cov6)
-    return image[None, None]
+    import diff_gaussian_rasterization as dgr
+    rs = settings[0]
+
+    def two_call():
+        image, _ = dgr.GaussianRasterizer(rs)(means3D=means, means2D=torch.zeros_like(means),
+                                              shs=shs, colors_precomp=None, opacities=opac,
+                                              cov3D_precomp=cov6)
+        return image[None, None]
+
+    if sizing is None or sizing.capacity is None:
+        out = two_call()
+        if sizing is not None:
+            sizing.update(dgr.last_num_rendered)
+        return out
+    image, _, info = dgr.rasterize_deferred(rs, means, opac, shs=shs, cov3D_precomp=cov6,
+                                            capacity=sizing.capacity, key_bits=sizing.key_bits)
+    out = image[None, None]
+    out._gsr_check = RenderCheck(info, two_call, sizing)
+    return out
 
 
 class S3wView(ctypes.Structure):

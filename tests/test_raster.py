@@ -416,3 +416,37 @@ def test_hip_camera_settings_from_sim3_vs_reference_capture():
     np.testing.assert_allclose(st.viewmatrix.cpu().numpy(), g["settings_viewmatrix"], atol=2e-6)
     np.testing.assert_allclose(st.projmatrix.cpu().numpy(), g["settings_projmatrix"], atol=1e-5)
     np.testing.assert_allclose(st.campos.cpu().numpy(), g["settings_campos"], atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,seed,mode,hw", [(2000, 0, "shs", (48, 64)), (5000, 1, "colors", (48, 64)),
+                                            (1, 2, "shs", (48, 64)), (60000, 3, "shs", (384, 512))])
+def test_hip_deferred_forward_equals_two_call_forward(P, seed, mode, hw):
+    """gsr_forward_deferred (no host read; instance count and depth-key range
+    on the device) == gsr_preprocess + gsr_render bit for bit when the frame
+    fits; too small a capacity or key width raises the status bits (memory
+    safe, image not used) and reports the sizes for the next call."""
+    import diff_gaussian_rasterization as dgr
+    H, W = hw
+    sc = small_scene(P, seed, H=H, W=W, fx=60.0 * W / 64)
+    rs, scale, img, radii, kw = _gpu_render(sc, mode)
+    R = dgr.last_num_rendered
+    args = dict(means3D=kw["means3D"].detach(), opacities=kw["opacities"].detach(),
+                cov3D_precomp=kw["cov3D_precomp"].detach())
+    if mode == "shs":
+        args["shs"] = kw["shs"].detach()
+    else:
+        args["colors_precomp"] = kw["colors_precomp"].detach()
+    for cap, bits in ((R + 1000, 32), (max(R, 1), 32), (2 * R + 1, 24)):
+        c, r, info = dgr.rasterize_deferred(rs, capacity=cap, key_bits=bits, **args)
+        st, tot, live = info.tolist()
+        assert tot == R and live <= 32
+        if live <= bits:
+            assert st == 0, (cap, bits, st)
+            assert torch.equal(c, img.detach()) and torch.equal(r, radii)
+    if R > 1:
+        _, _, info = dgr.rasterize_deferred(rs, capacity=R // 2, key_bits=32, **args)
+        assert info.tolist()[0] & 1
+    _, _, info = dgr.rasterize_deferred(rs, capacity=R + 10, key_bits=1, **args)
+    st, tot, live = info.tolist()
+    assert (st & 2) == (2 if live > 1 else 0)

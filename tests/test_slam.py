@@ -453,3 +453,58 @@ def test_frontend_writes_render_pngs(tmp_path):
         want = render_to_uint8(fe2.last_render.cpu().numpy())
         got = np.asarray(Image.open(tmp_path / "renders" / names[i]))
         np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_sync_free_render_matches_two_call_render():
+    """The frame loop renders without a host read of the instance count
+    (Frontend deferred_render, diff_gaussian_rasterization.rasterize_deferred)
+    and delivers each image once its validity flag has landed: the renders,
+    poses and counters equal the two-call path bit for bit, also when every
+    frame overflows the binning capacity or the depth-key width and is
+    re-rendered."""
+    from splatt3r_amd.slam import Frontend
+    from splatt3r_amd.splatt3r_utils import load_splatt3r
+    from splatt3r_amd.synthetic import tum_like_sequence
+    from splatt3r_amd.weights import FULL
+
+    dev = torch.device("cuda", 0)
+    model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
+    n = 8
+    frames = tum_like_sequence(n + 1, 384, 512, seed=3, step_px=2.0, device=dev)
+
+    def run(deferred, force=None, per_frame=True):
+        fe = Frontend(model, device=dev, spatial_stride=4, render=True, main_priority=-1,
+                      deferred_render=deferred)
+        if force is not None:
+            cap, bits = force
+            fe.sizing.update = lambda *a, **k: None
+            fe.sizing.capacity, fe.sizing.key_bits = cap, bits
+        poses, renders = [], []
+        for i in range(n):
+            f = fe.step(i, frames[i], next_img=[frames[i + 1]])
+            poses.append(f.T_WC.data.clone())
+            if per_frame:
+                renders.append(fe.last_render.clone())
+        fe.drain()
+        if not per_frame:
+            renders.append(fe.last_render.clone())
+        torch.cuda.synchronize()
+        st = dict(fe.stats)
+        fe.close()
+        return poses, renders, st
+
+    p0, r0, s0 = run(False)
+    assert s0["rerendered"] == 0 and s0["rendered"] == n
+    for force in (None, (1000, 32), (1 << 22, 2)):
+        p1, r1, s1 = run(True, force)
+        re = s1.pop("rerendered")
+        assert re == (0 if force is None else n), (force, re)
+        assert s1 == {k: v for k, v in s0.items() if k != "rerendered"}, force
+        for a, b in zip(p0, p1):
+            assert torch.equal(a, b)
+        for a, b in zip(r0, r1):
+            assert torch.equal(a, b), force
+    # delivery lagging behind the loop (no read between frames): same last image
+    _, r2, s2 = run(True, per_frame=False)
+    assert torch.equal(r2[-1], r0[-1]) and s2["rendered"] == n

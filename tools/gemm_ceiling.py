@@ -58,6 +58,7 @@ def main():
              for _ in range(g)]
         C = [torch.empty(M, N, device="cuda", dtype=torch.float16) for _ in range(g)]
         fl = 2.0 * M * N * K * g
+        ref = [(A[i].float() @ B[i].float().T) for i in range(g)]
         res = []
         for t in tiles:
             if t in ops._HALO:
@@ -65,6 +66,14 @@ def main():
             for sk in splits:
                 try:
                     c = ops.gemm(A, B, C, M, N, K, lda=K, split_k=sk, tile=t)
+                    for x in C:
+                        x.fill_(float("nan"))
+                    c(_lib.stream())
+                    err = max(float(((C[i].float() - ref[i]).abs().max() /
+                                     ref[i].abs().max()).item()) for i in range(g))
+                    if not err < 2e-3:
+                        print(f"  t{t}s{sk}: WRONG rel err {err:.3g}", flush=True)
+                        continue
                     us = timeit(lambda: c(_lib.stream()))
                 except Exception as e:   # tile not valid for this shape
                     print(f"  t{t}s{sk}: {type(e).__name__}: {str(e)[:80]}", flush=True)
