@@ -102,6 +102,10 @@ def _args(argv=None):
                     help="end-to-end leg: dataset read + resize_img threads")
     ap.add_argument("--e2e-writers", type=int, default=3,
                     help="end-to-end leg: render PNG writer threads")
+    ap.add_argument("--no-deferred-render", dest="deferred_render", action="store_false",
+                    help="two-call rasterizer (host read of num_rendered every frame)")
+    ap.add_argument("--no-spans", action="store_true",
+                    help="no per-frame HIP events in the timed region (no critical_path)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="encode each frame inside its own step (no side-stream overlap)")
     ap.add_argument("--dist-dry-run", action="store_true",
@@ -660,14 +664,17 @@ def main(argv=None):
     if look > 16:
         raise SystemExit("--enc-batch + --enc-ahead must be <= 16")
     # a fixed length past the timed frames: the texture (and so every frame)
-    # does not depend on the lookahead configuration
-    n_seq = nfr + 33
-    assert plan["frames_needed"] <= n_seq, plan
-    frames = tum_like_sequence(n_seq, H, W, seed=rank, step_px=2.0, device=dev)
+    # does not depend on the lookahead configuration (the same sequence as
+    # rounds 1-3); lookahead images past it (encoded by the last timed steps,
+    # never tracked) repeat its last frame
+    frames = tum_like_sequence(nfr + 16, H, W, seed=rank, step_px=2.0, device=dev)
+    if plan["frames_needed"] > frames.shape[0]:
+        pad = plan["frames_needed"] - frames.shape[0]
+        frames = torch.cat([frames, frames[-1:].expand(pad, *frames.shape[1:])])
     fe = Frontend(model, device=dev, spatial_stride=4, render=True, enc_batch=kb,
                   main_priority=a.main_priority, late_prefetch=a.late_prefetch,
                   decode_ahead=a.decode_ahead, enc_ahead=a.enc_ahead,
-                  render_async=a.render_async)
+                  render_async=a.render_async, deferred_render=a.deferred_render)
     # lookahead only below plan["cap_warm"] in warm-up, plan["cap"] when timed
     cap = [plan["cap_warm"]]
 
@@ -677,6 +684,11 @@ def main(argv=None):
         hi = i + 1 + look if cap[0] is None else min(i + 1 + look, cap[0])
         return [frames[j] for j in range(i + 1, hi)]
 
+    # every encoder batch size the run can queue (a partial last batch when
+    # --steps is not a multiple of --enc-batch, lookahead tails of the other
+    # legs): plans built and captured here, never inside a timed region
+    for b in range(1, kb + 1):
+        model.encoder.encoder_plan(b, H, W)
     for i in range(a.warmup + 1):          # frame 0 = INIT, then W tracked frames
         fe.step(i, frames[i], next_img=nxt(i))
     fe.drain()
@@ -686,7 +698,7 @@ def main(argv=None):
     cap[0] = plan["cap"]
     s0 = dict(fe.stats)
     model.encoder.events = []
-    fe.spans = []
+    fe.spans = None if a.no_spans else []
     ahead0 = dict(model.encoder.ahead_counts)
     units0 = model.encoder.plan_units()
     enc0 = _encodes(model.encoder)
@@ -703,7 +715,7 @@ def main(argv=None):
     ev = model.encoder.events
     model.encoder.events = None
     encodes = _encodes(model.encoder) - enc0
-    crit = _critical_path(fe, ev, t, a.steps)
+    crit = _critical_path(fe, ev, t, a.steps) if fe.spans is not None else None
     fe.spans = None
     net_ms = sum(e0.elapsed_time(e1) for _, e0, e1 in ev) / a.steps
     st = {k: fe.stats[k] - s0[k] for k in fe.stats}

@@ -549,32 +549,49 @@ __global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
         s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[ks], s[kb], 0, 0, 0);
       }
     }
+    // raw scores: the max of s * scale is max(s) * scale (scale > 0, exact);
+    // keys past Nk exist only in the last tile (wave-uniform test)
     float mx = -INFINITY;
+    if ((t + 1) * KT <= p.Nk) {
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+      for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool kok = t * KT + kb * 16 + 4 * grp + r < p.Nk;
-        s[kb][r] = kok ? s[kb][r] * p.scale_log2 : -INFINITY;
-        mx = fmaxf(mx, s[kb][r]);
-      }
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kb][r]);
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (t * KT + kb * 16 + 4 * grp + r >= p.Nk) s[kb][r] = -INFINITY;
+          mx = fmaxf(mx, s[kb][r]);
+        }
+    }
     mx = fmaxf(mx, xchg16(mx));
     mx = fmaxf(mx, xchg32(mx));
-    const float m_new = fmaxf(m_run, mx);
+    const float m_new = fmaxf(m_run, mx * p.scale_log2);
     const float alpha = exp2f(m_run - m_new);
     m_run = m_new;
     float ls = 0.f;
+    {
+      // the rounded product, then the difference (not one fma): the same
+      // exponent as scaling the scores first
+#pragma clang fp contract(off)
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+      for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = exp2f(s[kb][r] - m_new);
-        s[kb][r] = e;
-        ls += e;
-      }
+        for (int r = 0; r < 4; ++r) {
+          const float e = exp2f(s[kb][r] * p.scale_log2 - m_new);
+          s[kb][r] = e;
+          ls += e;
+        }
+    }
     l_run = l_run * alpha + ls;
+    // the running max of most rows stops moving after the first tiles:
+    // alpha == 1 for the whole wave skips the rescale (exact)
+    if (__any(alpha != 1.0f)) {
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) o[nb] *= alpha;
+      for (int nb = 0; nb < 4; ++nb) o[nb] *= alpha;
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       f16x8 pb;

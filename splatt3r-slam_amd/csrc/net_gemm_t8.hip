@@ -1,4 +1,4 @@
-// GEMM tiles 60, 62-66: the k_gemm tile math (LDS-DMA ring, XOR-swizzled
+// GEMM tiles 60, 62-68: the k_gemm tile math (LDS-DMA ring, XOR-swizzled
 // fragments, fused epilogues: net_gemm_kernel.hpp) with a K loop whose LDS
 // fragment reads overlap the MFMAs of the same wave.
 //
@@ -264,7 +264,7 @@ int launch_pp(const GemmP& p, hipStream_t st) {
 
 namespace s3gemm {
 int launch_t8(int tile, const GemmP& p, hipStream_t st) {
-  if (tile < 60 || tile > 66) return kNotMine;
+  if (tile < 60 || tile > 68) return kNotMine;
   if (tile == 61) return kNotMine;   // 256 x 128 with 32x32 MFMAs spills (576 B/lane)
   const bool mf16 = tile != 65;
   if (mf16 && !p.vec_epi) return launch_t1(1, p, st);
@@ -274,7 +274,9 @@ int launch_t8(int tile, const GemmP& p, hipStream_t st) {
     case 63: return launch_pp<128, 128, 2, 2, 2, 16>(p, st);   // 64 KiB: 2 workgroups per CU
     case 64: return launch_pp<192, 128, 3, 2, 2, 16>(p, st);   // wave 96 x 64
     case 65: return launch_pp<128, 128, 2, 2, 2, 32>(p, st);
-    default: return launch_pp<128, 192, 3, 2, 2, 16>(p, st);   // wave 64 x 96
+    case 66: return launch_pp<128, 192, 3, 2, 2, 16>(p, st);   // wave 64 x 96
+    case 67: return kNotMine;   // 256 x 256: the fp32 tile does not fit the 2-stage ring
+    default: return launch_pp<256, 128, 3, 4, 2, 16>(p, st);   // 8 waves, wave 64 x 64
   }
 }
 int sat_t8(int reset) { return read_sat(reset); }

@@ -324,7 +324,6 @@ def _estimate_default_intrinsics(h, w, device="cuda"):
                         dtype=torch.float32)
 
 
-@torch.inference_mode()
 class RasterSizing:
     """Binning capacity and depth-key width for the sync-free render
     (diff_gaussian_rasterization.rasterize_deferred), learnt from the frames
@@ -356,6 +355,7 @@ class RenderCheck:
         self.info, self.rerender, self.sizing = info, rerender, sizing
 
 
+@torch.inference_mode()
 def splatt3r_render(model, frame, ref_frame, K=None, target_T_WC=None, sizing=None):
     """splatt3r_utils.py:332-432 -> [1,1,3,H,W].
 

@@ -33,7 +33,7 @@ def test_timed_region_holds_exactly_steps_encodes(steps, kb, ahead):
     assert frames == list(range(len(frames)))
     # every stepped frame is encoded (frames 0 .. warmup + steps)
     assert len(frames) >= warmup + steps + 1
-    # the bench's sequence covers every lookahead image it hands over
+    # lookahead images past the bench's 16-frame tail repeat its last frame
     assert p["frames_needed"] <= warmup + steps + 1 + 33
     # timed replays come after every warm-up replay
     flags = [t for _, _, t in p["batches"]]

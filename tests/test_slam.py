@@ -444,6 +444,7 @@ def test_frontend_writes_render_pngs(tmp_path):
     fe = Frontend(model, device=dev, spatial_stride=4, render=True, render_writer=w)
     for i in range(5):
         fe.step(i, frames[i])
+    fe.drain()          # renders are delivered once validated (sync-free render)
     w.close()
     names = sorted(os.listdir(tmp_path / "renders"))
     assert names == ["gs_init_000000.png"] + [f"gs_track_{i:06d}.png" for i in range(1, 5)]
