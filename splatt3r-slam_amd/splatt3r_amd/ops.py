@@ -211,8 +211,11 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
                 # 3x3 conv with halo reuse of the input row segment (net_gemm_t6.hip)
                 40: (128, 128), 41: (256, 64), 42: (128, 128), 43: (128, 128), 45: (128, 128),
                 46: (128, 128), 47: (256, 64), 48: (128, 128), 49: (128, 128), 50: (256, 64),
-                51: (128, 128), 52: (128, 128), 53: (256, 64)}
-_TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14, 40, 42, 43, 45, 46, 48, 49, 51, 52}
+                51: (128, 128), 52: (128, 128), 53: (256, 64),
+                # k_gemm_pp: fragment reads of half a K tile overlap the MFMAs
+                # of the other half (net_gemm_t8.hip)
+                63: (128, 128), 65: (128, 128), 68: (256, 128)}
+_TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14, 40, 42, 43, 45, 46, 48, 49, 51, 52, 63, 65}
 # S3_GEMM_MF16=0: leave the 16x16x32 tile family out of the tuner (A/B)
 _EXCLUDED = set(range(21, 32)) if os.environ.get("S3_GEMM_MF16", "1") == "0" else set()
 
@@ -231,7 +234,8 @@ _TILE_RED = {1: (64, 1, 32), 2: (64, 1, 32), 3: (64, 1, 32), 4: (64, 1, 32), 5: 
              32: (64, 1, 16), 34: (64, 1, 32), 35: (64, 1, 32), 36: (64, 1, 16), 37: (64, 1, 16),
              40: (64, 1, 16), 41: (64, 1, 16), 42: (64, 1, 32), 43: (64, 1, 16),
              45: (64, 1, 32), 46: (64, 1, 16), 47: (64, 1, 16), 48: (64, 1, 32), 49: (64, 1, 16),
-             50: (64, 1, 16), 51: (64, 1, 16), 52: (64, 1, 32), 53: (64, 1, 16)}
+             50: (64, 1, 16), 51: (64, 1, 16), 52: (64, 1, 32), 53: (64, 1, 16),
+             63: (64, 1, 16), 65: (64, 1, 32), 68: (64, 1, 16)}
 _REGS_EPILOGUE = {14, 34, 35}   # the fp32 tile does not fit the LDS ring
 # K tiles in (ky, channel chunk, kx) order instead of (ky, kx, channel chunk)
 _HALO = set(range(40, 54)) - {44}
