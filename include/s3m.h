@@ -36,9 +36,13 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21,
                        int n, int fdim, int radius, int dilation_max,
                        void* stream);
 
-/* Tuning hook (not on the product path): lanes per query point of the
- * cooperative refine kernel (8, 16 = default, 32, 64); results identical. */
+/* Tuning hooks (not on the product path): lanes per query point of the
+ * refine (1 = default or 2: per-lane kernel for radius 3 / fdim 24; 8, 16,
+ * 32, 64: cooperative kernel, also used for every other radius / fdim) and
+ * the per-lane kernel's load distance in candidates (2, 3, 4 = default, 6);
+ * results identical for every setting. */
 void s3m_refine_set_lanes(int lanes);
+void s3m_refine_set_prefetch(int pf);
 
 /* Fused prep_for_iter_proj (matching.py:25-49 + image.py:5-38):
  * rays = normalize(X11); rays_with_grad = [rays, Scharr_x(rays)/32,

@@ -279,6 +279,156 @@ k_refine_coop(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21
   }
 }
 
+// Radius 3 (a 7 x 7 window per dilation level), F = 24, LPQ lanes per query
+// point (1, 2 or 4).  Candidate c = i * 7 + j is pixel (u0 - 3d + i d,
+// v0 - 3d + j d) (matching_kernels.cu:50-72: i outer, j inner; the first
+// candidate that strictly beats the running maximum wins).  Lane s of a
+// query takes the window rows j in [s RPL, s RPL + RPL) (RPL = 7, 4, 2) and
+// scores its candidates against the maximum carried in from the
+// previous levels (rows outer, columns inner: L1 reuse along a row) and
+// keeps its subset's largest score and, of those, the smallest c; a
+// log2(LPQ)-step butterfly keeps (larger score, then smaller c) -- the
+// sequential scan's choice.  Every candidate is loaded with three
+// 16-B buffer loads PF candidates ahead of the one being scored, from
+// per-level column / row byte-offset tables: an off-image candidate loads an
+// in-image pixel (its off-image coordinate's offset is 0) and is masked out
+// of the compare, so the loop has no branches.  The fp16 dot product keeps
+// the reference's rounding of every product and partial sum (packed
+// v_pk_mul_f16 products, then 24 dependent v_add_f16).
+template <int LPQ, int PF>
+__global__ void __launch_bounds__(kBlock)
+k_refine_lane(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
+              const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
+              int n, int dilation_max) {
+  constexpr int F = 24, CH = F / 8, R = 3, SIDE = 2 * R + 1;
+  constexpr int RPL = (SIDE + LPQ - 1) / LPQ;   // window rows per lane
+  constexpr int PER = SIDE * RPL;               // candidate slots per lane
+  static_assert(LPQ == 1 || LPQ == 2 || LPQ == 4, "1, 2 or 4 lanes per query");
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  typedef int i4 __attribute__((ext_vector_type(4)));
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = t / LPQ;
+  const int sub = (int)(threadIdx.x & (LPQ - 1));
+  const int64_t b = blockIdx.y;
+  if (LPQ == 1 && i >= n) return;
+  const bool live = i < n;                  // dead lanes still join the butterfly
+  const int64_t pi = b * (int64_t)n + (live ? i : 0);
+  h2 q[F / 2];
+  {
+    const i4* q4 = reinterpret_cast<const i4*>(D21 + pi * F);
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const i4 x = q4[k];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // through a scalar: this clang bit-casts a vector-element lvalue
+        // from element 0 whatever the index
+        const int xe = x[e];
+        q[k * 4 + e] = __builtin_bit_cast(h2, xe);
+      }
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<_Float16*>(D11 + b * (int64_t)h * w * F), (short)0, (int)((int64_t)h * w * F * 2),
+      0x00020000);
+  constexpr uint32_t PIX = F * 2;           // bytes per pixel
+  const uint32_t rowb = (uint32_t)w * PIX;
+  int64_t u0 = p1[pi * 2 + 0], v0 = p1[pi * 2 + 1];
+  _Float16 max_score = (_Float16)0.0f;      // Half() == 0, see k_refine
+  int64_t u_new = u0, v_new = v0;
+  for (int d = dilation_max; d > 0; --d) {
+    const int64_t ub = u0 - R * d, vb = v0 - R * d;
+    // column offsets of the whole window, row offsets of this lane's rows
+    uint32_t coff[SIDE], roff[RPL], cm = 0, rm = 0;
+#pragma unroll
+    for (int k = 0; k < SIDE; ++k) {
+      const int64_t u = ub + (int64_t)k * d;
+      const bool oc = u >= 0 && u < w;
+      coff[k] = oc ? (uint32_t)u * PIX : 0u;
+      cm |= (uint32_t)oc << k;
+    }
+#pragma unroll
+    for (int x = 0; x < RPL; ++x) {
+      const int j = sub * RPL + x;
+      const int64_t v = vb + (int64_t)j * d;
+      const bool orr = j < SIDE && v >= 0 && v < h;
+      roff[x] = orr ? (uint32_t)v * rowb : 0u;
+      rm |= (uint32_t)orr << x;
+    }
+    // slot k = x * SIDE + ii walks this lane's rows outer and the window
+    // columns inner: the 7 candidates of one row read one image row at
+    // shifts of d pixels, so a wave's loads of a row overlap in the vector
+    // L1 (~4.5 KiB of lines per row instead of 7 x 3 KiB from L2); the
+    // scan order changes, so ties are resolved on the candidate index
+    uint64_t okl = 0;                       // bit k: slot inside the image
+#pragma unroll
+    for (int x = 0; x < RPL; ++x) okl |= ((rm >> x) & 1u) ? (uint64_t)cm << (x * SIDE) : 0ull;
+    i4 rows[PF + 1][CH];
+    auto load = [&](int k, i4 (&r)[CH]) {
+      const uint32_t off = coff[k % SIDE] + roff[k / SIDE];
+#pragma unroll
+      for (int kk = 0; kk < CH; ++kk)
+        r[kk] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * kk, 0, 0);
+    };
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+      if (p < PER) load(p, rows[p]);
+    _Float16 best = max_score;
+    int best_c = -1;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (k + PF < PER) load(k + PF, rows[(k + PF) % (PF + 1)]);
+      const i4 (&cur)[CH] = rows[k % (PF + 1)];
+      // the 12 packed products first (a packed result read by the next
+      // instruction costs a wait state), then the dependent sum
+      h2 prod[F / 2];
+#pragma unroll
+      for (int kk = 0; kk < CH; ++kk)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int re = cur[kk][e];
+          prod[kk * 4 + e] = q[kk * 4 + e] * __builtin_bit_cast(h2, re);
+        }
+      _Float16 score = (_Float16)0.0f;
+#pragma unroll
+      for (int e = 0; e < F / 2; ++e) {
+        score = score + prod[e][0];
+        score = score + prod[e][1];
+      }
+      const bool ok = (okl >> k) & 1ull;
+      const int c = (k % SIDE) * SIDE + sub * RPL + k / SIDE;
+      // best_c == -1 (the carried maximum) is never displaced by a tie
+      if (ok && (score > best || (score == best && c < best_c))) {
+        best = score;
+        best_c = c;
+      }
+    }
+#pragma unroll
+    for (int m = 1; m < LPQ; m <<= 1) {
+      const _Float16 ob = __builtin_bit_cast(
+          _Float16, (short)__shfl_xor((int)__builtin_bit_cast(short, best), m, LPQ));
+      const int oc = __shfl_xor(best_c, m, LPQ);
+      // best_c == -1 only at the carried maximum, which no improving lane ties
+      if (ob > best || (ob == best && oc < best_c)) {
+        best = ob;
+        best_c = oc;
+      }
+    }
+    if (best_c >= 0) {
+      max_score = best;
+      const int ii = best_c / SIDE, jj = best_c - ii * SIDE;
+      u_new = ub + (int64_t)ii * d;
+      v_new = vb + (int64_t)jj * d;
+    }
+    u0 = u_new;
+    v0 = v_new;
+  }
+  if (live && sub == 0) {
+    p1_new[pi * 2 + 0] = u_new;
+    p1_new[pi * 2 + 1] = v_new;
+  }
+}
+
 // |x| / max(||x||, 1e-12) (F.normalize), strict order ((x0^2+x1^2)+x2^2).
 __device__ __forceinline__ void normalize3(const float* x, float* o) {
   float nrm = sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
@@ -380,12 +530,53 @@ int s3m_iter_proj(const float* rays_img_with_grad, const float* pts_3d_norm,
   return S3_OK;
 }
 
-// lanes per query point of the cooperative refine (8, 16, 32, 64; tuning
-// hook, not on the product path)
-static int g_refine_lanes = 16;
+// lanes per query point of the refine: 1, 2 or 4 (k_refine_lane, radius 3,
+// F = 24; the default is 1) or 8 / 16 / 32 / 64 (k_refine_coop), and the
+// lane kernel's load distance in candidates (2, 3, 4 or 6); tuning hooks for
+// A/B runs
+static int g_refine_lanes = 1;
+static int g_refine_pf = 4;
 extern "C" void s3m_refine_set_lanes(int lanes) {
-  g_refine_lanes = (lanes == 8 || lanes == 32 || lanes == 64) ? lanes : 16;
+  g_refine_lanes = (lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == 32 || lanes == 64)
+                       ? lanes : 1;
 }
+extern "C" void s3m_refine_set_prefetch(int pf) {
+  g_refine_pf = (pf == 2 || pf == 3 || pf == 6) ? pf : 4;
+}
+
+}  // extern "C"
+
+template <int LPQ>
+static void launch_refine_lane(const _Float16* d11, const _Float16* d21, const int64_t* p1,
+                               int64_t* p1_new, int b, int h, int w, int n, int dilation_max,
+                               hipStream_t st) {
+  dim3 grid((unsigned)s3::cdiv((int64_t)n * LPQ, kBlock), (unsigned)b);
+  switch (g_refine_pf) {
+    case 2: k_refine_lane<LPQ, 2><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max); break;
+    case 4: k_refine_lane<LPQ, 4><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max); break;
+    case 6: k_refine_lane<LPQ, 6><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max); break;
+    default: k_refine_lane<LPQ, 3><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max); break;
+  }
+}
+
+static void refine_lane(const _Float16* d11, const _Float16* d21, const int64_t* p1,
+                        int64_t* p1_new, int b, int h, int w, int n, int dilation_max,
+                        hipStream_t st) {
+  if (g_refine_lanes == 4)
+    launch_refine_lane<4>(d11, d21, p1, p1_new, b, h, w, n, dilation_max, st);
+  else if (g_refine_lanes == 2)
+    launch_refine_lane<2>(d11, d21, p1, p1_new, b, h, w, n, dilation_max, st);
+  else
+    launch_refine_lane<1>(d11, d21, p1, p1_new, b, h, w, n, dilation_max, st);
+}
+
+// the per-lane kernel: radius 3, fdim 24, one image of D11 addressable
+// with 32-bit buffer offsets
+static bool refine_lane_ok(int h, int w, int fdim, int radius) {
+  return radius == 3 && fdim == 24 && (int64_t)h * w * fdim * 2 < 0x7fffffff;
+}
+
+extern "C" {
 
 int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
                        int64_t* p1_new, int b, int h, int w, int n, int fdim,
@@ -398,8 +589,10 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* 
   auto d11 = reinterpret_cast<const _Float16*>(D11);
   auto d21 = reinterpret_cast<const _Float16*>(D21);
   const int side = 2 * radius + 1;
-  if (side * side <= 64 && (fdim == 24 || fdim == 16 || fdim == 32)) {
-    const int lanes = g_refine_lanes;
+  if (g_refine_lanes <= 4 && refine_lane_ok(h, w, fdim, radius)) {
+    refine_lane(d11, d21, p1, p1_new, b, h, w, n, dilation_max, s3::as_stream(stream));
+  } else if (side * side <= 64 && (fdim == 24 || fdim == 16 || fdim == 32)) {
+    const int lanes = g_refine_lanes <= 4 ? 16 : g_refine_lanes;
     dim3 cg((unsigned)s3::cdiv((int64_t)n * lanes, kBlock), (unsigned)b);
     auto go = [&](auto tag) {
       constexpr int F = decltype(tag)::value;

@@ -58,11 +58,8 @@ def refine_matches(D11, D21, p1, radius, dilation_max):
     n = p1.shape[1]
     if D21.shape != (b, n, f) or p1.shape != (b, n, 2):
         raise RuntimeError("refine_matches: shape mismatch")
-    p1_new = torch.zeros(b, n, 2, device=p1.device, dtype=torch.int64)
-    _lib.call("s3m_refine_matches", D11.data_ptr(), D21.data_ptr(), p1.data_ptr(),
-              p1_new.data_ptr(), b, h, w, n, f, int(radius), int(dilation_max),
-              _lib.stream(p1.device))
-    return [p1_new]
+    from splatt3r_amd.matching import refine_matches as _refine
+    return [_refine(D11, D21, p1, int(radius), int(dilation_max))]
 
 
 _lib.register({

@@ -43,6 +43,17 @@ def prep_for_iter_proj(X11, X21, idx_1_to_2_init):
     return rays, pts, p_init
 
 
+def refine_matches(D11, D21, p1, radius, dilation_max):
+    """s3m_refine_matches: contiguous fp16 D11 [b,h,w,F] / D21 [b,n,F],
+    int64 p1 [b,n,2] -> p1_new."""
+    b, h, w, f = D11.shape
+    n = D21.shape[1]
+    p1_new = torch.empty_like(p1)
+    _lib.call("s3m_refine_matches", D11.data_ptr(), D21.data_ptr(), p1.data_ptr(),
+              p1_new.data_ptr(), b, h, w, n, f, radius, dilation_max, _lib.stream(D11.device))
+    return p1_new
+
+
 def match(X11, X21, D11, D21, idx_1_to_2_init=None):
     idx_1_to_2, valid_match2 = match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init)
     return idx_1_to_2, valid_match2
@@ -71,11 +82,7 @@ def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None):
         D21h = D21 if D21.dtype == torch.float16 else D21.half()
         D11h = D11h.contiguous()
         D21h = D21h.reshape(b, n, -1).contiguous()
-        p1_new = torch.empty_like(p1)
-        _lib.call("s3m_refine_matches", D11h.data_ptr(), D21h.data_ptr(), p1.data_ptr(),
-                  p1_new.data_ptr(), b, h, w, n, D11h.shape[-1], int(cfg["radius"]),
-                  int(cfg["dilation_max"]), stream)
-        p1 = p1_new
+        p1 = refine_matches(D11h, D21h, p1, int(cfg["radius"]), int(cfg["dilation_max"]))
     idx = torch.empty(b, n, device=dev, dtype=torch.int64)
     _lib.call("s3m_pixel_to_lin", p1.data_ptr(), idx.data_ptr(), b * n, w, stream)
     return idx, valid.unsqueeze(-1)

@@ -135,12 +135,17 @@ def test_hip_refine_bitexact_vs_oracle(f):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lanes,pf", [(1, 4), (1, 6), (2, 2), (2, 4), (4, 3), (16, 3)])
 @pytest.mark.parametrize("f,radius,dil", [(24, 3, 5), (24, 2, 3), (32, 1, 2), (24, 4, 2), (8, 3, 5)])
-def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil):
-    """Quantised descriptors make many equal fp16 scores: the cooperative
-    kernel must keep the first candidate in the reference's scan order.
-    radius 4 (81 candidates) and fdim 8 take the per-lane kernel."""
+def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil, lanes, pf):
+    """Quantised descriptors make many equal fp16 scores: every kernel must
+    keep the first candidate in the reference's scan order.  lanes 1 / 2 / 4
+    = k_refine_lane with 1 / 2 / 4 lanes per query (radius 3, f 24; 1 is the
+    default; pf its load distance), 16 = k_refine_coop; radius 4 (81
+    candidates) and fdim 8 take the generic per-lane kernel.  Query points
+    up to 3 pixels off the image exercise the masked window slots."""
     import mast3r_slam_backends as be
+    from splatt3r_amd import _lib
     rng = np.random.default_rng(100 + f + radius)
     b, h, w = 2, 33, 47
     D11 = (rng.integers(-2, 3, size=(b, h, w, f)) * 0.125).astype(np.float16)
@@ -148,7 +153,13 @@ def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil):
     p1 = np.stack([rng.integers(-3, w + 3, size=(b, h * w)),
                    rng.integers(-3, h + 3, size=(b, h * w))], -1).astype(np.int64)
     ref = oracle.refine_matches(D11, D21, p1, radius, dil)
-    (out,) = be.refine_matches(_to(D11), _to(D21), _to(p1), radius, dil)
+    _lib.lib().s3m_refine_set_lanes(lanes)
+    _lib.lib().s3m_refine_set_prefetch(pf)
+    try:
+        (out,) = be.refine_matches(_to(D11), _to(D21), _to(p1), radius, dil)
+    finally:
+        _lib.lib().s3m_refine_set_lanes(1)
+        _lib.lib().s3m_refine_set_prefetch(4)
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
 
 

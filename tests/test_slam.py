@@ -58,7 +58,8 @@ def test_decode_ahead_frontend_matches_sequential():
     against the same keyframe in the tracked frame's Bp = 2 replay and used
     when no keyframe is added in between.  The tracker's pair plans are
     batch-invariant, so poses, renders, keyframes and counters equal the
-    frame-by-frame frontend bit for bit; slots are both used and dropped."""
+    frame-by-frame frontend bit for bit; slots are used here (the dropped
+    path is forced in test_decode_ahead_dropped_slots_match_sequential)."""
     from splatt3r_amd.slam import Frontend
     from splatt3r_amd.splatt3r_utils import load_splatt3r
     from splatt3r_amd.synthetic import tum_like_sequence
@@ -94,6 +95,55 @@ def test_decode_ahead_frontend_matches_sequential():
     assert c0 == {"paired": 0, "used": 0, "dropped": 0, "declined": 0}
     assert c1["paired"] > 0 and c1["used"] > 0, c1
     assert st0["tracked"] == n - 1 and st0["reloc"] == 0
+    assert kf0 == kf1 and st0 == st1
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
+    for a, b in zip(r0, r1):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_decode_ahead_dropped_slots_match_sequential():
+    """The invalidation path of decode-ahead: the pairing predictor is
+    overridden to always pair, on a sequence with enough motion to create
+    keyframes, so some slots are decoded against a keyframe that is replaced
+    before the next frame is tracked.  Those slots must be dropped (frame
+    tracked against the new keyframe), leaving poses, renders, keyframes and
+    counters bit-identical to the frame-by-frame frontend."""
+    from splatt3r_amd.slam import Frontend
+    from splatt3r_amd.splatt3r_utils import load_splatt3r
+    from splatt3r_amd.synthetic import tum_like_sequence
+    from splatt3r_amd.weights import FULL
+
+    dev = torch.device("cuda", 0)
+    model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
+    n = 16
+    frames = tum_like_sequence(n + 6, 384, 512, seed=5, step_px=6.0, device=dev)
+
+    def run(ahead):
+        kb = 2 if ahead else 1
+        fe = Frontend(model, device=dev, spatial_stride=4, render=True,
+                      enc_batch=kb, enc_ahead=3 if kb > 1 else None, decode_ahead=ahead)
+        if ahead:
+            fe._pair_likely_kept = lambda i: True
+        poses, renders = [], []
+        c0 = dict(model.encoder.ahead_counts)
+        for i in range(n):
+            nxt = [frames[j] for j in range(i + 1, min(n, i + 6))]
+            f = fe.step(i, frames[i], next_img=nxt)
+            poses.append(f.T_WC.data.clone())
+            renders.append(fe.last_render.clone())
+        torch.cuda.synchronize()
+        counts = {k: model.encoder.ahead_counts[k] - c0[k] for k in c0}
+        fe.close()
+        return poses, renders, list(fe.new_kf_frames), dict(fe.stats), counts
+
+    p0, r0, kf0, st0, c0 = run(False)
+    p1, r1, kf1, st1, c1 = run(True)
+    print("keyframes:", kf0, "slots:", c1)
+    assert len(kf0) >= 3, kf0          # the motion makes keyframes mid-sequence
+    assert c1["declined"] == 0 and c1["dropped"] > 0 and c1["used"] > 0, c1
+    assert c1["paired"] == c1["used"] + c1["dropped"], c1
     assert kf0 == kf1 and st0 == st1
     for a, b in zip(p0, p1):
         assert torch.equal(a, b)

@@ -1,11 +1,12 @@
 """Dense matching kernels at C2 size (tuning harness): per-kernel HIP-graph
-timing of prep / iter_proj / occlusion / refine_matches on a smooth synthetic
-pointmap pair.  python -m tools.bench_match"""
+timing of the whole match and of refine_matches alone, per lanes /
+load-distance variant, on a smooth synthetic pointmap pair.
+python -m tools.bench_match"""
 from __future__ import annotations
 
 import torch
 
-from splatt3r_amd import matching
+from splatt3r_amd import _lib, matching
 from tools.bench_gemm import timeit
 
 
@@ -21,22 +22,37 @@ def main():
     us = timeit(lambda: matching.match(X11, X21, D11, D21), reps=10)
     print(f"match (all kernels) {us:7.1f} us", flush=True)
     cfg = dict(matching.config["matching"])
+    r, dil = int(cfg["radius"]), int(cfg["dilation_max"])
     cfg["radius"] = 0
     us0 = timeit(lambda: matching.match_iterative_proj(X11, X21, D11, D21, cfg=cfg), reps=10)
     print(f"match without refine {us0:7.1f} us -> refine ~{us - us0:7.1f} us", flush=True)
-    import ctypes
-    from splatt3r_amd import _lib
+    idx0 = matching.match_iterative_proj(X11, X21, D11, D21, cfg=cfg)[0]
+    p1 = torch.stack((idx0 % w, idx0 // w), -1).contiguous()
+    D21r = D21.reshape(1, h * w, 24)
+    n = h * w
+    out = torch.empty_like(p1)
+
+    def plain():
+        _lib.call("s3m_refine_matches", D11.data_ptr(), D21r.data_ptr(), p1.data_ptr(),
+                  out.data_ptr(), 1, h, w, n, 24, r, dil, _lib.stream())
+
     L = _lib.lib()
-    L.s3m_refine_set_lanes.argtypes = [ctypes.c_int]
-    ref_idx = matching.match(X11, X21, D11, D21)[0].clone()
-    for lanes in (8, 16, 32, 64, 8, 16, 32, 64):
+    plain()
+    ref = out.clone()
+    for lanes, pf in ((1, 3), (16, 3), (1, 2), (1, 4), (1, 6), (2, 2), (2, 3), (2, 4),
+                      (4, 2), (4, 3), (1, 3), (16, 3)):
         L.s3m_refine_set_lanes(lanes)
-        idx = matching.match(X11, X21, D11, D21)[0]
-        same = bool(torch.equal(idx, ref_idx))
-        us_l = timeit(lambda: matching.match(X11, X21, D11, D21), reps=10)
-        print(f"refine lanes {lanes:2d}: match {us_l:7.1f} us -> refine ~{us_l - us0:7.1f} us "
-              f"(idx identical: {same})", flush=True)
-    L.s3m_refine_set_lanes(16)
+        L.s3m_refine_set_prefetch(pf)
+        line = f"refine lanes {lanes:2d} pf {pf}:"
+        for name, fn in (("refine", plain),):
+            out.fill_(-1)
+            fn()
+            same = bool(torch.equal(out, ref))
+            t = timeit(fn, reps=20)
+            line += f"  {name} {t:7.1f} us (same: {same})"
+        print(line, flush=True)
+    L.s3m_refine_set_lanes(1)
+    L.s3m_refine_set_prefetch(4)
 
 
 if __name__ == "__main__":
