@@ -37,7 +37,7 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21,
                        void* stream);
 
 /* Tuning hooks (not on the product path): lanes per query point of the
- * refine (1 = default or 2: per-lane kernel for radius 3 / fdim 24; 8, 16,
+ * refine (1, 2, 4: per-lane kernel for radius 3 / fdim 24; 8, 16 = default,
  * 32, 64: cooperative kernel, also used for every other radius / fdim) and
  * the per-lane kernel's load distance in candidates (2, 3, 4 = default, 6);
  * results identical for every setting. */

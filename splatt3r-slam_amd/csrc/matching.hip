@@ -531,14 +531,20 @@ int s3m_iter_proj(const float* rays_img_with_grad, const float* pts_3d_norm,
 }
 
 // lanes per query point of the refine: 1, 2 or 4 (k_refine_lane, radius 3,
-// F = 24; the default is 1) or 8 / 16 / 32 / 64 (k_refine_coop), and the
+// F = 24) or 8 / 16 / 32 / 64 (k_refine_coop; 16 is the default), and the
 // lane kernel's load distance in candidates (2, 3, 4 or 6); tuning hooks for
-// A/B runs
-static int g_refine_lanes = 1;
+// A/B runs.  The per-lane kernel wins when neighbouring query points have
+// neighbouring windows (129 vs 173 us at C2 on a clean 2-px shift,
+// tools/bench_match.py); on the tracking loop's matches, whose window
+// centres scatter (median row spread 3-6 px per 64 queries, 46-68 px on
+// every other call: tools/refine_stats.py), its lanes touch one cache line
+// each and the 16-lane kernel is faster (185 vs 208 us per call,
+// profiles/r04g_summary.txt)
+static int g_refine_lanes = 16;
 static int g_refine_pf = 4;
 extern "C" void s3m_refine_set_lanes(int lanes) {
-  g_refine_lanes = (lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 || lanes == 32 || lanes == 64)
-                       ? lanes : 1;
+  g_refine_lanes = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 32 || lanes == 64)
+                       ? lanes : 16;
 }
 extern "C" void s3m_refine_set_prefetch(int pf) {
   g_refine_pf = (pf == 2 || pf == 3 || pf == 6) ? pf : 4;
@@ -592,7 +598,7 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* 
   if (g_refine_lanes <= 4 && refine_lane_ok(h, w, fdim, radius)) {
     refine_lane(d11, d21, p1, p1_new, b, h, w, n, dilation_max, s3::as_stream(stream));
   } else if (side * side <= 64 && (fdim == 24 || fdim == 16 || fdim == 32)) {
-    const int lanes = g_refine_lanes <= 4 ? 16 : g_refine_lanes;
+    const int lanes = g_refine_lanes <= 4 ? 16 : g_refine_lanes;   // other radius / fdim
     dim3 cg((unsigned)s3::cdiv((int64_t)n * lanes, kBlock), (unsigned)b);
     auto go = [&](auto tag) {
       constexpr int F = decltype(tag)::value;

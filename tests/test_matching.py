@@ -140,8 +140,8 @@ def test_hip_refine_bitexact_vs_oracle(f):
 def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil, lanes, pf):
     """Quantised descriptors make many equal fp16 scores: every kernel must
     keep the first candidate in the reference's scan order.  lanes 1 / 2 / 4
-    = k_refine_lane with 1 / 2 / 4 lanes per query (radius 3, f 24; 1 is the
-    default; pf its load distance), 16 = k_refine_coop; radius 4 (81
+    = k_refine_lane with 1 / 2 / 4 lanes per query (radius 3, f 24; pf its
+    load distance), 16 = k_refine_coop (the default); radius 4 (81
     candidates) and fdim 8 take the generic per-lane kernel.  Query points
     up to 3 pixels off the image exercise the masked window slots."""
     import mast3r_slam_backends as be
@@ -158,7 +158,7 @@ def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil, lanes, pf):
     try:
         (out,) = be.refine_matches(_to(D11), _to(D21), _to(p1), radius, dil)
     finally:
-        _lib.lib().s3m_refine_set_lanes(1)
+        _lib.lib().s3m_refine_set_lanes(16)
         _lib.lib().s3m_refine_set_prefetch(4)
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
 

@@ -51,7 +51,7 @@ def main():
             t = timeit(fn, reps=20)
             line += f"  {name} {t:7.1f} us (same: {same})"
         print(line, flush=True)
-    L.s3m_refine_set_lanes(1)
+    L.s3m_refine_set_lanes(16)
     L.s3m_refine_set_prefetch(4)
 
 
