@@ -145,7 +145,9 @@ int s3n_attention(const s3n_attn_args* args, void* stream);
 
 /* Tuning hook (not on the product path), kernels for pre-rotated q/k:
  * 0 = transposed-score kernel with 2 key groups (default), 1 = the
- * P-through-LDS kernel, 2 = transposed-score with 1 key group, 3 = with 4. */
+ * P-through-LDS kernel, 2 = transposed-score with 1 key group, 3 = with 4;
+ * -1 / -2 = the transposed-score kernels' XCD-aware workgroup order off /
+ * on (default on). */
 void s3n_attention_set_variant(int variant);
 
 /* LayerNorm over the last dim C (eps), per group gamma/beta:

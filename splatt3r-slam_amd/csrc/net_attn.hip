@@ -42,7 +42,21 @@ struct AttnP {
   f16* O[S3N_MAX_GROUPS];
   int64_t os;
   float scale_log2;
+  int nqt;      // query tiles per (group, batch, head) (k_attn_st 1-D grid)
+  int xcd;      // k_attn_st: 1 = XCD-aware workgroup order
 };
+
+// Bijective XCD-aware order for a 1-D grid of n workgroups: consecutive ids
+// round-robin over the 8 XCDs (private L2 each), so id b is given logical
+// tile (b % 8)'s contiguous run + b / 8 (cdna_hip_programming.md §5 'XCD
+// swizzle must be bijective').  The query tiles of one (group, batch, head)
+// then share an XCD and read its K / V from that L2 instead of each XCD
+// fetching them.
+__device__ __forceinline__ int xcd_order(int b, int n) {
+  const int q = n / 8, r = n % 8;
+  const int xcd = b % 8, k = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
 
 __device__ __forceinline__ int kswz(int row, int c) { return c ^ ((row >> 1) & 7); }
 
@@ -468,10 +482,12 @@ __global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
   constexpr int NJ = 8 / QW;                       // K (and V) DMA pieces per wave per tile
   static_assert(QW == 1 || QW == 2 || QW == 4, "query waves");
   __shared__ __attribute__((aligned(1024))) f16 smem[SPLIT * RING];
-  const int qtile = blockIdx.x;
-  const int bh = blockIdx.y;
+  // 1-D grid: logical id = qtile + nqt * (bh + B H g)
+  const int lin = p.xcd ? xcd_order(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int qtile = lin % p.nqt;
+  const int bh = (lin / p.nqt) % (p.B * p.H);
   const int b = bh / p.H, h = bh % p.H;
-  const int g = blockIdx.z;
+  const int g = lin / (p.nqt * p.B * p.H);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sp = wid / QW, wave = wid % QW;         // key group, query wave
@@ -667,7 +683,13 @@ __global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
 }  // namespace
 
 static int g_attn_variant = 0;
-extern "C" void s3n_attention_set_variant(int v) { g_attn_variant = v; }
+static int g_attn_xcd = 1;
+// tuning hook: v >= 0 picks the kernel variant; v == -1 / -2 switches the
+// XCD-aware workgroup order of k_attn_st off / on
+extern "C" void s3n_attention_set_variant(int v) {
+  if (v == -1 || v == -2) g_attn_xcd = v == -2;
+  else g_attn_variant = v;
+}
 
 extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
   S3_REQUIRE(a && a->B > 0 && a->Nq >= 0 && a->Nk > 0 && a->H > 0, "s3n_attention: bad sizes");
@@ -692,7 +714,10 @@ extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
   p.qs = a->q_stride; p.ks = a->k_stride; p.vs = a->v_stride; p.os = a->o_stride;
   p.cosT = a->rope_cos; p.sinT = a->rope_sin; p.maxpos = a->rope_maxpos;
   p.scale_log2 = a->scale * 1.4426950408889634f;
+  p.nqt = (a->Nq + QT - 1) / QT;
+  p.xcd = g_attn_xcd;
   dim3 grid((a->Nq + QT - 1) / QT, a->B * a->H, a->groups);
+  const unsigned lin = (unsigned)(p.nqt * a->B * a->H * a->groups);
   bool rope = false;
   for (int g = 0; g < a->groups; ++g) rope = rope || p.qpos[g] || p.kpos[g];
   if (rope)
@@ -700,16 +725,17 @@ extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
   else if (g_attn_variant == 1)
     k_attn_dma<<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
   else if (g_attn_variant == 2)
-    k_attn_st<4, 1, kStages><<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+    k_attn_st<4, 1, kStages><<<lin, kThreads, 0, s3::as_stream(stream)>>>(p);
   else if (g_attn_variant == 3)
-    k_attn_st<4, 4, 2><<<grid, kThreads * 4, 0, s3::as_stream(stream)>>>(p);
+    k_attn_st<4, 4, 2><<<lin, kThreads * 4, 0, s3::as_stream(stream)>>>(p);
   else if (g_attn_variant == 4) {
     // 32-query workgroups (2 query waves): twice the workgroups per head
     // (in-graph 0.83 vs 0.75 ms/frame for the default: not used)
-    dim3 g32((a->Nq + 31) / 32, a->B * a->H, a->groups);
-    k_attn_st<2, 2, 2><<<g32, 64 * 2 * 2, 0, s3::as_stream(stream)>>>(p);
+    p.nqt = (a->Nq + 31) / 32;
+    k_attn_st<2, 2, 2><<<(unsigned)(p.nqt * a->B * a->H * a->groups), 64 * 2 * 2, 0,
+                         s3::as_stream(stream)>>>(p);
   } else
-    k_attn_st<4, 2, 2><<<grid, kThreads * 2, 0, s3::as_stream(stream)>>>(p);
+    k_attn_st<4, 2, 2><<<lin, kThreads * 2, 0, s3::as_stream(stream)>>>(p);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }

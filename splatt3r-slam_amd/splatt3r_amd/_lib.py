@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import time
 import threading
 
 import torch  # noqa: F401  (must be loaded before the HIP library, see above)
@@ -96,6 +97,34 @@ def check(status: int, what: str = "") -> None:
 def call(name: str, *args) -> None:
     """Call an s3_status-returning entry point and raise on failure."""
     check(getattr(lib(), name)(*args), name)
+
+
+# S3_SPIN_SYNC=0: blocking stream synchronize in wait_stream (A/B)
+_SPIN_SYNC = os.environ.get("S3_SPIN_SYNC", "1") != "0"
+
+
+def wait_stream(device: torch.device | None = None) -> None:
+    """Host wait for the work queued so far on the current stream.  Polls an
+    event (yielding the GIL between polls) instead of a blocking
+    synchronize: the blocking wait's wake-up latency is device idle time in
+    the frame loop, since the next launches are issued only after it
+    returns."""
+    s = torch.cuda.current_stream(device)
+    if not _SPIN_SYNC:
+        s.synchronize()
+        return
+    ev = torch.cuda.Event()
+    ev.record(s)
+    wait_event(ev)
+
+
+def wait_event(ev) -> None:
+    """Host wait for a recorded event (polled, see wait_stream)."""
+    if not _SPIN_SYNC:
+        ev.synchronize()
+        return
+    while not ev.query():
+        time.sleep(0)
 
 
 def stream(device: torch.device | None = None) -> int:

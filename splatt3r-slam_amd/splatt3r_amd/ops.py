@@ -102,6 +102,10 @@ GRAPHS_ENABLED = os.environ.get("S3_GRAPHS", "1") != "0"
 # S3_ATTN_VARIANT=<n>: the no-RoPE attention kernel variant (net_attn.hip
 # s3n_attention_set_variant; experiments only)
 ATTN_VARIANT = int(os.environ["S3_ATTN_VARIANT"]) if "S3_ATTN_VARIANT" in os.environ else None
+# S3_ATTN_XCD=0: attention workgroups in plain grid order (A/B of the
+# XCD-aware order; experiments only)
+if os.environ.get("S3_ATTN_XCD", "1") == "0":
+    _lib.lib().s3n_attention_set_variant(-1)
 # S3_GEMM_XCD=1: tiles placed on the XCDs by the band split only (A/B of the
 # 2-D XCD partition, net_gemm.hip; experiments only)
 if os.environ.get("S3_GEMM_XCD", "0") == "1":

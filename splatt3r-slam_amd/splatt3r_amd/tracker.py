@@ -163,7 +163,7 @@ class NormalEquations:
         self.host.copy_(self.out, non_blocking=True)
 
     def fetch(self):
-        torch.cuda.current_stream(self.device).synchronize()
+        _lib.wait_stream(self.device)
         return self.unpack(self.host.numpy())
 
     @staticmethod
@@ -178,6 +178,11 @@ class NormalEquations:
         self.set_pose_host(T)
         self.launch(Xf, Xk, Q, valid, sigma_ray, sigma_dist, huber_k)
         return self.fetch()
+
+
+# S3_GN_EVENT_WAIT=0: the tracker's decision wait also covers the render
+# queued behind the GN chunk (A/B)
+_GN_EVENT_WAIT = os.environ.get("S3_GN_EVENT_WAIT", "1") != "0"
 
 
 def solve_normal_eqs(H, g):
@@ -260,9 +265,17 @@ class FrameTracker:
         ne.pose.copy_(T_CkCf.data.reshape(8))
         ne.gn_begin(self.cfg)
         ne.gn_queue(Xf, Xk, Q, valid_c, self.cfg, GN_CHUNK, calib)
+        # the host waits for the GN chunk and the statistics copies only: the
+        # render queued by before_sync keeps the device busy while the host
+        # runs the post-GN glue and issues the next launches
+        gn_done = torch.cuda.Event()
+        gn_done.record(torch.cuda.current_stream(ne.device))
         if before_sync is not None:
             self.spec = before_sync(T_WCk * lietorch.Sim3(ne.pose.clone().view(1, 8)))
-        torch.cuda.current_stream(ne.device).synchronize()
+        if _GN_EVENT_WAIT:
+            _lib.wait_event(gn_done)
+        else:
+            _lib.wait_stream(ne.device)
         n_opt, n_kf, n_unique = stats_host.tolist()
 
         if n_opt / n < self.cfg["min_match_frac"]:
@@ -335,7 +348,7 @@ class FrameTracker:
             if flag != 0 or iters >= cfg["max_iters"]:
                 break
             ne.gn_queue(Xf, Xk, Q, valid, cfg, min(GN_CHUNK, cfg["max_iters"] - iters), calib)
-            torch.cuda.current_stream(ne.device).synchronize()
+            _lib.wait_stream(ne.device)
             extra += 1
         self.spec_valid = extra == 0
         self.last_iters = iters
@@ -360,7 +373,7 @@ class FrameTracker:
         ne.pose.copy_(T_CkCf.data.reshape(8))
         ne.gn_begin(self.cfg)
         ne.gn_queue(Xf, Xk, Q, valid, self.cfg, GN_CHUNK)
-        torch.cuda.current_stream(ne.device).synchronize()
+        _lib.wait_stream(ne.device)
         return self._gn_finish(Xf, Xk, Q, valid, T_WCk)
 
     def opt_pose_calib_sim3(self, Xf, Xk, T_WCf, T_WCk, Qk, valid, K, img_size):
@@ -379,7 +392,7 @@ class FrameTracker:
         ne.pose.copy_(T_CkCf.data.reshape(8))
         ne.gn_begin(self.cfg)
         ne.gn_queue(Xf, Xk, Q, valid, self.cfg, GN_CHUNK, calib)
-        torch.cuda.current_stream(ne.device).synchronize()
+        _lib.wait_stream(ne.device)
         return self._gn_finish(Xf, Xk, Q, valid, T_WCk, calib)
 
     def opt_pose_ray_dist_sim3_host(self, Xf, Xk, T_WCf, T_WCk, Qk, valid):

@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 4: attention QB variants, plan fork (kv GEMM / head MLP on a side stream) A/B
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python3 -m tools.bench_attn > gpurun_out/r04i_attn.log 2>&1 || { tail -20 gpurun_out/r04i_attn.log; exit 1; }
+grep " us " gpurun_out/r04i_attn.log
+timeout -k 10 900 python -u -m pytest tests/test_tracker.py tests/test_net.py tests/test_slam.py -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/r04i_tests.log 2>&1 || { tail -40 gpurun_out/r04i_tests.log; exit 1; }
+tail -2 gpurun_out/r04i_tests.log
+OFF="--no-e2e --no-pairs --no-backend --no-map --no-c3 --no-cpu-baseline --no-kprof --no-live"
+for rep in 1 2; do
+for fork in 1 0; do
+  S3_PLAN_FORK=$fork timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 $OFF > gpurun_out/r04i_one.log 2>&1 || { tail -20 gpurun_out/r04i_one.log; exit 1; }
+  grep '^{' gpurun_out/r04i_one.log | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); c=d['critical_path']
+print('fork=$fork', round(d['value'],1), round(d['ms_per_step'],3), 'net', round(c['main_network_ms'],3), 'other', round(c['main_other_ms'],3), 'idle', round(c['main_idle_ms'],3))"
+done
+done
