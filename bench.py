@@ -488,6 +488,7 @@ def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, wri
         writer.flush()
         t = time.perf_counter() - t0
         st = {k: fe.stats[k] - s0[k] for k in fe.stats}
+        fe.close()
         loader.close()
         writer.close()
         written = len(os.listdir(os.path.join(root, "renders")))
@@ -589,8 +590,14 @@ def bench_live(model, dev, frames, steps, warmup, main_priority=-1):
     fe = Frontend(model, device=dev, spatial_stride=4, render=True, enc_batch=1,
                   decode_ahead=False, main_priority=main_priority)
     lat = []
+    prof = None
+    if os.environ.get("S3_PROFILE_LIVE"):      # host cProfile of the timed frames (diagnostic)
+        import cProfile
+        prof = cProfile.Profile()
     try:
         for i in range(warmup + 1 + steps):
+            if prof is not None and i == warmup + 1:
+                prof.enable()
             torch.cuda.synchronize()
             if i == warmup + 1:
                 s0 = dict(fe.stats)
@@ -603,6 +610,14 @@ def bench_live(model, dev, frames, steps, warmup, main_priority=-1):
         st = {k: fe.stats[k] - s0[k] for k in fe.stats}
     finally:
         fe.close()
+    if prof is not None:
+        import io
+        import pstats
+        import sys
+        prof.disable()
+        out = io.StringIO()
+        pstats.Stats(prof, stream=out).sort_stats("tottime").print_stats(25)
+        print(out.getvalue(), file=sys.stderr)
     ms = np.sort(np.array(lat) * 1e3)
     return {"frames_per_s": len(lat) / float(np.sum(lat)), "steps": len(lat),
             "latency_ms": {"p50": float(np.percentile(ms, 50)),

@@ -678,7 +678,10 @@ class Plan:
             self.run()  # warm-up outside capture (module load, lazy init)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread-local capture: a plan built lazily inside the frame loop is
+        # captured while loader / PNG-writer threads wait on their own
+        # events, which would invalidate a global-mode capture
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self.run()
         self.graph = g
         return g

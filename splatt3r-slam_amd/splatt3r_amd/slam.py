@@ -46,6 +46,23 @@ from splatt3r_amd.tracker import FrameTracker
 __all__ = ["Frontend", "should_append_gaussians", "lookahead_batches"]
 
 
+_STREAMS: dict = {}
+
+
+def _shared_stream(device, priority, role):
+    """One HIP stream per (device, priority, role) for the whole process:
+    Frontends created one after another (bench legs, tests) reuse the same
+    streams instead of creating two or three more each; every new stream is
+    mapped onto one of the process's few hardware queues (GPU_MAX_HW_QUEUES),
+    and a frontend whose streams came late in that assignment ran its
+    frames ~1.6x slower (tools/live_ab.py, profiles/r04k_live_ab.log)."""
+    key = (str(torch.device(device)), int(priority), role)
+    s = _STREAMS.get(key)
+    if s is None:
+        s = _STREAMS[key] = torch.cuda.Stream(device=device, priority=int(priority))
+    return s
+
+
 def _clear_ahead_slot(model):
     enc = getattr(model, "encoder", None)
     if enc is not None and getattr(enc, "_ahead_slot", None) is not None:
@@ -115,7 +132,7 @@ class _RenderWorker:
     DECISION_TIMEOUT_S = 60.0
 
     def __init__(self, device):
-        self.stream = torch.cuda.Stream(device=device)
+        self.stream = _shared_stream(device, 0, "render")
         self.q: queue.Queue = queue.Queue()
         self.error = None
         self.timeouts = 0          # renders dropped for want of a decision (drain raises)
@@ -219,7 +236,7 @@ class Frontend:
         self._rb_i = 0
         self._rb_event = None
         self.fps_timer = None
-        self.enc_stream = torch.cuda.Stream(device=device) if torch.cuda.is_available() else None
+        self.enc_stream = _shared_stream(device, 0, "encoder") if torch.cuda.is_available() else None
         self._queue = {}           # frame index -> (Frame whose encoder is queued, done event)
         self.enc_batch = enc_batch # images per encoder replay when lookahead frames are given
         # frames kept queued ahead of the current one (None: queue the next
@@ -257,7 +274,7 @@ class Frontend:
         # main chain on a stream of its own priority (the encoder side stream
         # keeps the default one): the dispatcher then prefers the frame's
         # critical path and the encoder fills the CUs it leaves idle
-        self.main_stream = (torch.cuda.Stream(device=device, priority=main_priority)
+        self.main_stream = (_shared_stream(device, main_priority, "main")
                             if main_priority is not None and self.enc_stream is not None else None)
 
     def _prefetch(self, i, imgs):
