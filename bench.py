@@ -717,14 +717,28 @@ def main(argv=None):
     ahead0 = dict(model.encoder.ahead_counts)
     units0 = model.encoder.plan_units()
     enc0 = _encodes(model.encoder)
+    hprof = None
+    if os.environ.get("S3_PROFILE_HOST"):  # host cProfile of the timed region (diagnostic)
+        import cProfile
+        hprof = cProfile.Profile()
     _barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if hprof is not None:
+        hprof.enable()
     for i in range(a.warmup + 1, nfr):
         fe.step(i, frames[i], next_img=nxt(i))
     fe.drain()                             # every frame's render issued
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
+    if hprof is not None:
+        import io
+        import pstats
+        hprof.disable()
+        for key in ("tottime", "cumulative"):
+            out = io.StringIO()
+            pstats.Stats(hprof, stream=out).sort_stats(key).print_stats(45)
+            print(out.getvalue(), file=__import__("sys").stderr)
     _barrier(ws)
     t_max = _max_over_ranks(t, ws, dev)
     ev = model.encoder.events

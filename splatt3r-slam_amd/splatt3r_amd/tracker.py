@@ -234,7 +234,9 @@ class FrameTracker:
         keyframe = self.keyframes.last_keyframe()
         idx_f2k, valid_match_k, Xff, Cff, Qff, Xkf, Ckf, Qkf = splatt3r_match_asymmetric(
             self.model, frame, keyframe, idx_i2j_init=self.idx_f2k, ahead=ahead)
-        self.idx_f2k = idx_f2k.clone()
+        # matching.match returns a fresh tensor that nothing writes later, so
+        # the reference's clone (tracker.py:40) is not needed to keep it
+        self.idx_f2k = idx_f2k
         idx_f2k = idx_f2k[0]
         valid_match_k = valid_match_k[0]
         frame.update_pointmap(Xff, Cff)
@@ -252,7 +254,11 @@ class FrameTracker:
         Xf, Qk, valid_opt, stats = track_prep(idx_f2k, valid_match_k, Xf_all, Cf_all, Ck, Qff,
                                               Qkf, self.cfg["C_conf"], self.cfg["Q_conf"])
         n = valid_opt.numel()
-        stats_host = torch.empty(3, dtype=torch.int64, pin_memory=True)
+        # pinned mirror reused frame to frame: the host reads it before the
+        # next frame's copy is queued
+        if getattr(self, "_stats_host", None) is None:
+            self._stats_host = torch.empty(3, dtype=torch.int64, pin_memory=True)
+        stats_host = self._stats_host
         stats_host.copy_(stats, non_blocking=True)
         # queue the first GN chunk at the device-side relative pose, then one
         # sync covers the decision statistics and (usually) the whole GN
