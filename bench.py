@@ -565,6 +565,8 @@ def _critical_path(fe, net_events, wall_s, steps):
            "source": "HIP events on the main / encoder streams over the timed region"}
     out["sum_ms"] = (out["main_network_ms"] + out["main_other_ms"] + out["main_idle_ms"]
                      + out["edge_ms"])
+    # main-stream idle between consecutive frames' chains, per frame
+    out["idle_gaps_ms"] = [round(a[1].elapsed_time(b[0]), 3) for a, b in zip(mains, mains[1:])]
     return out
 
 
@@ -717,6 +719,13 @@ def main(argv=None):
     ahead0 = dict(model.encoder.ahead_counts)
     units0 = model.encoder.plan_units()
     enc0 = _encodes(model.encoder)
+    if os.environ.get("S3_GC_FREEZE", "1") != "0":
+        # the warm-up's objects (plans, frames, tensors) leave the collected
+        # generations: a garbage collection inside the timed region then
+        # walks only what the timed frames allocate
+        import gc
+        gc.collect()
+        gc.freeze()
     hprof = None
     if os.environ.get("S3_PROFILE_HOST"):  # host cProfile of the timed region (diagnostic)
         import cProfile
@@ -782,6 +791,9 @@ def main(argv=None):
                             "reloc": st["reloc"],
                             "decode_ahead": ahead,
                             "rendered": st["rendered"], "tracked": st["tracked"],
+                            # sync-free renders that did not fit the learnt
+                            # capacity / key width and were re-rendered
+                            "rerendered": st.get("rerendered", 0),
                             # a lost frame (RELOC) in this frontend-only loop would
                             # turn later frames into untracked mono inferences
                             "tracking_complete": st["tracked"] == a.steps and st["reloc"] == 0},

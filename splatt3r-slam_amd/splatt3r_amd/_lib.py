@@ -118,13 +118,21 @@ def wait_stream(device: torch.device | None = None) -> None:
     wait_event(ev)
 
 
+# S3_SPIN_YIELD=0: poll without yielding the CPU between polls (A/B)
+_SPIN_YIELD = os.environ.get("S3_SPIN_YIELD", "1") != "0"
+
+
 def wait_event(ev) -> None:
     """Host wait for a recorded event (polled, see wait_stream)."""
     if not _SPIN_SYNC:
         ev.synchronize()
         return
-    while not ev.query():
-        time.sleep(0)
+    if _SPIN_YIELD:
+        while not ev.query():
+            time.sleep(0)
+    else:
+        while not ev.query():
+            pass
 
 
 def stream(device: torch.device | None = None) -> int:

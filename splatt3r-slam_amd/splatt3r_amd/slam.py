@@ -179,6 +179,7 @@ class _RenderWorker:
 
 
 class Frontend:
+    _INFO_RING = 16
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
                  readback=True, enc_batch=1, main_priority=None, late_prefetch=False,
@@ -261,6 +262,8 @@ class Frontend:
         # to the host behind it, shows it fitted the binning capacity
         # (re-rendered with the two-call path otherwise), in frame order
         self.sizing = RasterSizing() if deferred_render else None
+        self._info_ring = None     # pinned {status, instances, key bits} mirrors
+        self._info_i = 0
         self._pending: list = []
         self._tickets: list = []
         # min(match_frac_k, unique_frac_f) of the frames tracked against the
@@ -444,7 +447,16 @@ class Frontend:
             self._stats["rendered"] += 1
         chk = getattr(img, "_gsr_check", None)
         if chk is not None:
-            info = torch.empty(3, dtype=torch.int64, pin_memory=True)
+            # pinned flag mirrors from a fixed ring (a pinned allocation in
+            # the frame loop can stall the host for milliseconds); a slot is
+            # reused only after its render has been delivered
+            if self._info_ring is None:
+                self._info_ring = [torch.empty(3, dtype=torch.int64, pin_memory=True)
+                                   for _ in range(self._INFO_RING)]
+            while len(self._pending) >= self._INFO_RING:
+                self._deliver_one(block=True)
+            info = self._info_ring[self._info_i]
+            self._info_i = (self._info_i + 1) % self._INFO_RING
             info.copy_(chk.info, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
@@ -458,18 +470,23 @@ class Frontend:
         for it unless `block`), re-rendered by the two-call path if it did
         not fit."""
         while self._pending:
-            img, chk, info, ev, index, prefix = self._pending[0]
-            if not block and not ev.query():
+            if not self._deliver_one(block):
                 return
-            ev.synchronize()
-            self._pending.pop(0)
-            status, total, bits = (int(v) for v in info.tolist())
-            chk.sizing.update(total, bits)
-            if status != 0:
-                chk.sizing.rerenders += 1
-                self._stats["rerendered"] += 1
-                img = chk.rerender()
-            self._deliver_image(img, index, prefix)
+
+    def _deliver_one(self, block: bool) -> bool:
+        img, chk, info, ev, index, prefix = self._pending[0]
+        if not block and not ev.query():
+            return False
+        ev.synchronize()
+        self._pending.pop(0)
+        status, total, bits = (int(v) for v in info.tolist())
+        chk.sizing.update(total, bits)
+        if status != 0:
+            chk.sizing.rerenders += 1
+            self._stats["rerendered"] += 1
+            img = chk.rerender()
+        self._deliver_image(img, index, prefix)
+        return True
 
     def _deliver_image(self, img, index, prefix):
         if img is not None:

@@ -327,9 +327,12 @@ def _estimate_default_intrinsics(h, w, device="cuda"):
 class RasterSizing:
     """Binning capacity and depth-key width for the sync-free render
     (diff_gaussian_rasterization.rasterize_deferred), learnt from the frames
-    already validated: capacity 1.25 x the most instances seen + 64k, key
-    width the widest seen + 1 bit.  Before the first validated frame the
-    render takes the two-call path (one host read)."""
+    already validated: capacity 1.25 x the most instances seen + 64k rounded
+    up to a power of two (the binning buffer is then re-allocated only when
+    the count crosses one, not whenever it sets a new maximum: a device
+    allocation in the frame loop stalls the host), key width the widest seen
+    + 1 bit.  Before the first validated frame the render takes the two-call
+    path (one host read)."""
 
     def __init__(self):
         self.capacity = None
@@ -340,7 +343,8 @@ class RasterSizing:
 
     def update(self, total: int, bits=None):
         self.max_total = max(self.max_total, int(total))
-        self.capacity = int(self.max_total * 1.25) + 65536
+        need = int(self.max_total * 1.25) + 65536
+        self.capacity = 1 << (need - 1).bit_length()
         if bits is not None:
             self.max_bits = max(self.max_bits, int(bits))
             self.key_bits = min(32, self.max_bits + 1)
