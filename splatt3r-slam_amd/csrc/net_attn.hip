@@ -480,7 +480,7 @@ template <int QW, int SPLIT, int STAGES>
 __global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
   constexpr int RING = STAGES * 2 * KT * D;        // fp16 elements per group
   constexpr int NJ = 8 / QW;                       // K (and V) DMA pieces per wave per tile
-  static_assert(QW == 1 || QW == 2 || QW == 4, "query waves");
+  static_assert(QW == 1 || QW == 2 || QW == 4 || QW == 8, "query waves");
   __shared__ __attribute__((aligned(1024))) f16 smem[SPLIT * RING];
   // 1-D grid: logical id = qtile + nqt * (bh + B H g)
   const int lin = p.xcd ? xcd_order(blockIdx.x, gridDim.x) : (int)blockIdx.x;
@@ -637,7 +637,7 @@ __global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
     // merge the key groups: groups 1.. publish (m, l, O) per lane, group 0
     // rescales to the common max and sums
     constexpr int REC = 18;                        // m, l, 16 O values
-    static_assert(SPLIT * QW * 64 * REC * 4 <= SPLIT * RING * 2, "merge scratch");
+    static_assert((SPLIT - 1) * QW * 64 * REC * 4 <= SPLIT * RING * 2, "merge scratch");
     float* xs = reinterpret_cast<float*>(smem);
     __syncthreads();                               // all rings drained
     if (sp > 0) {
@@ -733,6 +733,12 @@ extern "C" int s3n_attention(const s3n_attn_args* a, void* stream) {
     // (in-graph 0.83 vs 0.75 ms/frame for the default: not used)
     p.nqt = (a->Nq + 31) / 32;
     k_attn_st<2, 2, 2><<<(unsigned)(p.nqt * a->B * a->H * a->groups), 64 * 2 * 2, 0,
+                         s3::as_stream(stream)>>>(p);
+  } else if (g_attn_variant == 5) {
+    // 128-query workgroups (8 query waves x 2 key groups, 1024 threads):
+    // half the workgroups, each K / V tile feeds twice the queries
+    p.nqt = (a->Nq + 127) / 128;
+    k_attn_st<8, 2, 2><<<(unsigned)(p.nqt * a->B * a->H * a->groups), 64 * 8 * 2, 0,
                          s3::as_stream(stream)>>>(p);
   } else
     k_attn_st<4, 2, 2><<<lin, kThreads * 2, 0, s3::as_stream(stream)>>>(p);

@@ -23,7 +23,8 @@ def main():
         fl = 4 * B * H * N * N * 64 * g
         ref = None
         for v, name in ((0, "default xcd"), (-1, "default plain"), (-2, "default xcd"),
-                        (2, "1 key group"), (3, "4 key groups"), (0, "default")):
+                        (2, "1 key group"), (3, "4 key groups"), (5, "128-query WG"),
+                        (0, "default")):
             L.s3n_attention_set_variant(v)
             if v == -1:
                 L.s3n_attention_set_variant(0)
