@@ -735,8 +735,12 @@ def main(argv=None):
     t0 = time.perf_counter()
     if hprof is not None:
         hprof.enable()
+    host_ms = []
+    ms0 = torch.cuda.memory_stats(dev)
     for i in range(a.warmup + 1, nfr):
+        h0 = time.perf_counter()
         fe.step(i, frames[i], next_img=nxt(i))
+        host_ms.append(round((time.perf_counter() - h0) * 1e3, 3))
     fe.drain()                             # every frame's render issued
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
@@ -754,6 +758,13 @@ def main(argv=None):
     model.encoder.events = None
     encodes = _encodes(model.encoder) - enc0
     crit = _critical_path(fe, ev, t, a.steps) if fe.spans is not None else None
+    if crit is not None:
+        crit["host_step_ms"] = host_ms      # host time inside each Frontend.step
+        # device allocations (caching-allocator segments) made by the timed frames
+        ms1 = torch.cuda.memory_stats(dev)
+        crit["segments_allocated"] = {
+            k: ms1.get(f"segment.{k}.allocated", 0) - ms0.get(f"segment.{k}.allocated", 0)
+            for k in ("small_pool", "large_pool")}
     fe.spans = None
     net_ms = sum(e0.elapsed_time(e1) for _, e0, e1 in ev) / a.steps
     st = {k: fe.stats[k] - s0[k] for k in fe.stats}
