@@ -173,9 +173,10 @@ k_finalize(const double* __restrict__ state, const float* __restrict__ partial, 
 // equations, tau = H^-1 g, T <- Exp(tau) * T, convergence flags.
 // state: [0] previous cost (starts +inf), [1] iterations done, [2] flag
 // (0 running, 1 converged, 2 Cholesky failed, 3 max iterations), [3] cost.
-__device__ __forceinline__ void gn_update(const float* out36, float* __restrict__ T,
-                                          double* __restrict__ state, int max_iters,
-                                          float rel_error, float delta_norm) {
+__global__ void k_gn_solve(const float* __restrict__ out36, float* __restrict__ T,
+                           double* __restrict__ state, int max_iters, float rel_error,
+                           float delta_norm) {
+  if (threadIdx.x != 0 || state[2] != 0.0) return;
   double H[7][7], g[7];
   int q = 0;
   for (int a = 0; a < 7; ++a)
@@ -225,55 +226,10 @@ __device__ __forceinline__ void gn_update(const float* out36, float* __restrict_
   else if (it >= max_iters) state[2] = 3.0;
 }
 
-// k_finalize + k_gn_solve in one launch of one workgroup (device GN loop):
-// every thread loads its block rows of all 36 partial sums first (the same
-// per-thread order over blocks as k_finalize), then one butterfly per value
-// and the 4 wave sums in k_finalize's order, so `out36` and the solve are
-// bit-identical to the two launches.
-__global__ void __launch_bounds__(kThreads)
-k_finalize_solve(const float* __restrict__ partial, int nblocks, float* __restrict__ out36,
-                 float* __restrict__ T, double* __restrict__ state, int max_iters,
-                 float rel_error, float delta_norm) {
-  if (state[2] != 0.0) return;
-  double acc[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += kThreads) {
-    const float4* row = reinterpret_cast<const float4*>(partial + (int64_t)b * NV);
-#pragma unroll
-    for (int c = 0; c < NV / 4; ++c) {
-      const float4 v = row[c];
-      acc[4 * c + 0] += (double)v.x;
-      acc[4 * c + 1] += (double)v.y;
-      acc[4 * c + 2] += (double)v.z;
-      acc[4 * c + 3] += (double)v.w;
-    }
-  }
-  __shared__ double wred[kThreads / 64][NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    double v = acc[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6][k] = v;
-  }
-  __syncthreads();
-  __shared__ float sums[NV];
-  if (threadIdx.x < NV) {
-    const int k = threadIdx.x;
-    sums[k] = (float)((wred[0][k] + wred[1][k]) + (wred[2][k] + wred[3][k]));
-    out36[k] = sums[k];
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  gn_update(sums, T, state, max_iters, rel_error, delta_norm);
-}
-
 int blocks_for(int64_t n) {
   int64_t b = s3::cdiv(n, kThreads);
   return (int)(b < kMaxBlocks ? (b > 0 ? b : 1) : kMaxBlocks);
 }
-static_assert(NV % 4 == 0, "float4 partial rows (k_finalize_solve)");
 
 }  // namespace
 
@@ -314,8 +270,9 @@ extern "C" int s3t_gn_iterations(const float* Xf, const float* Xk, const float* 
                                                    1.0f / sigma_ray, 1.0f / sigma_dist, huber_k,
                                                    CalibP{}, partial);
     S3_LAUNCH_CHECK();
-    k_finalize_solve<<<1, kThreads, 0, st>>>(partial, nb, out36, T, state, max_iters, rel_error,
-                                             delta_norm);
+    k_finalize<<<NV, kThreads, 0, st>>>(state, partial, nb, out36);
+    S3_LAUNCH_CHECK();
+    k_gn_solve<<<1, 64, 0, st>>>(out36, T, state, max_iters, rel_error, delta_norm);
     S3_LAUNCH_CHECK();
   }
   return S3_OK;
@@ -377,8 +334,9 @@ extern "C" int s3t_gn_iterations_calib(const float* Xf, const float* Xk, const f
                                                  1.0f / sigma_pixel, 1.0f / sigma_depth,
                                                  huber_k, cp, partial);
     S3_LAUNCH_CHECK();
-    k_finalize_solve<<<1, kThreads, 0, st>>>(partial, nb, out36, T, state, max_iters, rel_error,
-                                             delta_norm);
+    k_finalize<<<NV, kThreads, 0, st>>>(state, partial, nb, out36);
+    S3_LAUNCH_CHECK();
+    k_gn_solve<<<1, 64, 0, st>>>(out36, T, state, max_iters, rel_error, delta_norm);
     S3_LAUNCH_CHECK();
   }
   return S3_OK;
