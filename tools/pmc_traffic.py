@@ -35,7 +35,8 @@ from collections import defaultdict
 
 
 def _family(name: str) -> str:
-    m = re.search(r"k_gemm<(\d+), (\d+), \d+, \d+, (\d+),", name)
+    # k_gemm / k_gemm_pp <BM, BN, NWM, NWN, AMODE, ...>: AMODE 0 = dense
+    m = re.search(r"k_gemm(?:_pp)?<(\d+), (\d+), \d+, \d+, (\d+),", name)
     if m:
         return "gemm_dense" if m.group(3) == "0" else "gemm_conv"
     if "k_conv3_halo" in name:        # halo-reuse conv tiles: the conv GEMM family
