@@ -504,10 +504,22 @@ __device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int 
     // fused 1x1 tail: out[row, o] = sum_k v[row, k] w[o, k] + b[o] (fp32
     // activations, fp16 weights, fp32 accumulation), 8 outputs per thread.
     // The tail weights sit behind the staged tile in LDS when they fit.
+    // (converted to fp32 once, so the product loop has no conversions:
+    // (float)w is exact, the same fma chain)
     constexpr int kWOff = BM * LDT * 4;
-    constexpr bool kWLds = kWOff + 16 * BN * 2 <= RING_BYTES;
+    constexpr bool kWLds32 = kWOff + 16 * BN * 4 <= RING_BYTES;
+    constexpr bool kWLds = !kWLds32 && kWOff + 16 * BN * 2 <= RING_BYTES;
     const f16* wsrc = tw;
-    if constexpr (kWLds) {
+    float* wl32 = reinterpret_cast<float*>(reinterpret_cast<char*>(stage) + kWOff);
+    if constexpr (kWLds32) {
+      for (int i = tid * 8; i < p.tail_n * BN; i += NT * 8) {
+        const f16x8 w8 = *reinterpret_cast<const f16x8*>(tw + i);
+        float w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = (float)w8[j];
+        store8_f32(wl32 + i, w);
+      }
+    } else if constexpr (kWLds) {
       f16* wl = reinterpret_cast<f16*>(reinterpret_cast<char*>(stage) + kWOff);
       for (int i = tid * 8; i < p.tail_n * BN; i += NT * 8)
         *reinterpret_cast<f16x8*>(wl + i) = *reinterpret_cast<const f16x8*>(tw + i);
@@ -528,9 +540,16 @@ __device__ __forceinline__ void epilogue_vec(const GemmP& p, int g, int m0, int 
         load8(stage + rl * LDT + k, x);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const f16x8 w8 = *reinterpret_cast<const f16x8*>(wsrc + (oc + e) * BN + k);
+          if constexpr (kWLds32) {
+            float w[8];
+            load8(wl32 + (oc + e) * BN + k, w);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) a[e] += x[j] * (float)w8[j];
+            for (int j = 0; j < 8; ++j) a[e] += x[j] * w[j];
+          } else {
+            const f16x8 w8 = *reinterpret_cast<const f16x8*>(wsrc + (oc + e) * BN + k);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[e] += x[j] * (float)w8[j];
+          }
         }
       }
       if (tb) {

@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(64 * NWM * NWN, S == 1 ? 2 : 1) k_conv3_halo(G
   // S = 1 (one super-stage, two workgroups per CU: one's DMA and epilogue
   // overlap the other's MFMAs): the stage also holds the epilogue's padded
   // fp32 tile and the fused tail's weights
-  constexpr int EPI_EL = (BM * (BN + 4) * 4 + 16 * BN * 2) / 2;
+  constexpr int EPI_EL = (BM * (BN + 4) * 4 + 16 * BN * 4) / 2;   // + fp32 tail weights
   constexpr int STAGE = S == 1 ? ((STAGE0 > EPI_EL ? STAGE0 : EPI_EL) + 511) / 512 * 512 : STAGE0;
   static_assert(S == 1 || S == 2, "one or two super-stages");
   __shared__ __attribute__((aligned(1024))) f16 smem[S * STAGE];
