@@ -736,6 +736,10 @@ def main(argv=None):
     if hprof is not None:
         hprof.enable()
     host_ms = []
+    phases = None
+    if os.environ.get("S3_HOST_PHASES"):     # host time between tracker phases (diagnostic)
+        phases = []
+        fe.tracker.mark = lambda name: phases.append((len(host_ms), name, time.perf_counter()))
     ms0 = torch.cuda.memory_stats(dev)
     for i in range(a.warmup + 1, nfr):
         h0 = time.perf_counter()
@@ -758,6 +762,14 @@ def main(argv=None):
     model.encoder.events = None
     encodes = _encodes(model.encoder) - enc0
     crit = _critical_path(fe, ev, t, a.steps) if fe.spans is not None else None
+    if phases is not None:
+        fe.tracker.mark = None
+        if crit is not None:
+            by = {}
+            for k, name, tt in phases:
+                by.setdefault(k, []).append((name, tt))
+            crit["host_phases_ms"] = {k: [(n, round((t1 - v[0][1]) * 1e3, 3)) for n, t1 in v]
+                                      for k, v in by.items()}
     if crit is not None:
         crit["host_step_ms"] = host_ms      # host time inside each Frontend.step
         # device allocations (caching-allocator segments) made by the timed frames

@@ -180,6 +180,7 @@ class _RenderWorker:
 
 class Frontend:
     _INFO_RING = 16
+    _RB_RING = 4               # pinned read-back buffers of delivered renders
     def __init__(self, model, device="cuda", K=None, spatial_stride=4, render=True,
                  depth_max_percentile=0.98, max_scale=1.0, min_confidence=1.5,
                  readback=True, enc_batch=1, main_priority=None, late_prefetch=False,
@@ -473,9 +474,18 @@ class Frontend:
             if not self._deliver_one(block):
                 return
 
+    def _readback_slot_free(self) -> bool:
+        """Whether the next read-back buffer's previous copy has landed (a
+        non-blocking delivery never waits for it: that copy can sit behind
+        a whole pair-plan replay on the stream, ~6-7 ms, profiles/r04s)."""
+        if self.render_writer is not None or not self.readback or self._rb_events is None:
+            return True
+        e = self._rb_events[self._rb_i]
+        return e is None or e.query()
+
     def _deliver_one(self, block: bool) -> bool:
         img, chk, info, ev, index, prefix = self._pending[0]
-        if not block and not ev.query():
+        if not block and (not ev.query() or not self._readback_slot_free()):
             return False
         ev.synchronize()
         self._pending.pop(0)
@@ -500,11 +510,11 @@ class Frontend:
                 return
             if self._rb_bufs is None or self._rb_bufs[0].shape != out.shape:
                 self._rb_bufs = [torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
-                                 for _ in range(2)]
-                self._rb_events = [None, None]
+                                 for _ in range(self._RB_RING)]
+                self._rb_events = [None] * self._RB_RING
             k = self._rb_i
-            self._rb_i ^= 1
-            if self._rb_events[k] is not None:      # copy of two frames ago
+            self._rb_i = (k + 1) % self._RB_RING
+            if self._rb_events[k] is not None:      # copy of _RB_RING renders ago
                 self._rb_events[k].synchronize()
             host = self._rb_bufs[k]
             host.copy_(out, non_blocking=True)
@@ -604,10 +614,15 @@ class Frontend:
         return frame
 
     def _step(self, i: int, img, next_img=None, e0=None) -> Frame:
+        mark = getattr(self.tracker, "mark", None)     # host-phase recorder (diagnostic)
+        if mark:
+            mark("step_begin")
         if self.fps_timer is None:
             self.fps_timer = time.time()
         # renders of earlier frames whose validity flags have landed
         self._deliver(block=False)
+        if mark:
+            mark("delivered")
         # keyframe poses the backend worker has finished optimising
         # (SharedKeyframes' in-place writes, frame.py:269-330)
         self.keyframes.apply_pending()
@@ -641,6 +656,8 @@ class Frontend:
                 pending = []
         if e0 is not None:
             e0[0] = self._event()
+        if mark:
+            mark("prefetched")
         self._stats["frames"] += 1
         add_new_kf = False
         T_state = frame.T_WC
@@ -668,6 +685,8 @@ class Frontend:
             # the tracked pose, not from what the backend later writes into
             # the keyframe (the same object here, a shared-memory copy there)
             T_state = frame.T_WC
+            if mark:
+                mark("tracked")
             spec = self.tracker.spec if (self.tracker.spec_valid and not try_reloc) else None
             if (spec is None and self.tracker.spec is not None
                     and isinstance(self.tracker.spec[1], _RenderTicket)):
@@ -728,4 +747,6 @@ class Frontend:
             self.tracker.reset_idx_f2k()
             self._kf_added(frame)
         self.last_T_WC = T_state
+        if mark:
+            mark("step_end")
         return frame

@@ -231,13 +231,18 @@ class FrameTracker:
         _decode_ahead), or None."""
         self.spec, self.spec_valid = None, False
         from splatt3r_amd.splatt3r_utils import splatt3r_match_asymmetric
+        mark = getattr(self, "mark", None)       # host-phase recorder (diagnostic)
         keyframe = self.keyframes.last_keyframe()
+        if mark:
+            mark("track_start")
         idx_f2k, valid_match_k, Xff, Cff, Qff, Xkf, Ckf, Qkf = splatt3r_match_asymmetric(
             self.model, frame, keyframe, idx_i2j_init=self.idx_f2k, ahead=ahead)
         # matching.match returns a fresh tensor that nothing writes later, so
         # the reference's clone (tracker.py:40) is not needed to keep it
         self.idx_f2k = idx_f2k
         idx_f2k = idx_f2k[0]
+        if mark:
+            mark("matched")
         valid_match_k = valid_match_k[0]
         frame.update_pointmap(Xff, Cff)
 
@@ -276,13 +281,19 @@ class FrameTracker:
         # runs the post-GN glue and issues the next launches
         gn_done = torch.cuda.Event()
         gn_done.record(torch.cuda.current_stream(ne.device))
+        if mark:
+            mark("gn_queued")
         if before_sync is not None:
             self.spec = before_sync(T_WCk * lietorch.Sim3(ne.pose.clone().view(1, 8)))
+        if mark:
+            mark("spec_queued")
         if _GN_EVENT_WAIT:
             _lib.wait_event(gn_done)
         else:
             _lib.wait_stream(ne.device)
         n_opt, n_kf, n_unique = stats_host.tolist()
+        if mark:
+            mark("gn_done")
 
         if n_opt / n < self.cfg["min_match_frac"]:
             print(f"Skipped frame {frame.frame_id}")
