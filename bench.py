@@ -719,6 +719,8 @@ def main(argv=None):
     ahead0 = dict(model.encoder.ahead_counts)
     units0 = model.encoder.plan_units()
     enc0 = _encodes(model.encoder)
+    if os.environ.get("S3_RESERVE", "1") != "0":
+        fe.reserve_memory()                # plans are captured: grow the allocator's cache now
     if os.environ.get("S3_GC_FREEZE", "1") != "0":
         # the warm-up's objects (plans, frames, tensors) leave the collected
         # generations: a garbage collection inside the timed region then

@@ -474,6 +474,28 @@ class Frontend:
             if not self._deliver_one(block):
                 return
 
+    def reserve_memory(self, large_mb: int = 2048, small_blocks: int = 64):
+        """Grow torch's caching allocator on this frontend's streams (call
+        once the plans are captured: a graph capture empties the cache).
+        The map and keyframe state grow frame after frame; an allocation the
+        cache cannot serve is a device allocation inside the frame loop,
+        which can hold the host until the device drains (~6-7 ms,
+        profiles/r04p_host_steps.log).  A freed large segment is split for
+        later large allocations of its stream, and `small_blocks` freed 1 MiB
+        blocks keep the small pool (<= 1 MiB requests) from growing."""
+        streams = [s for s in (self.enc_stream, self.main_stream) if s is not None]
+        streams.append(torch.cuda.current_stream(self.device))
+        seen = set()
+        for st in streams:
+            if st.cuda_stream in seen:
+                continue
+            seen.add(st.cuda_stream)
+            with torch.cuda.stream(st):
+                big = torch.empty(large_mb << 20, dtype=torch.uint8, device=self.device)
+                small = [torch.empty(1 << 20, dtype=torch.uint8, device=self.device)
+                         for _ in range(small_blocks)]
+                del big, small
+
     def _readback_slot_free(self) -> bool:
         """Whether the next read-back buffer's previous copy has landed (a
         non-blocking delivery never waits for it: that copy can sit behind
