@@ -478,6 +478,7 @@ def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, wri
             if i == warmup + 1:                  # frame 0 = INIT, W warm-up frames
                 fe.drain()
                 writer.flush()
+                fe.reserve_memory()
                 torch.cuda.synchronize()
                 s0 = dict(fe.stats)
                 t0 = time.perf_counter()
@@ -600,6 +601,8 @@ def bench_live(model, dev, frames, steps, warmup, main_priority=-1):
         for i in range(warmup + 1 + steps):
             if prof is not None and i == warmup + 1:
                 prof.enable()
+            if i == warmup + 1:
+                fe.reserve_memory()
             torch.cuda.synchronize()
             if i == warmup + 1:
                 s0 = dict(fe.stats)
