@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 OFF="--no-e2e --no-pairs --no-backend --no-map --no-c3 --no-cpu-baseline --no-kprof --no-live"
-for CFG in S3_POOL_RESERVE_MB=2048 S3_POOL_RESERVE_MB=0; do
+for CFG in PYTORCH_HIP_ALLOC_CONF=expandable_segments:True S3_A=0 PYTORCH_HIP_ALLOC_CONF=expandable_segments:True S3_A=0 PYTORCH_HIP_ALLOC_CONF=expandable_segments:True S3_A=0; do
   env ${CFG:-S3_X=0} timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 $OFF > gpurun_out/r04p_one.log 2>&1 || { tail -20 gpurun_out/r04p_one.log; exit 1; }
   grep '^{' gpurun_out/r04p_one.log | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read()); c=d['critical_path']
