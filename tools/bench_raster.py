@@ -102,12 +102,8 @@ def main():
     ap.add_argument("--P", type=int, default=4_194_304)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--no-backward", action="store_true")
-    ap.add_argument("--binning", type=int, default=0, help="0 single-pass, 1 radix tile sort")
     a = ap.parse_args()
     t0 = time.time()
-    if a.binning:
-        import diff_gaussian_rasterization as dgr
-        dgr.set_binning(a.binning)
     print(json.dumps(run(a.P, a.iters, backward=not a.no_backward)))
     print(f"# wall {time.time() - t0:.1f}s")
 
