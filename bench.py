@@ -114,6 +114,11 @@ def _args(argv=None):
     return ap.parse_args(argv)
 
 
+# S3_PLAN_OVERLAP=0: the first exact plan of the search (round-4 driver runs;
+# the last timed replay is then queued by the last timed step) (A/B)
+_PLAN_OVERLAP = os.environ.get("S3_PLAN_OVERLAP", "1") != "0"
+
+
 def plan_encodes(steps: int, warmup: int, enc_batch: int, enc_ahead, pipeline: bool = True):
     """The encoder queueing of the bench's frame sequence, simulated with the
     frontend's own rule (slam.lookahead_batches), and the lookahead caps that
@@ -125,9 +130,9 @@ def plan_encodes(steps: int, warmup: int, enc_batch: int, enc_ahead, pipeline: b
     only frames below `cap_warm`, timed steps only frames below `cap`.  The
     caps are chosen so that the encodes queued by timed steps number exactly
     `steps` (the last replay is a partial batch when `steps` is not a
-    multiple of `enc_batch`), with the warm-up lookahead as deep as that
-    allows (None = uncapped: the steady-state pipeline at the start of the
-    timed region).  Returns {batches: [(first frame, count, timed)], cap,
+    multiple of `enc_batch`), every timed replay queued as far ahead of its
+    first frame as in the steady state and the last one as early as that
+    allows (see below; None = uncapped).  Returns {batches: [(first frame, count, timed)], cap,
     cap_warm, timed_encodes, next_enc_before (the frontend's _next_enc after
     warm-up), frames_needed, look}."""
     from splatt3r_amd.slam import lookahead_batches
@@ -137,6 +142,8 @@ def plan_encodes(steps: int, warmup: int, enc_batch: int, enc_ahead, pipeline: b
 
     def sim(cap_warm, cap):
         nxt_enc, batches, before = 0, [], None
+        sim.last_q = -1                     # frame whose step queued the last timed replay
+        sim.slack = 1 << 30                 # min over timed replays: first frame - queuing frame
         for i in range(nfr):
             timed = i > warmup
             if i == warmup + 1:
@@ -151,25 +158,35 @@ def plan_encodes(steps: int, warmup: int, enc_batch: int, enc_ahead, pipeline: b
             for s, c in lookahead_batches(i, nxt_enc, max(0, hi - (i + 1)), kb, enc_ahead):
                 batches.append((s, c, timed))
                 nxt_enc = s + c
+                if timed:
+                    sim.last_q = i
+                    sim.slack = min(sim.slack, s - i)
         return batches, before, sum(c for _, c, t in batches if t)
 
     if not pipeline:
         batches, before, n = sim(None, None)
         return dict(batches=batches, cap=None, cap_warm=None, timed_encodes=n,
                     next_enc_before=before, frames_needed=nfr, look=look)
+    # Of the (cap_warm, cap) pairs that give exactly `steps` timed encodes:
+    # the largest lead of every timed replay over its first frame (the
+    # steady state's: no frame waits for its encode), then the last timed
+    # replay queued earliest, so that it overlaps later timed frames'
+    # main-stream work as every replay does in the steady state (one queued
+    # by the last timed step would run alone after the last frame, for
+    # frames past the region).
     best = None
     for cap_warm in [None] + list(range(warmup + 1 + look, warmup, -1)):
         _, before, _ = sim(cap_warm, None)
         # timed encodes are non-decreasing in the cap, by at most one per frame
         for cap in range(before + steps, before + steps + look + kb + 2):
             b, bf, n = sim(cap_warm, cap)
-            if best is None or abs(n - steps) < abs(best[3] - steps):
-                best = (cap_warm, cap, b, n, bf)
+            key = ((abs(n - steps), -sim.slack, sim.last_q) if _PLAN_OVERLAP
+                   else (abs(n - steps),))
+            if best is None or key < best[5]:
+                best = (cap_warm, cap, b, n, bf, key)
             if n >= steps:
                 break
-        if best[3] == steps:
-            break
-    cap_warm, cap, batches, n, before = best
+    cap_warm, cap, batches, n, before, _ = best
     need = max(nfr + look, cap)
     return dict(batches=batches, cap=cap, cap_warm=cap_warm, timed_encodes=n,
                 next_enc_before=before, frames_needed=need, look=look)
@@ -539,7 +556,7 @@ def _encodes(net) -> int:
     return sum(ep.calls * key[0] for key, ep in net._enc.items())
 
 
-def _critical_path(fe, net_events, wall_s, steps):
+def _critical_path(fe, net_events, wall_s, steps, ev_t0=None):
     """Where the frame period goes, from the HIP events of the timed region
     (one stream each): the main chain of frame i (Frontend.spans "main",
     decoder + heads + matching + GN + render on the main stream) and the
@@ -566,6 +583,13 @@ def _critical_path(fe, net_events, wall_s, steps):
            "source": "HIP events on the main / encoder streams over the timed region"}
     out["sum_ms"] = (out["main_network_ms"] + out["main_other_ms"] + out["main_idle_ms"]
                      + out["edge_ms"])
+    # the edge, split: timer start -> first chain, and the encoder side
+    # stream's work still running after the last chain (ms, whole region)
+    if ev_t0 is not None:
+        out["edge_head_ms_total"] = round(ev_t0.elapsed_time(mains[0][0]), 3)
+    if encs:
+        out["enc_tail_ms_total"] = round(mains[-1][1].elapsed_time(max(
+            (e1 for _, e1 in encs), key=lambda e: mains[0][0].elapsed_time(e))), 3)
     # main-stream idle between consecutive frames' chains, per frame
     out["idle_gaps_ms"] = [round(a[1].elapsed_time(b[0]), 3) for a, b in zip(mains, mains[1:])]
     return out
@@ -738,6 +762,10 @@ def main(argv=None):
     _barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev_t0 = None
+    if fe.spans is not None:
+        ev_t0 = torch.cuda.Event(enable_timing=True)
+        ev_t0.record(fe.main_stream or torch.cuda.current_stream(dev))
     if hprof is not None:
         hprof.enable()
     host_ms = []
@@ -766,7 +794,7 @@ def main(argv=None):
     ev = model.encoder.events
     model.encoder.events = None
     encodes = _encodes(model.encoder) - enc0
-    crit = _critical_path(fe, ev, t, a.steps) if fe.spans is not None else None
+    crit = _critical_path(fe, ev, t, a.steps, ev_t0) if fe.spans is not None else None
     if phases is not None:
         fe.tracker.mark = None
         if crit is not None:

@@ -85,3 +85,25 @@ def test_world_size_must_match_gpus():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
                         "--dist-dry-run"], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_driver_plan_overlaps_every_timed_replay():
+    """The driver's plan queues every timed encoder replay enc_ahead frames
+    before its first frame (the steady state's lead: no timed frame waits for
+    its encode) and the last one before the last timed step, so that no
+    replay runs alone after the last tracked frame."""
+    from splatt3r_amd.slam import lookahead_batches
+    steps, warmup, kb, ahead = 20, 5, 8, 8
+    p = bench.plan_encodes(steps, warmup, kb, ahead)
+    assert p["timed_encodes"] == steps
+    # replay the frontend's rule with the plan's caps to get the queuing steps
+    look = p["look"]
+    nxt_enc, queued = p["next_enc_before"], []
+    for i in range(warmup + 1, warmup + steps + 1):
+        hi = min(i + 1 + look, p["cap"])
+        for s, c in lookahead_batches(i, nxt_enc, max(0, hi - (i + 1)), kb, ahead):
+            queued.append((i, s, c))
+            nxt_enc = s + c
+    assert sum(c for _, _, c in queued) == steps
+    assert all(s - i >= ahead for i, s, _ in queued)
+    assert queued[-1][0] < warmup + steps
