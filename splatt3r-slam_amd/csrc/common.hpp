@@ -16,6 +16,31 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Wave reduce-scatter of N <= 64 per-lane sums (padded to 64 slots): at
+// offset o each lane keeps the half of its slots selected by lane bit o and
+// adds its partner's copy of that half (63 shuffles in all, against N x 6
+// for N separate butterflies).  Returns, in lane k < N, the wave total of
+// acc[k] (the other lanes return 0 or a padding slot).
+template <int N>
+__device__ __forceinline__ float wave_reduce_scatter(const float (&acc)[N]) {
+  static_assert(N <= 64, "at most 64 sums");
+  const int lane = threadIdx.x & 63;
+  float v[64];
+#pragma unroll
+  for (int k = 0; k < 64; ++k) v[k] = k < N ? acc[k] : 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const bool hi = (lane & o) != 0;
+#pragma unroll
+    for (int j = 0; j < o; ++j) {
+      const float keep = hi ? v[j + o] : v[j];
+      const float send = hi ? v[j] : v[j + o];
+      v[j] = keep + __shfl_xor(send, o, 64);
+    }
+  }
+  return v[0];
+}
+
 }  // namespace s3
 
 // Validate an argument; on failure record the message and return S3_ERR_INVALID.

@@ -189,15 +189,12 @@ __global__ void __launch_bounds__(kThreads) k_edge_align(EdgeP p) {
       for (int r = 0; r < 3; ++r) accum_row(Ti, Jl[r], w[r], err[r], acc);
     }
   }
+  // wave reduce-scatter (lane k gets the wave total of sum k), then the
+  // wave partials through LDS
   __shared__ float red[kThreads / 64][NA];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < NA; ++k) {
-    float v = acc[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) red[wave][k] = v;
-  }
+  const float wsum = s3::wave_reduce_scatter(acc);
+  if (lane < NA) red[wave][lane] = wsum;
   __syncthreads();
   if (threadIdx.x < NA)
     p.partial[((int64_t)e * S + s) * NA + threadIdx.x] =

@@ -136,27 +136,12 @@ k_normal_eqs(const double* __restrict__ state, const float* __restrict__ Tdev,
       }
     }
   }
-  // block reduction: a reduce-scatter across the wave (the 36 sums padded
-  // to 64 slots; at offset o each lane keeps the half of its slots selected
-  // by lane bit o and adds its partner's copy of them: 63 shuffles instead
-  // of 36 x 6), after which lane k holds the wave total of slot k; then the
-  // 4 wave partials through LDS
+  // block reduction: a reduce-scatter across the wave (lane k gets the wave
+  // total of sum k), then the 4 wave partials through LDS
   __shared__ float red[4][NV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float v[64];
-#pragma unroll
-  for (int k = 0; k < 64; ++k) v[k] = k < NV ? acc[k] : 0.f;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const bool hi = (lane & o) != 0;
-#pragma unroll
-    for (int j = 0; j < o; ++j) {
-      const float keep = hi ? v[j + o] : v[j];
-      const float send = hi ? v[j] : v[j + o];
-      v[j] = keep + __shfl_xor(send, o, 64);
-    }
-  }
-  if (lane < NV) red[wave][lane] = v[0];
+  const float wsum = s3::wave_reduce_scatter(acc);
+  if (lane < NV) red[wave][lane] = wsum;
   __syncthreads();
   if (threadIdx.x < NV)
     partial[blockIdx.x * NV + threadIdx.x] =
