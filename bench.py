@@ -296,6 +296,15 @@ def _kernel_profile(units, reps=3):
 _KFAM = re.compile(r"k_gemm<([^>]*)>")
 
 
+def _algo_bytes(units, kind):
+    """Algorithmic HBM bytes per frame of one kernel family (ops.Call.nbytes:
+    every operand read once, every output written once), weighted by the
+    plans' replays per frame like the FLOPs."""
+    return sum(wgt * sum(getattr(c, "nbytes", 0) for c in pl.calls
+                         if getattr(c, "kind", None) == kind)
+               for wgt, plans in units for pl in plans)
+
+
 def _kernel_trace(units, reps=5):
     """{family: [launches per frame, ms per frame]} of the network kernels:
     a torch.profiler (roctracer) kernel trace of `reps` serial replays of
@@ -588,8 +597,13 @@ def _critical_path(fe, net_events, wall_s, steps, ev_t0=None):
     if ev_t0 is not None:
         out["edge_head_ms_total"] = round(ev_t0.elapsed_time(mains[0][0]), 3)
     if encs:
-        out["enc_tail_ms_total"] = round(mains[-1][1].elapsed_time(max(
-            (e1 for _, e1 in encs), key=lambda e: mains[0][0].elapsed_time(e))), 3)
+        # the encoder side stream's work still running after the last chain
+        # (0 when the last encode ended first), and the signed offset of the
+        # last encode's end from the last chain's end
+        off = mains[-1][1].elapsed_time(max(
+            (e1 for _, e1 in encs), key=lambda e: mains[0][0].elapsed_time(e)))
+        out["enc_after_last_chain_ms_total"] = round(max(0.0, off), 3)
+        out["last_enc_end_minus_last_chain_end_ms"] = round(off, 3)
     # main-stream idle between consecutive frames' chains, per frame
     out["idle_gaps_ms"] = [round(a[1].elapsed_time(b[0]), 3) for a, b in zip(mains, mains[1:])]
     return out
@@ -885,11 +899,17 @@ def main(argv=None):
                       f"timing: {prof[dom][2]:.3f} ms/frame")
         achieved = fl / (ms * 1e-3) / 1e12
         tr = _pmc_traffic(dom)
+        # algorithmic bytes of the same (non-speculative) launches
+        ab = _algo_bytes(units, dom) * (fl / fl_run if fl_run else 1.0) / a.steps
         result["roofline"] = {
             "bound": "mfma", "kernel": f"s3n {dom} (all launches of one frame)",
             "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / PEAK_F16_TFLOPS,
-            "traffic": tr["bytes_per_launch"] if tr else None,
+            # per frame, like `achieved` (all launches of the family in one frame)
+            "traffic": tr["bytes_per_frame"] if tr else None,
+            "traffic_unit": "HBM bytes per frame (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "algorithmic_bytes_per_frame": ab,
+            "traffic_over_algorithmic": (tr["bytes_per_frame"] / ab) if (tr and ab) else None,
             "launches_per_frame": n_l, "avg_launch_us": ms / n_l * 1e3,
             "ms_per_frame": ms, "timing": source,
             "algorithmic_gflop_per_frame": fl / 1e9,
@@ -910,6 +930,11 @@ def main(argv=None):
                              "tflops_wall": flops_frame / (net_ms * 1e-3) / 1e12}
     result["device_path_fps"] = value
     fe.close()
+    # fp16 store guards of the network (GEMM epilogues, LayerNorm) that fired
+    # since the process started: > 0 means activations beyond +-65504 were
+    # saturated (the Frontend warns at close() too)
+    from splatt3r_amd import ops as _ops
+    result["f16_saturations"] = _ops.f16_saturations()
     if rank == 0 and not a.no_e2e:
         e2e = bench_end_to_end(model, dev, a.steps, a.warmup, a.main_priority,
                                workers=a.e2e_loaders, writers=a.e2e_writers,

@@ -190,8 +190,12 @@ class _OracleCam(ctypes.Structure):
 
 
 def raster(settings: dict, means3D, opacities, shs=None, colors_precomp=None, scales=None,
-           rotations=None, cov3D_precomp=None, dL_dout=None, nthreads=8):
+           rotations=None, cov3D_precomp=None, dL_dout=None, nthreads=8, exp="kernel"):
     """graphdeco forward (+ backward if dL_dout) on the CPU.
+
+    exp = "kernel": the blend's exponential is the HIP kernels' fixed-sequence
+    fexp (bit-comparable forward); "libm": glibc expf, the canonical
+    graphdeco `exp(power)` (the HIP image then agrees within a tolerance).
 
     settings: dict with image_height, image_width, tanfovx, tanfovy, bg(3),
     scale_modifier, viewmatrix(16, memory order of the torch arg),
@@ -233,8 +237,14 @@ def raster(settings: dict, means3D, opacities, shs=None, colors_precomp=None, sc
     f.restype = ctypes.c_int64
     gk = ("dL_dmeans2D", "dL_dconic", "dL_dopacity", "dL_dcolors", "dL_dmeans3D", "dL_dcov3D",
           "dL_dsh")
-    R = f(ctypes.byref(cam), ctypes.c_int64(P), M, _p(m), q(sc), q(rot), q(cov), q(sh), q(col),
-          _p(op), _p(color), _p(radii), q(g),
-          *[q(out[k]) if g is not None else None for k in gk], nthreads)
+    if exp not in ("kernel", "libm"):
+        raise ValueError(f"exp must be 'kernel' or 'libm', not {exp!r}")
+    lib().oracle_raster_set_exp(int(exp == "libm"))
+    try:
+        R = f(ctypes.byref(cam), ctypes.c_int64(P), M, _p(m), q(sc), q(rot), q(cov), q(sh),
+              q(col), _p(op), _p(color), _p(radii), q(g),
+              *[q(out[k]) if g is not None else None for k in gk], nthreads)
+    finally:
+        lib().oracle_raster_set_exp(0)
     out["num_rendered"] = int(R)
     return out

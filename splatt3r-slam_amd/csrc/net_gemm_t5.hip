@@ -6,7 +6,9 @@ namespace s3gemm {
 // v_mfma_f32_16x16x32 tiles, continued
 int launch_t5(int tile, const GemmP& p, hipStream_t st) {
   if (tile < 26 || tile > 31) return kNotMine;
-  if (!p.vec_epi) return launch_t1(1, p, st);
+  // no silent fallback to another tile: that would change the launch's
+  // reduction class (ops.reduction_class); the tuner skips the error
+  S3_REQUIRE(p.vec_epi, "s3n_gemm: 16x16 MFMA tiles need the vector epilogue");
   if (tile == 26) return launch<64, 64, 3, 2, 2, 64, 1, 16>(p, st);
   if (tile == 27) return launch<128, 128, 3, 2, 2, 64, 1, 16>(p, st);
   if (tile == 28) return launch<64, 128, 3, 2, 2, 64, 1, 16>(p, st);

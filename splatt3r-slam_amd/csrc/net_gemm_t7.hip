@@ -11,7 +11,8 @@ namespace s3gemm {
 int launch_t7(int tile, const GemmP& p, hipStream_t st) {
   if (tile < 32 || tile > 37 || tile == 33) return kNotMine;
   const bool mf16 = tile == 32 || tile == 36 || tile == 37;
-  if (mf16 && !p.vec_epi) return launch_t1(1, p, st);
+  // no silent fallback to another tile (it would change the reduction class)
+  S3_REQUIRE(!mf16 || p.vec_epi, "s3n_gemm: 16x16 MFMA tiles need the vector epilogue");
   if (tile == 32) return launch<128, 128, 2, 2, 4, 64, 1, 16>(p, st);
   if (tile == 34) return launch<256, 128, 2, 4, 2, 64, 1, 32>(p, st);
   if (tile == 35) return launch<128, 256, 2, 2, 4, 64, 1, 32>(p, st);

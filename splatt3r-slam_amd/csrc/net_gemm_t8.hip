@@ -266,8 +266,9 @@ namespace s3gemm {
 int launch_t8(int tile, const GemmP& p, hipStream_t st) {
   if (tile < 60 || tile > 68) return kNotMine;
   if (tile == 61) return kNotMine;   // 256 x 128 with 32x32 MFMAs spills (576 B/lane)
-  const bool mf16 = tile != 65;
-  if (mf16 && !p.vec_epi) return launch_t1(1, p, st);
+  // the 16x16 tiles stage their fp32 tile through LDS: no silent fallback to
+  // another tile (that would change the launch's reduction class)
+  S3_REQUIRE(tile == 65 || p.vec_epi, "s3n_gemm: 16x16 MFMA tiles need the vector epilogue");
   switch (tile) {
     case 60: return launch_pp<256, 128, 3, 2, 2, 16>(p, st);   // wave 128 x 64
     case 62: return launch_pp<128, 256, 3, 2, 2, 16>(p, st);   // wave 64 x 128

@@ -120,19 +120,28 @@ def wait_stream(device: torch.device | None = None) -> None:
 
 # S3_SPIN_YIELD=0: poll without yielding the CPU between polls (A/B)
 _SPIN_YIELD = os.environ.get("S3_SPIN_YIELD", "1") != "0"
+# Longest a host wait polls before it falls back to a blocking synchronize
+# (S3_SPIN_US, microseconds): the frame loop's waits (a GN chunk, the render
+# flags) end within a few hundred us, where polling saves the blocking wait's
+# wake-up latency; a longer wait stops spinning, so a core and the GIL are
+# not held by the poll loop while the backend worker, the loader and the PNG
+# writer threads need them.
+_SPIN_BUDGET_S = float(os.environ.get("S3_SPIN_US", "1000")) * 1e-6
 
 
 def wait_event(ev) -> None:
-    """Host wait for a recorded event (polled, see wait_stream)."""
+    """Host wait for a recorded event (polled up to the spin budget, then a
+    blocking synchronize; see wait_stream)."""
     if not _SPIN_SYNC:
         ev.synchronize()
         return
-    if _SPIN_YIELD:
-        while not ev.query():
+    deadline = time.perf_counter() + _SPIN_BUDGET_S
+    while not ev.query():
+        if time.perf_counter() > deadline:
+            ev.synchronize()
+            return
+        if _SPIN_YIELD:
             time.sleep(0)
-    else:
-        while not ev.query():
-            pass
 
 
 def stream(device: torch.device | None = None) -> int:

@@ -129,13 +129,14 @@ def _parr(items: Sequence, n=G):
 
 class Call:
     """A prebuilt library call: fn(*args) with status check."""
-    __slots__ = ("fn", "args", "name", "keep", "kind", "flops", "desc")
+    __slots__ = ("fn", "args", "name", "keep", "kind", "flops", "desc", "nbytes")
 
-    def __init__(self, name, *args, keep=(), kind=None, flops=0, desc=""):
+    def __init__(self, name, *args, keep=(), kind=None, flops=0, desc="", nbytes=0):
         self.desc = desc             # shape string for per-launch profiles
         self.name = name
         self.kind = kind or name     # roofline bucket (bench.py)
         self.flops = flops           # algorithmic flops of one launch
+        self.nbytes = nbytes         # algorithmic HBM bytes of one launch (operands once)
         self.fn = getattr(_lib.lib(), name)
         self.args = args
         # Everything the call points into must outlive it: the ctypes
@@ -186,11 +187,34 @@ _FLUSH: dict = {}
 TUNE_DB = os.environ.get("S3_GEMM_TUNE_DB",
                          os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune_gfx950.json"))
 TUNE_DB_SAVE = os.environ.get("S3_GEMM_TUNE_DB_SAVE", "")
-_DB_STATE = {"loaded": False, "entries": {}}
-# Bumped whenever a net_gemm_t*.hip launch precondition or kernel changes the
-# meaning of a (tile, split) choice: a database written under another value is
-# ignored (its "abi" field; files without one were written under 1).
-_KERNEL_ABI = 1
+# Cache and database keys start with the gfx target of the device that was
+# tuned; "loaded" holds the targets whose database entries were read.
+_DB_STATE = {"loaded": set(), "entries": {}}
+
+
+def _kernel_abi() -> str:
+    """Digest of the GEMM kernel sources (csrc/net_gemm*.hip, the kernel
+    template header and common.hpp): any edit of a kernel or of a launch
+    precondition changes it, and a database written under another digest
+    (its "abi" field) is ignored -- no stale tile choice is replayed after a
+    kernel change.  "unknown" when the sources are not beside the package."""
+    import glob
+    import hashlib
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "net_gemm*.hip")) +
+                   glob.glob(os.path.join(csrc, "net_gemm*.hpp")) +
+                   [os.path.join(csrc, "common.hpp")])
+    if not all(os.path.isfile(f) for f in files) or len(files) < 3:
+        return "unknown"
+    h = hashlib.sha1()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+_KERNEL_ABI = _kernel_abi()
 
 
 def _flush_buffer(dev):
@@ -269,46 +293,57 @@ def _device_arch(dev) -> str:
 
 
 def _db_load(dev=None):
-    """Fill _TUNE_CACHE from TUNE_DB once (cold-tuned entries only, none whose
-    tile this process excludes).  The file is ignored when its tile tables,
-    kernel ABI or gfx target differ from this process's."""
-    if _DB_STATE["loaded"]:
+    """Fill _TUNE_CACHE from TUNE_DB once per gfx target (cold-tuned entries
+    only, none whose tile this process excludes).  The file is ignored when
+    its tile tables, kernel sources (abi) or gfx target differ from this
+    process's / `dev`'s."""
+    arch = _device_arch(dev) if dev is not None else ""
+    tag = arch or "*"
+    if tag in _DB_STATE["loaded"]:
         return
-    _DB_STATE["loaded"] = True
+    _DB_STATE["loaded"].add(tag)
     if not TUNE_DB or not TUNE_COLD or not os.path.isfile(TUNE_DB):
         return
     import json
     with open(TUNE_DB) as f:
         db = json.load(f)
+    db_arch = db.get("arch", "gfx950")
     why = None
     if db.get("digest") != _db_digest():
         why = "tile tables changed"
-    elif int(db.get("abi", 1)) != _KERNEL_ABI:
-        why = f"kernel ABI {db.get('abi', 1)} != {_KERNEL_ABI}"
-    elif dev is not None and _device_arch(dev) and db.get("arch") != _device_arch(dev):
-        why = f"written for {db.get('arch')}, device is {_device_arch(dev)}"
+    elif str(db.get("abi", 1)) != _KERNEL_ABI:
+        why = f"kernel sources {db.get('abi', 1)} != {_KERNEL_ABI}"
+    elif arch and db_arch != arch:
+        why = f"written for {db_arch}, device is {arch}"
     if why is not None:
         if TUNE_LOG:
             print(f"[gemm-tune] {TUNE_DB}: {why}, database ignored", flush=True)
         return
     for k, v in db["entries"]:
-        key, val = _db_decode(k), (int(v[0]), int(v[1]))
+        key, val = (db_arch,) + _db_decode(k), (int(v[0]), int(v[1]))
         if val[0] in _EXCLUDED or (val[0] and val[0] not in _TILE_SHAPES):
             continue
         _DB_STATE["entries"][key] = val
         _TUNE_CACHE.setdefault(key, val)
 
 
-def save_tune_db(path: str):
-    """Write the loaded database merged with this process's choices."""
+def save_tune_db(path: str, arch: str = ""):
+    """Write the loaded database merged with this process's choices, for the
+    gfx target the choices were tuned on (`arch`; by default the only target
+    this process tuned or loaded, gfx950 when there is none)."""
     import json
     merged = dict(_DB_STATE["entries"])
     merged.update(_TUNE_CACHE)
-    entries = [[list(k[:-1]) + [list(k[-1]) if k[-1] is not None else None], list(v)]
-               for k, v in merged.items()]
+    if not arch:
+        archs = sorted({k[0] for k in merged})
+        if len(archs) > 1:
+            raise ValueError(f"tuning choices for several targets {archs}: pass arch=")
+        arch = archs[0] if archs else "gfx950"
+    entries = [[list(k[1:-1]) + [list(k[-1]) if k[-1] is not None else None], list(v)]
+               for k, v in merged.items() if k[0] == arch]
     entries.sort(key=repr)
     with open(path, "w") as f:
-        json.dump({"digest": _db_digest(), "abi": _KERNEL_ABI, "arch": "gfx950",
+        json.dump({"digest": _db_digest(), "abi": _KERNEL_ABI, "arch": arch,
                    "entries": entries}, f)
 
 
@@ -369,7 +404,7 @@ def _tune_candidates(a, split_ok, like=None):
 def _tuned(a, A, B, bias, rope, rope_pos, split_ok, like=None):
     dev = next(t.device for t in (*A, *B) if isinstance(t, torch.Tensor))
     _db_load(dev)
-    key = _tune_key(a) + (like,)
+    key = (_device_arch(dev) or "gfx950",) + _tune_key(a) + (like,)
     if key in _TUNE_CACHE:
         return _TUNE_CACHE[key]
     g = a.groups
@@ -554,10 +589,28 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         dev = next(t.device for t in (*A, *C) if isinstance(t, torch.Tensor))
         ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
         a.workspace = ws.data_ptr()
+    # algorithmic bytes: every operand read once, every output written once
+    # (fp16 A / B, the residuals, bias, the outputs; split-K partials are not
+    # algorithmic)
+    M_, N_, K_ = int(M), int(N), int(K)
+    a_elems = M_ * K_ if conv is None else M_ // (conv["oH"] * conv["oW"]) * \
+        conv["H"] * conv["W"] * conv["C"]
+    per = 2 * a_elems + 2 * N_ * K_
+    if C[0] is not None:
+        per += M_ * N_ * (2 if a.c_f16 else 4)
+    if C2 is not None:
+        per += 2 * M_ * N_
+    for R, f16 in ((R1, a.r1_f16), (R2, a.r2_f16)):
+        if R is not None:
+            per += M_ * N_ * (2 if f16 else 4)
+    if bias:
+        per += 4 * N_
+    if tail is not None:
+        per += 4 * M_ * int(tail[3]) + 2 * int(tail[3]) * N_
     return Call("s3n_gemm", ctypes.byref(a), keep=(a, A, B, C, bias, R1, R2, C2, ws, rope,
                                                     rope_pos, tail),
                 kind="gemm.conv" if conv is not None else "gemm.dense",
-                flops=2 * int(M) * int(N) * int(K) * groups,
+                flops=2 * int(M) * int(N) * int(K) * groups, nbytes=per * groups,
                 desc=f"gemm{'.conv' if conv is not None else ''} {M}x{N}x{K} g{groups}"
                      + (f" k{conv['k']}s{conv['stride']}" if conv is not None else "")
                      + (f" {act}" if act != "none" else "") + (" R1" if R1 else "")

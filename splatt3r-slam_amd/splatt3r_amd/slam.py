@@ -226,7 +226,7 @@ class Frontend:
         self.min_translation, self.min_frame_gap = 0.12, 3   # main.py:339-340
         self.new_kf_frames: list[int] = []
         self._gw_count = None   # device count of world records (no-viz path)
-        self._stats = dict(frames=0, tracked=0, reloc=0, keyframes=0, gn_iters=0,
+        self._stats = dict(frames=0, tracked=0, reloc=0, keyframes=0, gn_iters=0, f16_saturations=0,
                           gaussians_world=0, rendered=0, rerendered=0)
         self._last_render = None
         # host read-back of the render: double-buffered pinned images filled by
@@ -381,6 +381,24 @@ class Frontend:
                 self._rworker.close()
                 self._rworker = None
             _clear_ahead_slot(self.model)
+        self.check_f16_range()
+
+    def check_f16_range(self) -> int:
+        """Warn when an fp16 store guard of the network fired (an activation
+        beyond +-65504 was saturated instead of becoming inf: a real
+        checkpoint whose GELU / fc2 / LayerNorm outputs overflow fp16 would
+        otherwise degrade silently).  Reads the device flags (a sync): called
+        at close(), never inside step().  Returns the count since the last
+        reset (the flags are per process, shared by every frontend)."""
+        from . import ops
+        n = ops.f16_saturations()
+        self._stats["f16_saturations"] = n
+        if n:
+            import warnings
+            warnings.warn(f"splatt3r-slam_amd: {n} fp16 store guard(s) fired: network "
+                          f"activations exceeded the fp16 range and were saturated",
+                          RuntimeWarning, stacklevel=2)
+        return n
 
     @property
     def last_render(self):
@@ -458,9 +476,13 @@ class Frontend:
                 self._deliver_one(block=True)
             info = self._info_ring[self._info_i]
             self._info_i = (self._info_i + 1) % self._INFO_RING
-            info.copy_(chk.info, non_blocking=True)
+            # the copy and the event on the frontend device's stream (the
+            # Frontend's device need not be the current device)
+            st = torch.cuda.current_stream(self.device)
+            with torch.cuda.stream(st):
+                info.copy_(chk.info, non_blocking=True)
             ev = torch.cuda.Event()
-            ev.record()
+            ev.record(st)
             self._pending.append((img, chk, info, ev, index, prefix))
             return
         self._deliver_image(img, index, prefix)

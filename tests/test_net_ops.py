@@ -62,7 +62,12 @@ def test_gemm_dense_bias_residual(M, N, K, groups):
     (1536, 2304, 768, 2, 1, 32), (130, 300, 968, 1, 2, 32), (6144, 1024, 1024, 1, 1, 34),
     (300, 200, 1000, 2, 3, 34), (1536, 768, 3072, 1, 1, 35), (520, 300, 640, 1, 1, 35),
     (6144, 4096, 1024, 1, 1, 36), (130, 96, 2000, 2, 2, 36), (1536, 3072, 768, 2, 1, 37),
-    (64, 64, 136, 1, 1, 37)])
+    (64, 64, 136, 1, 1, 37),
+    # k_gemm_pp tiles (63, 65, 68: half-K-tile fragment pipeline): ragged M / N,
+    # K % 64 != 0, global split-K 2 and 3
+    (1536, 2304, 768, 2, 1, 63), (300, 200, 1000, 2, 3, 63), (130, 300, 968, 1, 2, 65),
+    (1536, 3072, 768, 2, 2, 65), (768, 6400, 1792, 2, 2, 68), (520, 296, 640, 1, 1, 68),
+    (300, 136, 520, 1, 3, 68)])
 def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
     """Split-K partials + ordered reduce + the full epilogue (bias, GELU,
     fp32 residual, fp16 out + fp16 copy) for every tile shape."""
@@ -89,7 +94,8 @@ def test_gemm_split_k_and_tiles(M, N, K, groups, split, tile):
                                             (1, 24, 96), (1, 25, 136), (1, 27, 768),
                                             (1, 29, 256), (1, 31, 768), (1, 32, 768),
                                             (2, 34, 256), (1, 35, 136), (1, 36, 768),
-                                            (1, 37, 96)])
+                                            (1, 37, 96), (1, 63, 768), (2, 65, 256),
+                                            (1, 68, 136), (3, 63, 96)])
 def test_gemm_implicit_conv_split_k(split, tile, Cin):
     from splatt3r_amd import ops, _lib
     B, H, W, Cout, k, stride, pad = 1, 12, 16, 256, 3, 1, 1
@@ -102,6 +108,31 @@ def test_gemm_implicit_conv_split_k(split, tile, Cin):
              tile=tile)(_lib.stream())
     ref = F.conv2d(x.float().permute(0, 3, 1, 2).clamp_min(0), w.float(), padding=pad)
     assert rel_err(out, ref.permute(0, 2, 3, 1)) < 1e-5
+
+
+@pytest.mark.parametrize("pp,ref,M,N,K,groups,split", [
+    (63, 32, 1536, 2304, 768, 2, 1), (63, 26, 300, 200, 1000, 2, 3), (65, 3, 130, 300, 968, 1, 2),
+    (65, 3, 1536, 768, 3072, 2, 1), (68, 36, 768, 6400, 1792, 2, 2), (68, 25, 520, 296, 640, 1, 1)])
+def test_gemm_pp_tiles_bitexact_vs_same_reduction_class(pp, ref, M, N, K, groups, split):
+    """k_gemm_pp (net_gemm_t8.hip: its own two-half register pipeline and
+    stage reuse) computes every element with the same MFMA k order as a
+    k_gemm tile of the same ops.reduction_class: bit-identical outputs, with
+    the full epilogue, ragged tails and split-K."""
+    from splatt3r_amd import ops, _lib
+    assert ops.reduction_class(K, pp, split) == ops.reduction_class(K, ref, split)
+    A = [_rand(M, K, seed=g) for g in range(groups)]
+    W = [_rand(N, K, scale=K ** -0.5, seed=10 + g) for g in range(groups)]
+    b = [_rand(N, dtype=torch.float32, seed=20 + g) for g in range(groups)]
+    R = [_rand(M, N, dtype=torch.float32, seed=30 + g) for g in range(groups)]
+    outs = []
+    for tile in (pp, ref):
+        C = [torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16)
+             for _ in range(groups)]
+        ops.gemm(A, W, C, M, N, K, lda=K, bias=b, act="gelu", R1=R, ldr1=N, split_k=split,
+                 tile=tile)(_lib.stream())
+        outs.append(C)
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
 
 
 def test_gemm_split_k_is_deterministic():
@@ -371,7 +402,7 @@ def test_gaussian_postprocess_vs_torch(n):
 
 
 @pytest.mark.parametrize("case", ["plain", "res16", "split", "rope", "convt", "tile3", "tile4",
-                                  "tile16", "tile17_rope", "tile20"])
+                                  "tile16", "tile17_rope", "tile20", "tile65", "tile65_split"])
 def test_gemm_vector_epilogue_matches_register_epilogue(case):
     """The LDS-staged 8-column epilogue and the per-register epilogue
     (s3n_gemm_set_debug(16)) apply the same operations in the same order:
@@ -400,8 +431,11 @@ def test_gemm_vector_epilogue_matches_register_epilogue(case):
         kw.update(tile=3, split_k=1)
     if case == "tile4":
         kw.update(tile=4, split_k=1)
-    if case in ("tile16", "tile20"):
+    if case in ("tile16", "tile20", "tile65"):
         kw.update(tile=int(case[4:]), split_k=1)
+    if case == "tile65_split":
+        kw.update(tile=65, split_k=2, R1=[_rand(M, N, dtype=torch.float32, seed=70 + i)
+                                          for i in range(g)], ldr1=N)
     if case == "tile17_rope":
         cos, sin = rope_tables(64, "cuda")
         pos = [positions(3, 10, 10, "cuda").reshape(-1, 2) for _ in range(g)]
@@ -435,7 +469,7 @@ def test_gemm_vector_epilogue_matches_register_epilogue(case):
 
 
 @pytest.mark.parametrize("tile,tn,store_c", [(3, 16, False), (2, 16, True), (4, 8, False),
-                                             (0, 16, False)])
+                                             (0, 16, False), (63, 16, False), (65, 8, True)])
 def test_gemm_conv_fused_1x1_tail(tile, tn, store_c):
     """conv3x3 + bias + ReLU with the 1x1 conv fused in the epilogue (the DPT
     head's last two convs, dpt_block.py:321-323) vs torch fp32."""
