@@ -429,20 +429,29 @@ def _cpu_render(oracle, r1, r2, img, kimg, threads):
                   nthreads=threads)
 
 
-def bench_backend(model, dev, steps, rank):
+def bench_backend(model, dev, steps, rank, ws=1):
     """The frontend with the reference backend running concurrently
     (single_thread: False, main.py:122-190): keyframe tasks (retrieval
     update, add_factors over consecutive + retrieved keyframes, GN) on a
     worker thread and its own HIP stream.  Timed from the first tracked
-    frame until the backend has drained the queue."""
+    frame until the backend has drained the queue.  With ws > 1 the
+    backend's keyframe-pair batches are sharded (pairs.PairShard: keyframe
+    features broadcast from rank 0's worker thread, each pair's two decode
+    directions on ranks u mod ws, idx / valid / Q gathered back to rank 0);
+    ranks > 0 serve the tasks (pairs.serve_backend) until rank 0 stops."""
     from splatt3r_amd.backend import Backend
     from splatt3r_amd.frame import Keyframes
+    from splatt3r_amd.pairs import PairShard, serve_backend
     from splatt3r_amd.slam import Frontend
     from splatt3r_amd.synthetic import tum_like_sequence
-    frames = tum_like_sequence(steps + 4, H, W, seed=100 + rank, step_px=2.0, device=dev)
     for b in range(1, 5):                   # backend pair plans, built before timing
         model.encoder.pair_plan(b, H, W, tag="backend")
-    be = Backend(model, Keyframes(), device=dev)
+    if rank > 0:
+        sh = serve_backend(model, dev)
+        return {"rank": rank, "served_units": sh.stats["units"]}
+    frames = tum_like_sequence(steps + 4, H, W, seed=100 + rank, step_px=2.0, device=dev)
+    shard = PairShard(model, dev) if ws > 1 else None
+    be = Backend(model, Keyframes(), device=dev, shard=shard)
     be.start_worker()
     fe = Frontend(model, device=dev, spatial_stride=4, render=True, backend=be)
     nxt = lambda i: [frames[i + 1]]
@@ -461,15 +470,71 @@ def bench_backend(model, dev, steps, rank):
         torch.cuda.synchronize()
         t = time.perf_counter() - t0
     finally:
-        be.stop()
+        be.stop()                           # also releases ranks > 0 (OP_STOP)
+        fe.close()
     st = {k: fe.stats[k] - s0[k] for k in fe.stats}
     bs = {k: be.stats[k] - b0.get(k, 0) for k in be.stats if isinstance(be.stats[k], int)}
-    return {"frames_per_s": steps / t, "frames_per_s_frontend_only_window": steps / t_front,
-            "steps": steps, "keyframes": st["keyframes"],
-            "keyframe_rate": st["keyframes"] / steps, "backend_tasks": bs["optimized"],
-            "factor_graph_edges": be.stats["edges"],
-            "retrieval_candidates": bs["retrieval_candidates"],
-            "mode": "single_thread: False (worker thread + HIP stream, same GPU)"}
+    out = {"frames_per_s": steps / t, "frames_per_s_frontend_only_window": steps / t_front,
+           "steps": steps, "keyframes": st["keyframes"],
+           "keyframe_rate": st["keyframes"] / steps, "backend_tasks": bs["optimized"],
+           "factor_graph_edges": be.stats["edges"],
+           "retrieval_candidates": bs["retrieval_candidates"],
+           "mode": "single_thread: False (worker thread + HIP stream, same GPU)"}
+    if shard is not None:
+        out["mode"] += (f"; keyframe-pair batches sharded over {ws} ranks (PairShard, directed "
+                        f"units u -> rank u mod {ws})")
+        out["rank0_units"] = shard.stats["units"]
+    return out
+
+
+def _dry_backend(ws, rank, n_kf=9):
+    """--dist-dry-run: the sharded backend's protocol on the CPU (gloo): rank
+    0's Backend on its worker thread with a PairShard, ranks > 0 in
+    pairs.serve_backend; network, retrieval and GN are deterministic
+    stand-ins (no GPU work).  Returns the edge / unit counts."""
+    import lietorch
+    from splatt3r_amd.backend import Backend
+    from splatt3r_amd.frame import Frame, Keyframes
+    from splatt3r_amd.net import positions
+    from splatt3r_amd.pairs import PairShard, serve_backend
+
+    def match_dir(fa, pa, fb, pb, sa, sb):
+        hw = int(sa[0].reshape(-1)[0]) * int(sa[0].reshape(-1)[1])
+        ka, kb = fa[:, 0, 0].long(), fb[:, 0, 0].long()
+        ar = torch.arange(hw)
+        idx = (ar[None] * (ka[:, None] + 1) + kb[:, None]) % hw
+        q = (1.0 + (ar[None] % 5).float() + ka[:, None].float())[..., None]
+        return idx, ((ar[None] + kb[:, None]) % 3 != 0)[..., None], q, q + 1.0
+
+    if rank > 0:
+        sh = serve_backend(None, "cpu", match_dir_fn=match_dir)
+        return {"rank": rank, "units": sh.stats["units"], "keyframes": sh.stats["keyframes"]}
+
+    class _Retrieval:
+        def update(self, frame, add_after_query=True, k=3, min_thresh=0.0):
+            return [j for j in (frame.frame_id - 2, frame.frame_id - 3) if j >= 0]
+
+    class _Be(Backend):
+        def _solve(self):                   # no GN without a GPU
+            return None
+
+    sh = PairShard(None, "cpu", match_dir_fn=match_dir)
+    be = _Be(None, Keyframes(), device="cpu", retrieval=_Retrieval(), shard=sh)
+    be.start_worker()
+    try:
+        for k in range(n_kf):
+            f = Frame(k, torch.zeros(1, 3, 32, 48), torch.tensor([[32, 48]]),
+                      torch.tensor([[32, 48]]), T_WC=lietorch.Sim3.Identity(1))
+            f.feat = torch.full((1, 6, 8), float(k))
+            f.pos = positions(1, 2, 3, "cpu")
+            be.keyframes.append(f)
+            be.on_keyframe(k, f)
+            be.queue_global_optimization(k)
+        be.wait()
+    finally:
+        be.stop()
+    return {"keyframes": n_kf, "edges": int(be.factor_graph.ii.numel()),
+            "rank0_units": sh.stats["units"], "pairs": sh.stats["pairs"]}
 
 
 def bench_end_to_end(model, dev, steps, warmup, main_priority=-1, workers=4, writers=3,
@@ -687,11 +752,22 @@ def _dry_run(a, ws, rank):
     tot = torch.tensor([acc, len(mine)], dtype=torch.int64)
     if ws > 1:
         dist.all_reduce(tot)
+    # the sharded backend leg's protocol (bench_backend with ws > 1)
+    be = _dry_backend(ws, rank) if not a.no_backend else None
+    units = torch.tensor([be["units"] if rank else be["rank0_units"]] if be else [0],
+                         dtype=torch.int64)
+    if ws > 1:
+        dist.all_reduce(units)
     if rank == 0:
-        print(json.dumps({"metric": "dist-dry-run", "n_gpus": ws, "world_size": ws,
-                          "dist_backend": dist.get_backend() if ws > 1 else None,
-                          "pairs": len(pairs), "pairs_covered": int(tot[1]),
-                          "checksum": int(tot[0]), "t_max_s": t}), flush=True)
+        line = {"metric": "dist-dry-run", "n_gpus": ws, "world_size": ws,
+                "dist_backend": dist.get_backend() if ws > 1 else None,
+                "pairs": len(pairs), "pairs_covered": int(tot[1]),
+                "checksum": int(tot[0]), "t_max_s": t}
+        if be is not None:
+            line["backend"] = dict(be, units_all_ranks=int(units[0]),
+                                   mode="Backend worker thread + PairShard over the ranks "
+                                        "(serve_backend on ranks > 0), CPU stand-ins")
+        print(json.dumps(line), flush=True)
     if ws > 1:
         dist.destroy_process_group()
 
@@ -957,8 +1033,11 @@ def main(argv=None):
         c4 = tum_like_sequence(12, 320, 512, seed=200 + rank, step_px=2.0, device=dev)
         result["pairs_c4"] = dict(bench_pairs(model, c4, ws, rank, dev, a.pairs_per_rank),
                                   image="512x320 (C4, EuRoC MH_01 shape)", scaling="weak")
-    if rank == 0 and ws == 1 and not a.no_backend:
-        result["backend"] = bench_backend(model, dev, a.backend_steps, rank)
+    if not a.no_backend:
+        # ws > 1: rank 0's backend shards its pair batches over every rank
+        be = bench_backend(model, dev, a.backend_steps, rank, ws)
+        if rank == 0:
+            result["backend"] = be
     if rank == 0 and not a.no_map:
         result["map_c5"] = bench_map(dev)
     if rank == 0 and not a.no_c3:

@@ -15,10 +15,18 @@ frontend calls them directly (single_thread) or hands keyframe tasks to a
 worker thread that issues them on its own HIP stream (`start_worker`), so
 backend kernels run concurrently with the tracker's on the same device.
 With a pairs.PairShard over W ranks, keyframe features are broadcast at
-keyframe creation and add_factors' pair batches run across the ranks.
+keyframe creation and add_factors' pair batches run across the ranks
+(ranks 1..W-1 run pairs.serve_backend).  With the worker running, rank 0's
+collectives are all issued by the worker thread, in task order: the
+frontend's keyframe broadcast is queued as a task ahead of the keyframe's
+optimisation, so the frontend thread never blocks on a collective and never
+interleaves one with the worker's pair batches (PairShard.lock guards the
+remaining frontend-thread tasks: relocalisation, map refresh, stop).  The
+worker runs on the CPU too (no streams), for the gloo protocol tests.
 """
 from __future__ import annotations
 
+import contextlib
 import queue
 import threading
 
@@ -53,9 +61,14 @@ class Backend:
     def on_keyframe(self, idx: int, frame):
         """A keyframe was appended on the frontend: broadcast its features to
         the pair-shard ranks (the reference shares them through
-        SharedKeyframes' shared memory)."""
+        SharedKeyframes' shared memory).  With the worker running the
+        broadcast is its next task (issued on the worker thread and stream,
+        before the keyframe's optimisation, which is queued after it)."""
         if self.shard is not None and self.shard.ws > 1:
-            self.shard.broadcast_keyframe(idx, frame)
+            if self._q is not None:
+                self._q.put(("kf", idx, frame, self._ready_event()))
+            else:
+                self.shard.broadcast_keyframe(idx, frame)
 
     def _solve(self):
         if config["use_calib"]:
@@ -92,7 +105,11 @@ class Backend:
         if kf_idx:
             self.keyframes.append(frame)
             n_kf = len(self.keyframes)
-            self.on_keyframe(n_kf - 1, frame)
+            # synchronous broadcast: relocalisation runs on the calling
+            # thread after wait(), and its add_factors needs the keyframe on
+            # every rank
+            if self.shard is not None and self.shard.ws > 1:
+                self.shard.broadcast_keyframe(n_kf - 1, frame)
             frame_idx = [n_kf - 1] * len(kf_idx)
             if self.factor_graph.add_factors(frame_idx, kf_idx, config["reloc"]["min_match_frac"],
                                              is_reloc=config["reloc"]["strict"]):
@@ -146,29 +163,50 @@ class Backend:
     # --------------------------------------------------------- worker ----
     def start_worker(self):
         """single_thread: False -- keyframe tasks run on a worker thread and
-        its own HIP stream, concurrently with the frontend."""
+        its own HIP stream (no stream on the CPU), concurrently with the
+        frontend."""
         self._q = queue.Queue()
-        self._stream = torch.cuda.Stream(device=self.device)
+        if self.device.type == "cuda":
+            self._stream = torch.cuda.Stream(device=self.device)
         self._thread = threading.Thread(target=self._loop, daemon=True)
         self._thread.start()
 
+    def _ready_event(self):
+        """An event after the caller's queued work (None on the CPU)."""
+        if self.device.type != "cuda":
+            return None
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.device))
+        return ready
+
     def _loop(self):
-        torch.cuda.set_device(self.device)
+        if self._stream is not None:
+            torch.cuda.set_device(self.device)
         while True:
             item = self._q.get()
             if item is None:
                 self._q.task_done()
                 return
-            idx, ready = item
+            kind, idx, frame, ready = item
             # keyframe reads on this thread are stream-safe snapshots and pose
             # writes are handed to the frontend's stream (frame.Keyframes);
             # registered per task: the frontend may attach its keyframe list
             # after the worker started
-            self.keyframes.register_reader(self._stream)
+            if self._stream is not None:
+                self.keyframes.register_reader(self._stream)
+            ctx = (torch.cuda.stream(self._stream) if self._stream is not None
+                   else contextlib.nullcontext())
             try:
-                with torch.cuda.stream(self._stream), torch.inference_mode():
-                    self._stream.wait_event(ready)
-                    self.global_optimization(idx)
+                with ctx, torch.inference_mode():
+                    if ready is not None:
+                        self._stream.wait_event(ready)
+                    if kind == "kf":
+                        if self._stream is not None:
+                            for t in (frame.feat, frame.pos, frame.img):
+                                t.record_stream(self._stream)
+                        self.shard.broadcast_keyframe(idx, frame)
+                    else:
+                        self.global_optimization(idx)
             except Exception as e:   # surfaced by wait()/stop()
                 self._err = e
             self._q.task_done()
@@ -179,25 +217,28 @@ class Backend:
         if self._q is None:
             self.global_optimization(idx)
             return
-        ready = torch.cuda.Event()
-        ready.record(torch.cuda.current_stream(self.device))
-        self._q.put((idx, ready))
+        self._q.put(("opt", idx, None, self._ready_event()))
 
     def wait(self):
         if self._q is not None:
             self._q.join()
-            torch.cuda.current_stream(self.device).wait_stream(self._stream)
-            self.keyframes.apply_pending(wait=True)
+            if self._stream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self._stream)
+                self.keyframes.apply_pending(wait=True)
         if self._err is not None:
             e, self._err = self._err, None
             raise e
 
-    def stop(self):
+    def stop(self, stop_shard: bool = True):
+        """End the worker; with a shard over W > 1 ranks (stop_shard) also
+        release ranks 1..W-1 from serve_backend()."""
         if self._q is not None:
             self._q.put(None)
             self._q.join()
             self._thread.join()
             self._q = None
+        if stop_shard and self.shard is not None and self.shard.ws > 1:
+            self.shard.stop()
         if self._err is not None:
             e, self._err = self._err, None
             raise e

@@ -624,13 +624,17 @@ class Splatt3RNet:
 
     def pair_plan(self, Bp, H, W, keep_tokens=False, tag=None) -> PairPlan:
         """`tag` separates plan buffers of concurrent users of one network
-        (the frontend tracker and the backend worker thread).  The untagged
-        (tracker) plans are batch-invariant: pair b of a Bp > 1 replay equals
-        a Bp = 1 replay of that pair bit for bit."""
+        (the frontend tracker and the backend worker thread).  The tracker
+        and backend plans are batch-invariant: pair b of a Bp > 1 replay
+        equals a Bp = 1 replay of that pair bit for bit, so a keyframe-pair
+        batch gives the same bits however it is split over ranks
+        (pairs.PairShard) and the backend decodes a pair exactly as the
+        tracker would."""
         key = (Bp, H, W, keep_tokens, tag)
         if key not in self._pair:
             with torch.inference_mode(False):
-                pp = PairPlan(self, Bp, H, W, keep_tokens, batch_invariant=tag is None)
+                pp = PairPlan(self, Bp, H, W, keep_tokens,
+                              batch_invariant=tag in (None, "backend"))
             if self._capture_here() and not keep_tokens:
                 pp.decoder_plan.capture()
                 pp.head_plan.capture()

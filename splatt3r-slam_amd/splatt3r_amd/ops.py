@@ -566,7 +566,13 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
         a.rope_ncols = int(rope_ncols)
         a.rope_pos = _parr(rope_pos)
         split_k = 1
-    a.split_k = int(auto_split_k(M, N, K, groups) if split_k is None else split_k)
+    # the static policy of a batch-invariant plan splits K as for its class
+    # shape (class_batch items): the split is the only class-defining choice
+    # of the static tile (net_gemm_t1.hip tile 0: 32x32x16, one K-group)
+    M_split = M
+    if M % max(1, batch) == 0 and (batch > 1 or (class_batch or 1) > 1):
+        M_split = M // max(1, batch) * (class_batch or 1)
+    a.split_k = int(auto_split_k(M_split, N, K, groups) if split_k is None else split_k)
     a.tile = int(tile) or TILE_OVERRIDE
     if TUNE and not tile and not TILE_OVERRIDE and torch.cuda.is_available():
         split_ok = split_k is None and rope_pos is None

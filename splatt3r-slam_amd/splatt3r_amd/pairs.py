@@ -8,12 +8,18 @@ keyframe pair in both orders and matches both directions
   * keyframe features are broadcast from rank 0 when a keyframe is created
     (`PairShard.broadcast_keyframe`, one RCCL broadcast of the [1, N, 1024]
     fp32 encoder output, 3.1 MB at 512x384), so no rank re-encodes;
-  * `PairShard.match_pairs(ii, jj)` sends the pair list to every rank, pair
-    p runs on rank p mod W as ONE batched symmetric decode (grouped decoder
-    branches + heads over the rank's pairs) + matching, each rank folds the
-    reference's Q-weighting into its results (Qj, Qi), and rank 0 gathers
-    idx / valid / Q (26 B per pixel per pair) with three all-gathers and
-    restores the pair order; the GN solve stays on rank 0 (global_opt.py);
+  * `PairShard.match_pairs(ii, jj)` sends the pair list to every rank; each
+    pair's two decode directions (i, j) and (j, i) are separate units (a
+    direction is one asymmetric decode + one matching, with nothing shared
+    with the other direction: splatt3r_utils.py:466-576), unit u = 2 p + d
+    runs on rank u mod W -- so the reference's <= 4 pairs per keyframe keep
+    8 ranks busy -- as ONE batched decode (grouped decoder branches + heads
+    over the rank's units) + matching; each rank folds the reference's
+    Q-weighting into its results (Q = sqrt(Q_aa[idx] Q_ba)), and rank 0
+    gathers idx / valid / Q (13 B per pixel per unit) with three all-gathers
+    and restores the pair order; the GN solve stays on rank 0
+    (global_opt.py).  The backend pair plans are batch-invariant (net.py),
+    so every split gives the single-rank bits;
   * the global-map refresh after an optimisation (`PairShard.refresh_map`,
     the C5 path "batched ViT re-inference + full-map render"): every rank
     re-infers its share of the factor-graph edges, turns keyframe i's
@@ -32,13 +38,15 @@ collectives stage through host memory; with RCCL they run on the device.
 """
 from __future__ import annotations
 
+import threading
 import time
 from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist
 
-from splatt3r_amd.splatt3r_utils import splatt3r_match_symmetric, world_records
+from splatt3r_amd.splatt3r_utils import (splatt3r_match_directed, splatt3r_match_symmetric,
+                                         world_records)
 
 GAUSS_FLOATS = 13   # means 3 + cov_triu 6 + colour 3 + opacity 1 (52 B)
 
@@ -76,6 +84,11 @@ def _all_gather_equal(t: torch.Tensor, ws: int) -> list[torch.Tensor]:
     parts = [torch.empty_like(src) for _ in range(ws)]
     dist.all_gather(parts, src.contiguous())
     return [p.to(t.device) for p in parts]
+
+
+def _img_downsample() -> int:
+    from splatt3r_amd.config import config
+    return int(config["dataset"]["img_downsample"])
 
 
 class MapRecords:
@@ -121,12 +134,15 @@ class PairShard:
     holds, and the execution of this rank's share of a pair batch.
 
     match_fn(feat_i, pos_i, feat_j, pos_j, shape_i, shape_j) -> the 8-tuple
-    of splatt3r_match_symmetric; injectable so the collective protocol is
-    testable without the network (tests/test_pairs.py)."""
+    of splatt3r_match_symmetric (single rank), match_dir_fn(feat_a, pos_a,
+    feat_b, pos_b, shape_a, shape_b) -> (idx, valid, Q_aa, Q_ba) of
+    splatt3r_match_directed (one direction per unit, W > 1); injectable so
+    the collective protocol is testable without the network
+    (tests/test_pairs.py)."""
 
     def __init__(self, model, device, match_fn: Optional[Callable] = None, Q_conf=None,
                  map_fn: Optional[Callable] = None, gmap=None, local: bool = False,
-                 map_cap: Optional[Callable] = None):
+                 map_cap: Optional[Callable] = None, match_dir_fn: Optional[Callable] = None):
         from splatt3r_amd.config import config
         self.model = model
         # map_fn(pairs, poses [n_kf, 8], params (stride, q, max_scale, conf,
@@ -144,15 +160,24 @@ class PairShard:
         self.ws = dist.get_world_size() if _backend() and not local else 1
         self.rank = dist.get_rank() if _backend() and not local else 0
         self.match_fn = match_fn or (lambda *a: splatt3r_match_symmetric(model, *a))
+        self.match_dir_fn = match_dir_fn or (lambda *a: splatt3r_match_directed(model, *a))
         self.Q_conf = config["local_opt"]["Q_conf"] if Q_conf is None else Q_conf
         self.kf: dict[int, tuple] = {}   # keyframe index -> (feat, pos, true_shape)
-        self.stats = dict(pairs=0, keyframes=0)
+        self.stats = dict(pairs=0, units=0, keyframes=0)
+        # Rank 0 issues every task (header + payload collectives) as one
+        # uninterrupted sequence under this lock: the frontend thread
+        # (keyframe broadcasts, relocalisation) and the backend worker thread
+        # (pair batches) may both hold a shard, and the serving ranks read
+        # the tasks strictly in order.
+        self.lock = threading.RLock()
 
     # ------------------------------------------------------------ tasks ---
     def _header(self, op=0, a=0, b=0):
         h = torch.tensor([op, a, b], dtype=torch.int64, device=self.device)
         if self.ws > 1:
             _staged(h, lambda t: dist.broadcast(t, 0))
+        if self.rank == 0:
+            return [op, a, b]          # no host read of the broadcast on rank 0
         return [int(x) for x in h.tolist()]
 
     def _bcast(self, t):
@@ -166,16 +191,17 @@ class PairShard:
         if self.rank == 0:
             N, C = frame.feat.shape[-2:]
             H, W = (int(v) for v in frame.img_true_shape.reshape(-1)[:2].tolist())
-            self._header(OP_KEYFRAME, idx, (N << 32) | C)
-            dims = torch.tensor([H, W], dtype=torch.int64, device=self.device)
-            self._bcast(dims)
-            feat = frame.feat.reshape(1, N, C).float().contiguous()
-            self._bcast(feat)
-            pos = frame.pos.reshape(1, N, 2).contiguous()
-            # the image too: the map's colours are RGB2SH(image) + the
-            # predicted residual (splatt3r_utils.py:250-257)
-            img = frame.img.reshape(1, 3, H, W).float().contiguous()
-            self._bcast(img)
+            with self.lock:
+                self._header(OP_KEYFRAME, idx, (N << 32) | C)
+                dims = torch.tensor([H, W], dtype=torch.int64, device=self.device)
+                self._bcast(dims)
+                feat = frame.feat.reshape(1, N, C).float().contiguous()
+                self._bcast(feat)
+                pos = frame.pos.reshape(1, N, 2).contiguous()
+                # the image too: the map's colours are RGB2SH(image) + the
+                # predicted residual (splatt3r_utils.py:250-257)
+                img = frame.img.reshape(1, 3, H, W).float().contiguous()
+                self._bcast(img)
         else:
             raise RuntimeError("broadcast_keyframe is called on rank 0; workers use serve()")
         self.kf[idx] = (feat, pos, torch.tensor([[H, W]], dtype=torch.int32), img)
@@ -218,38 +244,65 @@ class PairShard:
         n = len(pairs)
         if self.ws == 1:
             return self._run_local(pairs)
-        self._header(OP_PAIRS, n)
-        pl = torch.tensor(pairs, dtype=torch.int64, device=self.device).reshape(n, 2)
-        self._bcast(pl)
-        return self._pairs_collective(pairs)
+        with self.lock:
+            self._header(OP_PAIRS, n)
+            pl = torch.tensor(pairs, dtype=torch.int64, device=self.device).reshape(n, 2)
+            self._bcast(pl)
+            return self._pairs_collective(pairs)
+
+    def _run_units(self, units):
+        """This rank's directed units (a, b): one batched decode + matching,
+        idx_a2b [k, hw], valid [k, hw] and the add_factors weighting
+        Q = sqrt(Q_aa[idx_a2b] * Q_ba) [k, hw] (global_opt.py:56-66, the same
+        expression as q_weighted for each direction)."""
+        if not units:
+            return None
+        cat = lambda s, f: torch.cat([self.kf[u[s]][f] for u in units])
+        idx, valid, Qaa, Qba = self.match_dir_fn(cat(0, 0), cat(0, 1), cat(1, 0), cat(1, 1),
+                                                 [self.kf[a][2] for a, _ in units],
+                                                 [self.kf[b][2] for _, b in units])
+        b = torch.arange(idx.shape[0], device=idx.device)[:, None].repeat(1, idx.shape[1])
+        Q = torch.sqrt(Qaa[b, idx] * Qba)
+        self.stats["units"] += len(units)
+        return idx, valid.reshape(idx.shape), Q.reshape(idx.shape)
+
+    @staticmethod
+    def units(pairs):
+        """Unit u = 2 p + d of pair p = (i, j): d = 0 decodes (i, j), d = 1
+        decodes (j, i)."""
+        return [u for i, j in pairs for u in ((i, j), (j, i))]
 
     def _pairs_collective(self, pairs):
         ws, rank = self.ws, self.rank
-        n = len(pairs)
-        mine = shard(pairs, ws, rank)
-        res = self._run_local(mine)
-        per = -(-n // ws)
-        feat, _, shp = self.kf[pairs[0][0]][:3]
+        units = self.units(pairs)
+        nu = len(units)
+        mine = shard(units, ws, rank)
+        res = self._run_units(mine)
+        per = -(-nu // ws)
+        shp = self.kf[pairs[0][0]][2]
         hw = int(shp.reshape(-1)[0]) * int(shp.reshape(-1)[1])
+        ds = _img_downsample()
+        if ds > 1:
+            H, W = int(shp.reshape(-1)[0]), int(shp.reshape(-1)[1])
+            hw = -(-H // ds) * -(-W // ds)
         dev = self.device
-        idx = torch.zeros(per, 2, hw, dtype=torch.int64, device=dev)
-        val = torch.zeros(per, 2, hw, dtype=torch.uint8, device=dev)
-        q = torch.zeros(per, 2, hw, dtype=torch.float32, device=dev)
+        idx = torch.zeros(per, hw, dtype=torch.int64, device=dev)
+        val = torch.zeros(per, hw, dtype=torch.uint8, device=dev)
+        q = torch.zeros(per, hw, dtype=torch.float32, device=dev)
         if res is not None:
             k = len(mine)
-            idx[:k, 0], idx[:k, 1] = res[0], res[1]
-            val[:k, 0], val[:k, 1] = res[2][..., 0], res[3][..., 0]
-            q[:k, 0], q[:k, 1] = res[4][..., 0], res[5][..., 0]
+            idx[:k], val[:k], q[:k] = res[0], res[1], res[2]
         idx_all = _all_gather_equal(idx, ws)
         val_all = _all_gather_equal(val, ws)
         q_all = _all_gather_equal(q, ws)
         if rank != 0:
             return None
-        # pair p sits on rank p % ws at local slot p // ws
-        order = [(p % ws, p // ws) for p in range(n)]
-        I = torch.stack([idx_all[r][s] for r, s in order])
-        V = torch.stack([val_all[r][s] for r, s in order]).bool()
-        Qt = torch.stack([q_all[r][s] for r, s in order])
+        # unit u sits on rank u % ws at local slot u // ws; pair p = units 2p, 2p + 1
+        at = lambda parts, u: parts[u % ws][u // ws]
+        I = torch.stack([at(idx_all, u) for u in range(nu)]).reshape(len(pairs), 2, hw)
+        V = torch.stack([at(val_all, u) for u in range(nu)]).reshape(len(pairs), 2, hw).bool()
+        Qt = torch.stack([at(q_all, u) for u in range(nu)]).reshape(len(pairs), 2, hw)
+        self.stats["pairs"] += len(pairs)
         return I[:, 0], I[:, 1], V[:, 0, :, None], V[:, 1, :, None], Qt[:, 0, :, None], \
             Qt[:, 1, :, None]
 
@@ -265,12 +318,14 @@ class PairShard:
         poses = poses.reshape(-1, 8).float().contiguous()
         hp = (float(spatial_stride), float(depth_max_percentile), float(max_scale),
               float(min_confidence), float(opacity_threshold))
-        if self.ws > 1:
+        if self.ws == 1:
+            return self._map_collective(pairs, poses, hp)
+        with self.lock:
             self._header(OP_MAP, len(pairs), poses.shape[0])
             self._bcast(torch.tensor(pairs, dtype=torch.int64, device=self.device).reshape(-1, 2))
             self._bcast(poses)
             self._bcast(torch.tensor(hp, dtype=torch.float64, device=self.device))
-        return self._map_collective(pairs, poses, hp)
+            return self._map_collective(pairs, poses, hp)
 
     def _map_collective(self, pairs, poses, hp) -> MapRecords:
         """Fixed-capacity exchange: every rank pads its pairs' records to
@@ -357,7 +412,21 @@ class PairShard:
 
     def stop(self):
         if self.rank == 0 and self.ws > 1:
-            self._header(OP_STOP)
+            with self.lock:
+                self._header(OP_STOP)
+
+
+def serve_backend(model, device, gmap=None, match_dir_fn=None, map_fn=None, map_cap=None):
+    """Ranks 1..W-1 of a sharded SLAM run: hold every keyframe rank 0
+    broadcasts and run this rank's share of each pair batch / map refresh
+    (the reference's backend process, main.py:122-190, spread over GPUs)
+    until rank 0's Backend.stop().  Returns the rank's PairShard."""
+    sh = PairShard(model, device, gmap=gmap, match_dir_fn=match_dir_fn, map_fn=map_fn,
+                   map_cap=map_cap)
+    if sh.rank == 0:
+        raise RuntimeError("serve_backend runs on ranks > 0; rank 0 runs the Frontend + Backend")
+    sh.serve()
+    return sh
 
 
 @torch.inference_mode()

@@ -308,6 +308,28 @@ def splatt3r_match_symmetric(model, feat_i, pos_i, feat_j, pos_j, shape_i, shape
             Qjj.reshape(b, -1, 1), Qji.reshape(b, -1, 1), Qij.reshape(b, -1, 1))
 
 
+def splatt3r_match_directed(model, feat_a, pos_a, feat_b, pos_b, shape_a, shape_b,
+                            tag="backend"):
+    """One direction of splatt3r_match_symmetric (splatt3r_utils.py:539-576)
+    for b ordered pairs (a, b): decode (a, b) once, match view a's own
+    prediction against view b's prediction in a's frame.  Returns idx_a2b
+    [b, hw], valid [b, hw, 1], Q_aa, Q_ba [b, hw, 1]: exactly the first half
+    of the symmetric call's outputs for (a, b), or the second half for (b, a)
+    -- so a pair's two directions can run on two ranks (pairs.PairShard).
+    Every operation is per pair or per pixel, and the backend pair plans are
+    batch-invariant, so the outputs do not depend on which pairs share a
+    batch."""
+    H, W = _hw(shape_a)
+    r11, r21, _ = model.encoder.infer_pair(feat_a, pos_a, feat_b, pos_b, (H, W), tag=tag)
+    X, C, D, Q = (torch.stack((r11[k], r21[k]), 0)
+                  for k in ("pts3d", "conf", "desc", "desc_conf"))
+    X, C, D, Q = downsample(X, C, D, Q)
+    b = X.shape[1]
+    idx, valid = matching.match(X[0].contiguous(), X[1].contiguous(), D[0].contiguous(),
+                                D[1].contiguous())
+    return idx, valid, Q[0].reshape(b, -1, 1).clone(), Q[1].reshape(b, -1, 1).clone()
+
+
 # ------------------------------------------------------------- rendering ---
 def _sim3_to_4x4(T_sim3):
     """splatt3r_utils.py:153-165: [sR | t; 0 0 0 1] (float32)."""

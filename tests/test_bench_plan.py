@@ -78,6 +78,11 @@ def test_gpus_flag_spawns_ranks_without_a_launcher():
     d = json.loads(lines[0])
     assert d["world_size"] == 2 and d["n_gpus"] == 2 and d["dist_backend"] == "gloo"
     assert d["pairs_covered"] == d["pairs"]
+    # the sharded backend leg's protocol: rank 0's worker thread + PairShard,
+    # rank 1 in serve_backend; every pair's two directed units ran somewhere
+    be = d["backend"]
+    assert be["keyframes"] == 9 and be["edges"] == be["pairs"] > 0
+    assert be["units_all_ranks"] == 2 * be["pairs"] and 0 < be["rank0_units"] < 2 * be["pairs"]
 
 
 def test_world_size_must_match_gpus():

@@ -28,23 +28,29 @@ def _free_port():
     return p
 
 
-def fake_match(feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
-    """Deterministic stand-in for splatt3r_match_symmetric (no network on the
-    CPU): the 8-tuple's shapes and dtypes, values derived from the keyframe
-    features so every pair differs."""
-    b = feat_i.shape[0]
-    H, W = (int(v) for v in shape_i[0].reshape(-1)[:2])
+def fake_match_dir(feat_a, pos_a, feat_b, pos_b, shape_a, shape_b):
+    """Deterministic stand-in for splatt3r_match_directed (no network on the
+    CPU): (idx_a2b, valid, Q_aa, Q_ba) with its shapes and dtypes, values
+    derived from the keyframe features so every ordered pair differs."""
+    H, W = (int(v) for v in shape_a[0].reshape(-1)[:2])
     hw = H * W
-    ki = feat_i[:, 0, 0].round().long()
-    kj = feat_j[:, 0, 0].round().long()
+    ka = feat_a[:, 0, 0].round().long()
+    kb = feat_b[:, 0, 0].round().long()
     ar = torch.arange(hw)
-    idx_i2j = (ar[None] * (ki[:, None] + 1) + kj[:, None] * 7) % hw
-    idx_j2i = (ar[None] * (kj[:, None] + 1) + ki[:, None] * 5) % hw
-    valid_j = ((ar[None] + ki[:, None]) % 3 != 0)[..., None]
-    valid_i = ((ar[None] + kj[:, None]) % 4 != 0)[..., None]
+    idx = (ar[None] * (ka[:, None] + 1) + kb[:, None] * 7) % hw
+    valid = ((ar[None] + ka[:, None] + 2 * kb[:, None]) % 3 != 0)[..., None]
     q = lambda s: (1.0 + ((ar[None] * (s[:, None] + 2)) % 11).float() * (s[:, None] + 1).float()
                    / 5.0)[..., None]
-    return idx_i2j, idx_j2i, valid_j, valid_i, q(ki), q(kj), q(ki + kj), q(ki * 2 + kj)
+    return idx, valid, q(ka), q(ka * 2 + kb)
+
+
+def fake_match(feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
+    """The symmetric 8-tuple (splatt3r_match_symmetric's order) of the two
+    directed stand-ins, as the network's symmetric call is its two
+    directions."""
+    a = fake_match_dir(feat_i, pos_i, feat_j, pos_j, shape_i, shape_j)
+    b = fake_match_dir(feat_j, pos_j, feat_i, pos_i, shape_j, shape_i)
+    return a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3]
 
 
 def _kf_frames(n, H=32, W=48):
@@ -74,7 +80,7 @@ def _shard_worker(rank, ws, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     from splatt3r_amd.global_opt import FactorGraph
     from splatt3r_amd.pairs import PairShard
-    sh = PairShard(None, "cpu", match_fn=fake_match)
+    sh = PairShard(None, "cpu", match_fn=fake_match, match_dir_fn=fake_match_dir)
     if rank == 0:
         frames = _kf_frames(6)
         for k, f in enumerate(frames):
@@ -112,9 +118,11 @@ def test_sharded_add_factors_matches_single_rank_gloo(ws):
     for k, v in _edges(fg).items():
         np.testing.assert_array_equal(edges[k], v.numpy(), err_msg=k)
     assert len(edges["ii"]) > 0
-    # every rank received every keyframe and ran its share of the pairs
+    # every rank received every keyframe and ran its share of the pairs'
+    # directed units (two per pair: no rank idles on a small batch)
     n_pairs = sum(len(ps) for ps in PAIRS)
-    assert sum(res[r]["pairs"] if r else st0["pairs"] for r in range(ws)) == n_pairs
+    assert sum(res[r]["units"] if r else st0["units"] for r in range(ws)) == 2 * n_pairs
+    assert st0["pairs"] == n_pairs
     assert all((res[r] if r else st0)["keyframes"] == 6 for r in range(ws))
 
 
@@ -178,7 +186,7 @@ def _gpu_shard_worker(rank, ws, port, q):
     _beat(rank, "process group up")
     try:
         from splatt3r_amd.frame import Keyframes, create_frame
-        from splatt3r_amd.pairs import PairShard, q_weighted, shard
+        from splatt3r_amd.pairs import PairShard, q_weighted
         from splatt3r_amd.splatt3r_utils import load_splatt3r, splatt3r_match_symmetric
         from splatt3r_amd.synthetic import tum_like_sequence
         from splatt3r_amd.weights import FULL
@@ -198,22 +206,15 @@ def _gpu_shard_worker(rank, ws, port, q):
             _beat(rank, "keyframes broadcast")
             got = sh.match_pairs([p[0] for p in pairs], [p[1] for p in pairs])
             _beat(rank, "pairs gathered")
-            # the same per-rank batches decoded locally, reassembled in order
-            want = [None] * len(pairs)
-            for r in range(ws):
-                mine = shard(pairs, ws, r)
-                cat = lambda ks, a: torch.cat([getattr(kfs[k], a) for k in ks])
-                m = splatt3r_match_symmetric(model, cat([p[0] for p in mine], "feat"),
-                                             cat([p[0] for p in mine], "pos"),
-                                             cat([p[1] for p in mine], "feat"),
-                                             cat([p[1] for p in mine], "pos"),
-                                             [kfs[0].img_true_shape] * len(mine),
-                                             [kfs[0].img_true_shape] * len(mine))
-                res = q_weighted(m, sh.Q_conf)
-                for s_, p in enumerate(range(r, len(pairs), ws)):
-                    want[p] = [t[s_] for t in res]
-            ok = all(torch.equal(got[k][p], want[p][k]) for p in range(len(pairs))
-                     for k in range(6))
+            # the single-rank answer: one symmetric decode of every pair (the
+            # batch-invariant backend plans make the rank split irrelevant)
+            cat = lambda ks, a: torch.cat([getattr(kfs[k], a) for k in ks])
+            ii, jj = [p[0] for p in pairs], [p[1] for p in pairs]
+            m = splatt3r_match_symmetric(model, cat(ii, "feat"), cat(ii, "pos"), cat(jj, "feat"),
+                                         cat(jj, "pos"), [kfs[0].img_true_shape] * len(pairs),
+                                         [kfs[0].img_true_shape] * len(pairs))
+            want = q_weighted(m, sh.Q_conf)
+            ok = all(torch.equal(got[k], want[k]) for k in range(6))
             # the global-map refresh: keyframe k re-inferred against partner
             # k+1 (k-1 for the last) on rank k mod 2, world records at its
             # pose, all-gathered into both ranks' maps
@@ -248,7 +249,7 @@ def _gpu_shard_worker(rank, ws, port, q):
             sh.serve()
             _beat(rank, "served")
             n = sh.gmap.n_gaussians
-            q.put((rank, (sh.stats["pairs"], n, sh.gmap.means[:n].double().sum().item())))
+            q.put((rank, (sh.stats["units"], n, sh.gmap.means[:n].double().sum().item())))
     except Exception as e:           # report instead of leaving the peer blocked
         q.put((rank, f"error: {e!r}"))
         raise
@@ -259,9 +260,10 @@ def _gpu_shard_worker(rank, ws, port, q):
 @pytest.mark.gpu
 def test_sharded_pairs_two_ranks_on_gpu_match_local_decode():
     """Two ranks on the GPU (gloo transport staged through the host): keyframe
-    features broadcast from rank 0, pairs decoded on rank p mod 2 with the
-    real network, idx/valid/Q gathered back in pair order -- identical to
-    decoding the same per-rank batches locally.  Then the global-map refresh
+    features broadcast from rank 0, each pair's two directions decoded as
+    units on ranks u mod 2 with the real network, idx/valid/Q gathered back
+    in pair order -- bit-identical to one symmetric decode of all pairs on a
+    single rank (batch-invariant backend plans).  Then the global-map refresh
     (PairShard.refresh_map): edges re-inferred across the ranks, filtered
     world records all-gathered into both ranks' SharedGaussians -- both maps
     equal the single-rank map and render_map of it is bit-identical."""
@@ -287,7 +289,7 @@ def test_sharded_pairs_two_ranks_on_gpu_match_local_decode():
     ok, map_ok, render_ok, n0, sum0 = res[0]
     pairs1, n1, sum1 = res[1]
     assert ok is True
-    assert pairs1 == 2          # pairs 1 and 3 ran on rank 1
+    assert pairs1 == 5          # units 1, 3, .., 9: the (j, i) direction of every pair
     # refresh_map: both ranks hold the same map, equal to the single-rank map,
     # and its render is bit-identical
     assert map_ok and render_ok
@@ -325,7 +327,7 @@ def _map_worker(rank, ws, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     from splatt3r_amd.pairs import PairShard
-    sh = PairShard(None, "cpu", match_fn=fake_match, map_fn=fake_map,
+    sh = PairShard(None, "cpu", match_fn=fake_match, map_fn=fake_map, match_dir_fn=fake_match_dir,
                    map_cap=lambda pairs, hp: FAKE_CAP)
     poses = torch.arange(6 * 8, dtype=torch.float32).reshape(6, 8) * 0.1
     if rank == 0:
