@@ -17,6 +17,9 @@ int launch_t7(int tile, const GemmP& p, hipStream_t st) {
   if (tile == 34) return launch<256, 128, 2, 4, 2, 64, 1, 32>(p, st);
   if (tile == 35) return launch<128, 256, 2, 2, 4, 64, 1, 32>(p, st);
   if (tile == 36) return launch<256, 128, 3, 4, 2, 64, 1, 16>(p, st);
+  // (deep rings of 4-6 stages for the small 1536-row decoder grids were
+  // slower on every decoder shape: fewer workgroups per CU hide less of the
+  // per-step latency than the extra tiles in flight, profiles/r05c)
   return launch<128, 128, 3, 2, 4, 64, 1, 16>(p, st);
 }
 int sat_t7(int reset) { return read_sat(reset); }

@@ -28,6 +28,7 @@ encoded exactly once from its own image, with M = 768k-row GEMMs.
 """
 from __future__ import annotations
 
+import contextlib
 import queue
 import threading
 import time
@@ -280,6 +281,12 @@ class Frontend:
         # critical path and the encoder fills the CUs it leaves idle
         self.main_stream = (_shared_stream(device, main_priority, "main")
                             if main_priority is not None and self.enc_stream is not None else None)
+        # the no-viz gaussians_to_world records of every tracked frame (the
+        # reference computes them and drops them, main.py:467-488) run on a
+        # side stream once the pose is known, off the frame's main chain;
+        # their consumers (stats, drain) wait for it
+        self.aux_stream = _shared_stream(device, 0, "aux") if self.enc_stream is not None else None
+        self._aux_used = False
 
     def _prefetch(self, i, imgs):
         """Create frames i, i+1, ... for `imgs` and queue their encoder on
@@ -355,6 +362,7 @@ class Frontend:
         for t in self._tickets:
             t.done.wait()
         self._tickets = []
+        self._aux_join()
         if self._pending:
             # on the stream the renders were issued on (their buffers belong to it)
             st = self.main_stream if self.main_stream is not None else \
@@ -448,7 +456,7 @@ class Frontend:
             saved = frame.T_WC
             frame.T_WC = T_WC
             try:
-                recs = self._world_records(frame)
+                recs = self._world_records_aux(frame)
                 if not self.render:
                     img = None
                 elif self._rworker is not None:
@@ -589,10 +597,35 @@ class Frontend:
             # device count, in viz mode only.
             return True if total is not None and int(total.item()) > 0 else None
         # viz off: the reference computes gaussians_to_world and drops the
-        # result (main.py:467-488); the same records are computed here and
-        # kept on the device with their device count (frame.gs_world), so
-        # the tracked frame pays no host sync for the count
-        return self._keep_world_records(frame, self._world_records(frame))
+        # result (main.py:467-488); the same records are computed here (on
+        # the aux stream) and kept on the device with their device count
+        # (frame.gs_world), so the tracked frame pays no host sync for the count
+        return self._keep_world_records(frame, self._world_records_aux(frame))
+
+    def _world_records_aux(self, frame):
+        """_world_records on the aux stream (no-viz path): ordered after the
+        calling stream's work so far (the pose, the predictions), inputs kept
+        alive for the aux stream, outputs allocated there."""
+        if self.aux_stream is None or self.gmap is not None or frame.gaussian_pred is None:
+            return self._world_records(frame)
+        cur = torch.cuda.current_stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        ins = [t for t in frame.gaussian_pred.values() if torch.is_tensor(t)]
+        ins += [frame.img, frame.T_WC.data]
+        with torch.cuda.stream(self.aux_stream):
+            self.aux_stream.wait_event(ready)
+            recs = self._world_records(frame)
+        for t in ins:
+            if t.is_cuda:
+                t.record_stream(self.aux_stream)
+        self._aux_used = True
+        return recs
+
+    def _aux_join(self):
+        """The current stream waits for the aux stream's world records."""
+        if self._aux_used and self.aux_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.aux_stream)
 
     def _world_records(self, frame):
         a = self.gs_args
@@ -612,8 +645,12 @@ class Frontend:
     def _keep_world_records(self, frame, recs):
         if recs is None:
             return None
-        for _, cnt in recs:
-            self._gw_count = cnt.clone() if self._gw_count is None else self._gw_count + cnt
+        # the running count on the stream that produced the records
+        ctx = (torch.cuda.stream(self.aux_stream) if self._aux_used and self.gmap is None
+               else contextlib.nullcontext())
+        with ctx:
+            for _, cnt in recs:
+                self._gw_count = cnt.clone() if self._gw_count is None else self._gw_count + cnt
         frame.gs_world = recs
         return recs
 
@@ -622,6 +659,7 @@ class Frontend:
         """Frame counters; `gaussians_world` is read from its device counter
         here (a host sync), never inside step()."""
         if self._gw_count is not None:
+            self._aux_join()
             self._stats["gaussians_world"] = int(self._gw_count.item())
         return self._stats
 

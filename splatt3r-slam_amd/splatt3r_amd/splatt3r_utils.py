@@ -452,10 +452,14 @@ _WS: dict = {}
 
 
 def _workspace(dev, n):
+    """The s3w scratch of the calling stream: one per (device, stream), so
+    the frontend's world records (main or aux stream) and the backend
+    worker's map refresh (its own stream) never share one concurrently."""
     need = _lib.lib().s3w_workspace_bytes(n)
-    ws = _WS.get(dev)
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    ws = _WS.get(key)
     if ws is None or ws.numel() < need:
-        ws = _WS[dev] = torch.empty(need, dtype=torch.uint8, device=dev)
+        ws = _WS[key] = torch.empty(need, dtype=torch.uint8, device=dev)
     return ws
 
 

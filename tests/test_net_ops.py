@@ -52,14 +52,16 @@ def test_gemm_dense_bias_residual(M, N, K, groups):
     (768, 1024, 1088, 1, 1, 20), (64, 64, 64, 1, 1, 16), (520, 384, 640, 2, 2, 16),
     (300, 256, 200, 1, 1, 20),
     # v_mfma_f32_16x16x32 tiles (21-31): ragged M / N / K tails, global split-K
-    (768, 3072, 1024, 1, 1, 21), (130, 300, 968, 2, 1, 21), (768, 768, 768, 2, 1, 22),
-    (300, 200, 1000, 1, 3, 22), (768, 4096, 1024, 1, 1, 23), (520, 300, 640, 2, 2, 23),
+    # (N % 8 == 0: these tiles need the vector epilogue, see
+    # test_gemm_mf16_tiles_reject_unaligned_n)
+    (768, 3072, 1024, 1, 1, 21), (130, 296, 968, 2, 1, 21), (768, 768, 768, 2, 1, 22),
+    (300, 200, 1000, 1, 3, 22), (768, 4096, 1024, 1, 1, 23), (520, 296, 640, 2, 2, 23),
     (768, 3072, 768, 2, 1, 24), (700, 256, 2304, 1, 1, 24), (768, 1600, 1792, 2, 1, 25),
     (300, 136, 520, 1, 1, 25), (768, 1024, 1024, 1, 1, 26), (64, 64, 136, 1, 2, 26),
     (768, 2304, 768, 2, 1, 27), (130, 96, 2000, 2, 1, 27), (600, 256, 200, 1, 1, 28),
-    (768, 768, 3072, 2, 3, 29), (300, 500, 1000, 1, 1, 29), (768, 3072, 1024, 1, 1, 30),
-    (200, 96, 200, 2, 5, 30), (768, 1024, 4096, 1, 2, 31), (130, 300, 968, 1, 1, 31),
-    (1536, 2304, 768, 2, 1, 32), (130, 300, 968, 1, 2, 32), (6144, 1024, 1024, 1, 1, 34),
+    (768, 768, 3072, 2, 3, 29), (300, 496, 1000, 1, 1, 29), (768, 3072, 1024, 1, 1, 30),
+    (200, 96, 200, 2, 5, 30), (768, 1024, 4096, 1, 2, 31), (130, 296, 968, 1, 1, 31),
+    (1536, 2304, 768, 2, 1, 32), (130, 296, 968, 1, 2, 32), (6144, 1024, 1024, 1, 1, 34),
     (300, 200, 1000, 2, 3, 34), (1536, 768, 3072, 1, 1, 35), (520, 300, 640, 1, 1, 35),
     (6144, 4096, 1024, 1, 1, 36), (130, 96, 2000, 2, 2, 36), (1536, 3072, 768, 2, 1, 37),
     (64, 64, 136, 1, 1, 37),
@@ -115,9 +117,10 @@ def test_gemm_implicit_conv_split_k(split, tile, Cin):
     (65, 3, 1536, 768, 3072, 2, 1), (68, 36, 768, 6400, 1792, 2, 2), (68, 25, 520, 296, 640, 1, 1)])
 def test_gemm_pp_tiles_bitexact_vs_same_reduction_class(pp, ref, M, N, K, groups, split):
     """k_gemm_pp (net_gemm_t8.hip: its own two-half register pipeline and
-    stage reuse) computes every element with the same MFMA k order as a
-    k_gemm tile of the same ops.reduction_class: bit-identical outputs, with
-    the full epilogue, ragged tails and split-K."""
+    stage reuse) computes every element with the same
+    MFMA k order as a k_gemm tile of the same ops.reduction_class:
+    bit-identical outputs, with the full epilogue, ragged tails and split-K
+    (ADVICE r04)."""
     from splatt3r_amd import ops, _lib
     assert ops.reduction_class(K, pp, split) == ops.reduction_class(K, ref, split)
     A = [_rand(M, K, seed=g) for g in range(groups)]
@@ -133,6 +136,20 @@ def test_gemm_pp_tiles_bitexact_vs_same_reduction_class(pp, ref, M, N, K, groups
         outs.append(C)
     for x, y in zip(*outs):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("tile", [21, 26, 32, 36, 63, 68])
+def test_gemm_mf16_tiles_reject_unaligned_n(tile):
+    """A 16x16x32 tile stages its fp32 tile through LDS (vector epilogue:
+    N % 8 == 0, aligned operands); with N % 8 != 0 the launch fails instead of
+    silently running another tile (which would change its reduction class,
+    ops.reduction_class)."""
+    from splatt3r_amd import ops, _lib
+    M, N, K = 130, 300, 968
+    A, W = [_rand(M, K)], [_rand(N, K, scale=K ** -0.5, seed=1)]
+    C = [torch.empty(M, N, device="cuda")]
+    with pytest.raises(RuntimeError, match="vector epilogue"):
+        ops.gemm(A, W, C, M, N, K, lda=K, split_k=1, tile=tile)(_lib.stream())
 
 
 def test_gemm_split_k_is_deterministic():
