@@ -60,6 +60,14 @@ __device__ __forceinline__ int xcd_order(int b, int n) {
 
 __device__ __forceinline__ int kswz(int row, int c) { return c ^ ((row >> 1) & 7); }
 
+// 2^x as the bare v_exp_f32.  The library exp2f wraps it in a denormal-range
+// rescale (compare, select, add 64, exp, select, ldexp: six instructions
+// instead of one) for x < -126; the softmax arguments here are <= 0 and a
+// weight under 2^-126 is zero in the fp16 P operand and leaves the fp32 row
+// sum (>= 1) unchanged, so every output is the same bit for bit while the
+// per-key VALU work of the score tile drops by half.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // Rotate chunk `c` (8 dims) of a head row given both it and its partner
 // chunk c^2; returns the rotated chunk c.
 __device__ __forceinline__ f16x8 rope_chunk(f16x8 x, f16x8 partner, int c, int64_t py, int64_t px,
@@ -197,14 +205,14 @@ __global__ void __launch_bounds__(kThreads) k_attn(AttnP p) {
 #pragma unroll
       for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
       const float m_new = fmaxf(m_run[r], mx);
-      const float alpha = exp2f(m_run[r] - m_new);
+      const float alpha = fexp2(m_run[r] - m_new);
       m_run[r] = m_new;
       l_run[r] *= alpha;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) o[nb][r] *= alpha;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
-        const float e = exp2f(s[kb][r] - m_new);
+        const float e = fexp2(s[kb][r] - m_new);
         s[kb][r] = e;
         l_run[r] += e;
       }
@@ -395,14 +403,14 @@ __global__ void __launch_bounds__(kThreads) k_attn_dma(AttnP p) {
 #pragma unroll
       for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
       const float m_new = fmaxf(m_run[r], mx);
-      const float alpha = exp2f(m_run[r] - m_new);
+      const float alpha = fexp2(m_run[r] - m_new);
       m_run[r] = m_new;
       l_run[r] *= alpha;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) o[nb][r] *= alpha;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
-        const float e = exp2f(s[kb][r] - m_new);
+        const float e = fexp2(s[kb][r] - m_new);
         s[kb][r] = e;
         l_run[r] += e;
       }
@@ -585,7 +593,7 @@ __global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
     mx = fmaxf(mx, xchg16(mx));
     mx = fmaxf(mx, xchg32(mx));
     const float m_new = fmaxf(m_run, mx * p.scale_log2);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = fexp2(m_run - m_new);
     m_run = m_new;
     float ls = 0.f;
     {
@@ -596,7 +604,7 @@ __global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = exp2f(s[kb][r] * p.scale_log2 - m_new);
+          const float e = fexp2(s[kb][r] * p.scale_log2 - m_new);
           s[kb][r] = e;
           ls += e;
         }
@@ -656,7 +664,7 @@ __global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
       const float* rec = xs + (((s2 - 1) * QW + wave) * 64 + lane) * REC;
       const float m2 = rec[0];
       const float m = fmaxf(m_run, m2);
-      const float a1 = exp2f(m_run - m), a2 = exp2f(m2 - m);
+      const float a1 = fexp2(m_run - m), a2 = fexp2(m2 - m);
       l_run = l_run * a1 + rec[1] * a2;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb)
