@@ -162,13 +162,15 @@ def _ensure_encoded(model, frame):
         frame.feat, frame.pos, _ = model.encoder._encode_image(frame.img, frame.img_true_shape)
 
 
-def _stack_outputs(res):
+def _stack_outputs(res, clone=True):
     """torch.stack of the two heads' (pts3d, conf, desc, desc_conf) at batch
-    element 0: one copy when the plan keeps them in one block (net.py)."""
+    element 0: one copy when the plan keeps them in one block (net.py), or
+    (clone=False) views of that block, valid until the plan's next replay."""
     keys = ("pts3d", "conf", "desc", "desc_conf")
     r0, r1 = res
     if all(r0[k].shape[0] == 1 and _adjacent(r0[k], r1[k]) for k in keys):
-        X, C, D, Q = (t[:, 0] for t in _clone_together(_pair_view(r0[k], r1[k]) for k in keys))
+        pv = [_pair_view(r0[k], r1[k]) for k in keys]
+        X, C, D, Q = (t[:, 0] for t in (_clone_together(pv) if clone else pv))
         return downsample(X, C, D, Q)
     X = torch.stack([r["pts3d"][0] for r in res])
     C = torch.stack([r["conf"][0] for r in res])
@@ -222,13 +224,12 @@ def _decode_ahead(model, frame_i, frame_j, ahead):
         key, pp, runs = cached
         if key == _ahead_key(frame_i, frame_j) and pp.runs == runs:
             net.ahead_counts["used"] += 1
-            return _slot(pp.res[0], 1), _slot(pp.res[1], 1)
+            return _slot(pp.res[0], 1), _slot(pp.res[1], 1), _desc16(pp, 1)
         net.ahead_counts["dropped"] += 1
     nxt = ahead() if ahead is not None else None
     if (nxt is None or nxt.feat is None or nxt.img.shape != frame_i.img.shape
             or nxt.feat.shape != frame_i.feat.shape):
-        return decoder(model, frame_i.feat, frame_j.feat, frame_i.pos, frame_j.pos,
-                       frame_i.img_true_shape, frame_j.img_true_shape)
+        return _decode_alone(model, frame_i, frame_j)
     H, W = _hw(frame_i.img_true_shape)
     feat1 = torch.cat((frame_i.feat, nxt.feat))
     pos1 = torch.cat((frame_i.pos, nxt.pos))
@@ -236,32 +237,63 @@ def _decode_ahead(model, frame_i, frame_j, ahead):
                                 frame_j.pos.expand(2, -1, -1), (H, W))
     net._ahead_slot = (_ahead_key(nxt, frame_j), pp, pp.runs)
     net.ahead_counts["paired"] += 1
-    return _slot(r1, 0), _slot(r2, 0)
+    return _slot(r1, 0), _slot(r2, 0), _desc16(pp, 0)
+
+
+def _desc16(pp, b):
+    """The pair plan's fp16 descriptor copies of pair b (net.py PairPlan.desc16,
+    written by the Gaussian postprocess beside the fp32 desc) as [1, H, W, F]
+    views of (head 1, head 2): the matching kernels' fp16 operands without a
+    conversion pass; None when the plan has none."""
+    d = getattr(pp, "desc16", None)
+    return None if d is None else (d[0][b:b + 1], d[1][b:b + 1])
+
+
+def _decode_alone(model, frame_i, frame_j):
+    H, W = _hw(frame_i.img_true_shape)
+    r1, r2, pp = model.encoder.infer_pair(frame_i.feat, frame_i.pos, frame_j.feat, frame_j.pos,
+                                          (H, W))
+    return r1, r2, _desc16(pp, 0)
+
+
+def _tracker_decode(model, frame_i, frame_j, ahead=None):
+    """(res_self, res_cross, desc16 pair or None) of the tracked pair."""
+    _ensure_encoded(model, frame_i)
+    _ensure_encoded(model, frame_j)
+    if ahead is not None or getattr(model.encoder, "_ahead_slot", None) is not None:
+        return _decode_ahead(model, frame_i, frame_j, ahead)
+    return _decode_alone(model, frame_i, frame_j)
 
 
 @torch.inference_mode()
 def splatt3r_asymmetric_inference(model, frame_i, frame_j, ahead=None):
     """splatt3r_utils.py:580-607.  `ahead`: decode-ahead source of the next
     frame (see _decode_ahead); None decodes this pair alone."""
-    _ensure_encoded(model, frame_i)
-    _ensure_encoded(model, frame_j)
-    if ahead is not None or getattr(model.encoder, "_ahead_slot", None) is not None:
-        res11, res21 = _decode_ahead(model, frame_i, frame_j, ahead)
-    else:
-        res11, res21 = decoder(model, frame_i.feat, frame_j.feat, frame_i.pos, frame_j.pos,
-                               frame_i.img_true_shape, frame_j.img_true_shape)
+    res11, res21, _ = _tracker_decode(model, frame_i, frame_j, ahead)
     X, C, D, Q = _stack_outputs([res11, res21])
     return X, C, D, Q, (res11, res21)
 
 
 def splatt3r_match_asymmetric(model, frame_i, frame_j, idx_i2j_init=None, ahead=None):
-    """splatt3r_utils.py:610-644."""
-    X, C, D, Q, (res_self, res_cross) = splatt3r_asymmetric_inference(model, frame_i, frame_j,
-                                                                       ahead)
+    """splatt3r_utils.py:610-644.
+
+    The stacked (X, C, D, Q) the reference copies out (torch.stack) are
+    views of the pair plan's output block here: every consumer reads them on
+    the same stream before the plan's next replay (matching, the tracker's
+    correspondence pass) or copies what it keeps (Frame.update_pointmap
+    clones or fuses into new tensors), so the ~46 MB copy per tracked frame
+    is not made.  Matching reads the plan's fp16 descriptors (the values
+    .half() of the fp32 ones gives, written by the postprocess)."""
+    res_self, res_cross, d16 = _tracker_decode(model, frame_i, frame_j, ahead)
+    X, C, D, Q = _stack_outputs([res_self, res_cross], clone=False)
     frame_i.gaussian_pred = _extract_gaussian_params(res_self)
     frame_i.gaussian_pred_cross = _extract_gaussian_params(res_cross)
     b = X.shape[0] // 2
-    idx_i2j, valid_match_j = matching.match(X[:b], X[b:], D[:b], D[b:],
+    if d16 is not None and X.shape[0] == 2 and config["dataset"]["img_downsample"] == 1:
+        D1, D2 = d16
+    else:
+        D1, D2 = D[:b], D[b:]
+    idx_i2j, valid_match_j = matching.match(X[:b], X[b:], D1, D2,
                                             idx_1_to_2_init=idx_i2j_init)
     Xii, Xji = X.reshape(2 * b, -1, 3)[:b], X.reshape(2 * b, -1, 3)[b:]
     Cii, Cji = C.reshape(2 * b, -1, 1)[:b], C.reshape(2 * b, -1, 1)[b:]

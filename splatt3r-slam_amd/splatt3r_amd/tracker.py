@@ -318,8 +318,10 @@ class FrameTracker:
         new_kf = min(match_frac_k, unique_frac_f) < self.cfg["match_frac_thresh"]
         if new_kf:
             self.reset_idx_f2k()
+        # Qkf / Qff are views of the pair plan's outputs (splatt3r_match_asymmetric):
+        # copies for a caller that keeps the match info past this frame
         return (new_kf, [keyframe.X_canon, keyframe.get_average_conf(), frame.X_canon,
-                         frame.get_average_conf(), Qkf, Qff], False)
+                         frame.get_average_conf(), Qkf.clone(), Qff.clone()], False)
 
     def _host_K(self, K):
         """K as a host float32[9], cached per tensor (K is constant for a
