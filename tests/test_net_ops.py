@@ -152,6 +152,27 @@ def test_gemm_mf16_tiles_reject_unaligned_n(tile):
         ops.gemm(A, W, C, M, N, K, lda=K, split_k=1, tile=tile)(_lib.stream())
 
 
+def test_gemm_gelu_erf_accuracy():
+    """The GELU epilogue's erf (Abramowitz & Stegun 7.1.26 on v_rcp / v_exp,
+    net_gemm_kernel.hpp erf_fast) over x in [-12, 12]: |gelu - exact| <=
+    0.5 |x| 5e-7 + 2 ulp, i.e. far below the fp16 quantum the network stores
+    GELU outputs in."""
+    from splatt3r_amd import ops, _lib
+    M, N, K = 64 * 1024, 8, 8
+    x = torch.linspace(-12, 12, M, device="cuda")
+    A = torch.zeros(M, K, device="cuda", dtype=torch.float16)
+    A[:, 0] = x.half()
+    xv = A[:, 0].double()                      # the exact fp16 inputs
+    W = torch.zeros(N, K, device="cuda", dtype=torch.float16)
+    W[:, 0] = 1.0
+    C = torch.empty(M, N, device="cuda")
+    ops.gemm([A], [W], [C], M, N, K, lda=K, act="gelu")(_lib.stream())
+    ref = 0.5 * xv * (1.0 + torch.erf(xv / 2 ** 0.5))
+    err = (C[:, 0].double() - ref).abs()
+    bound = 0.5 * xv.abs() * 5e-7 + 6e-7 * ref.abs() + 1e-12
+    assert bool((err <= bound).all()), float((err / bound).max())
+
+
 def test_gemm_split_k_is_deterministic():
     from splatt3r_amd import ops, _lib
     M, N, K = 768, 1024, 4096
