@@ -863,6 +863,23 @@ def main(argv=None):
     if os.environ.get("S3_HOST_PHASES"):     # host time between tracker phases (diagnostic)
         phases = []
         fe.tracker.mark = lambda name: phases.append((len(host_ms), name, time.perf_counter()))
+    if os.environ.get("S3_STALL_TRACE"):
+        # diagnostic: a watchdog dumps every thread's Python stack when the
+        # host spends more than S3_STALL_TRACE ms in a frame's issue phases
+        # (step start -> GN queued, GN done -> step end; the GN wait itself
+        # is not armed)
+        import faulthandler
+        lim = float(os.environ["S3_STALL_TRACE"]) * 1e-3
+        prev = fe.tracker.mark if phases is not None else None
+
+        def _mark(name, prev=prev):
+            if prev is not None:
+                prev(name)
+            if name in ("step_begin", "gn_done"):
+                faulthandler.dump_traceback_later(lim, exit=False)
+            elif name in ("spec_queued", "step_end"):
+                faulthandler.cancel_dump_traceback_later()
+        fe.tracker.mark = _mark
     ms0 = torch.cuda.memory_stats(dev)
     for i in range(a.warmup + 1, nfr):
         h0 = time.perf_counter()
@@ -885,8 +902,12 @@ def main(argv=None):
     model.encoder.events = None
     encodes = _encodes(model.encoder) - enc0
     crit = _critical_path(fe, ev, t, a.steps, ev_t0) if fe.spans is not None else None
-    if phases is not None:
+    if os.environ.get("S3_STALL_TRACE"):
+        import faulthandler
+        faulthandler.cancel_dump_traceback_later()
+    if phases is not None or os.environ.get("S3_STALL_TRACE"):
         fe.tracker.mark = None
+    if phases is not None:
         if crit is not None:
             by = {}
             for k, name, tt in phases:
