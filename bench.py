@@ -671,6 +671,18 @@ def _critical_path(fe, net_events, wall_s, steps, ev_t0=None):
         out["last_enc_end_minus_last_chain_end_ms"] = round(off, 3)
     # main-stream idle between consecutive frames' chains, per frame
     out["idle_gaps_ms"] = [round(a[1].elapsed_time(b[0]), 3) for a, b in zip(mains, mains[1:])]
+    # gaps over 1 ms: which frame, and how the next chain's start sits
+    # against the nearest encoder batch end (~0 => it waited on the encoder)
+    ids = [i for tag, i, _, _ in fe.spans if tag == "main"]
+    big = []
+    for k, g in enumerate(out["idle_gaps_ms"]):
+        if g > 1.0:
+            b0 = mains[k + 1][0]
+            near = min((e1.elapsed_time(b0) for _, e1 in encs), key=abs, default=None)
+            big.append({"frame": ids[k + 1], "gap_ms": g,
+                        "chain_start_minus_nearest_enc_end_ms":
+                            None if near is None else round(near, 3)})
+    out["big_gaps"] = big
     return out
 
 
@@ -875,9 +887,10 @@ def main(argv=None):
         def _mark(name, prev=prev):
             if prev is not None:
                 prev(name)
-            if name in ("step_begin", "gn_done"):
+            if name in ("step_begin", "gn_done", "step_end"):
+                # (step_end arms the window between steps: the bench loop)
                 faulthandler.dump_traceback_later(lim, exit=False)
-            elif name in ("spec_queued", "step_end"):
+            elif name == "spec_queued":
                 faulthandler.cancel_dump_traceback_later()
         fe.tracker.mark = _mark
     ms0 = torch.cuda.memory_stats(dev)

@@ -40,9 +40,13 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21,
  * refine (1, 2, 4: per-lane kernel for radius 3 / fdim 24; 8, 16 = default,
  * 32, 64: cooperative kernel, also used for every other radius / fdim) and
  * the per-lane kernel's load distance in candidates (2, 3, 4 = default, 6);
- * results identical for every setting. */
+ * results identical for every setting.  s3m_refine_set_sort: visit the
+ * queries in the order of the 2^sx x 2^sy pixel tile holding their window
+ * centre (mode = 16 sx + sy, sx, sy <= 6; 0 = pixel order).  An
+ * out-of-range value (e.g. -1) restores the default. */
 void s3m_refine_set_lanes(int lanes);
 void s3m_refine_set_prefetch(int pf);
+void s3m_refine_set_sort(int mode);
 
 /* Fused prep_for_iter_proj (matching.py:25-49 + image.py:5-38):
  * rays = normalize(X11); rays_with_grad = [rays, Scharr_x(rays)/32,

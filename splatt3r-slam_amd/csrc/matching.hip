@@ -10,7 +10,10 @@
 #include "common.hpp"
 #include "s3m.h"
 
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 namespace {
 
@@ -199,7 +202,7 @@ template <int F, int kRefLanes = 16>
 __global__ void __launch_bounds__(kBlock)
 k_refine_coop(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
               const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
-              int n, int radius, int dilation_max) {
+              int n, int radius, int dilation_max, const int* __restrict__ perm) {
   constexpr int kRefMaxPer = 64 / kRefLanes;
   static_assert(F % 8 == 0, "16-B descriptor chunks");
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -208,7 +211,8 @@ k_refine_coop(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kRefLanes;
   const int64_t b = blockIdx.y;
   const bool live = i < n;                 // dead groups still join the shuffles
-  const int64_t pi = b * (int64_t)n + (live ? i : 0);
+  // perm (may be null): visiting order of the queries, see k_refine_bin
+  const int64_t pi = b * (int64_t)n + (live ? (perm ? perm[b * (int64_t)n + i] : i) : 0);
   const h8* q8 = reinterpret_cast<const h8*>(D21 + pi * F);
   h8 q[NC];
 #pragma unroll
@@ -299,7 +303,7 @@ template <int LPQ, int PF>
 __global__ void __launch_bounds__(kBlock)
 k_refine_lane(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
               const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
-              int n, int dilation_max) {
+              int n, int dilation_max, const int* __restrict__ perm) {
   constexpr int F = 24, CH = F / 8, R = 3, SIDE = 2 * R + 1;
   constexpr int RPL = (SIDE + LPQ - 1) / LPQ;   // window rows per lane
   constexpr int PER = SIDE * RPL;               // candidate slots per lane
@@ -312,7 +316,8 @@ k_refine_lane(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21
   const int64_t b = blockIdx.y;
   if (LPQ == 1 && i >= n) return;
   const bool live = i < n;                  // dead lanes still join the butterfly
-  const int64_t pi = b * (int64_t)n + (live ? i : 0);
+  // perm (may be null): visiting order of the queries, see k_refine_bin
+  const int64_t pi = b * (int64_t)n + (live ? (perm ? perm[b * (int64_t)n + i] : i) : 0);
   h2 q[F / 2];
   {
     const i4* q4 = reinterpret_cast<const i4*>(D21 + pi * F);
@@ -429,6 +434,78 @@ k_refine_lane(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21
   }
 }
 
+// Window-centre binning ahead of the refine.  On the
+// tracking loop the queries' window centres scatter (pixel order puts 64
+// queries of one frame row on 64 columns and several rows of the keyframe),
+// so the lanes of a wave each pull their own cache lines.  Visiting the
+// queries in the order of the 2^sx x 2^sy pixel tile that holds their p1
+// makes a wave's windows overlap: candidate k of every lane falls in one
+// tile-sized patch, shifted by the candidate offset, and the loads of the
+// wave share lines in the vector L1.  Counting sort in three launches: bin
+// (tile count + arrival rank), scan (tile offsets; re-zeroes the counts for
+// the next call), scatter (perm[offset + rank] = query).  Batch b's tiles
+// follow batch b-1's, so batch b's queries occupy perm[b n, (b+1) n).  The
+// order inside a tile is the atomic arrival order: a query's result depends
+// on its own inputs only, so every order gives the same bits.
+__device__ __forceinline__ int refine_tile(const int64_t* __restrict__ p1, int64_t pi, int h,
+                                           int w, int sx, int sy, int tiles_x) {
+  const int64_t u = p1[pi * 2 + 0], v = p1[pi * 2 + 1];
+  const int uc = (int)(u < 0 ? 0 : (u >= w ? w - 1 : u));
+  const int vc = (int)(v < 0 ? 0 : (v >= h ? h - 1 : v));
+  return (vc >> sy) * tiles_x + (uc >> sx);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_refine_bin(const int64_t* __restrict__ p1, int* __restrict__ cnt, int* __restrict__ rank, int h,
+             int w, int n, int sx, int sy, int tiles_x, int tiles) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (i >= n) return;
+  const int64_t pi = b * (int64_t)n + i;
+  rank[pi] = atomicAdd(&cnt[b * tiles + refine_tile(p1, pi, h, w, sx, sy, tiles_x)], 1);
+}
+
+constexpr int kScanBlock = 1024;
+
+// exclusive scan of the tile counts of every batch (one workgroup; a
+// contiguous run of tiles per thread), counts reset to zero
+__global__ void __launch_bounds__(kScanBlock)
+k_refine_scan(int* __restrict__ cnt, int* __restrict__ off, int total) {
+  __shared__ int wsum[kScanBlock / 64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int per = (total + kScanBlock - 1) / kScanBlock;
+  const int lo = t * per, hi = min(lo + per, total);
+  int s = 0;
+  for (int k = lo; k < hi; ++k) s += cnt[k];
+  int x = s;                                  // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  int run = x - s;
+  for (int k = 0; k < wv; ++k) run += wsum[k];
+  for (int k = lo; k < hi; ++k) {
+    const int c = cnt[k];
+    off[k] = run;
+    run += c;
+    cnt[k] = 0;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_refine_scatter(const int64_t* __restrict__ p1, const int* __restrict__ rank,
+                 const int* __restrict__ off, int* __restrict__ perm, int h, int w, int n, int sx,
+                 int sy, int tiles_x, int tiles) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (i >= n) return;
+  const int64_t pi = b * (int64_t)n + i;
+  perm[off[b * tiles + refine_tile(p1, pi, h, w, sx, sy, tiles_x)] + rank[pi]] = (int)i;
+}
+
 // |x| / max(||x||, 1e-12) (F.normalize), strict order ((x0^2+x1^2)+x2^2).
 __device__ __forceinline__ void normalize3(const float* x, float* o) {
   float nrm = sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
@@ -540,40 +617,112 @@ int s3m_iter_proj(const float* rays_img_with_grad, const float* pts_3d_norm,
 // every other call: tools/refine_stats.py), its lanes touch one cache line
 // each and the 16-lane kernel is faster (185 vs 208 us per call,
 // profiles/r04g_summary.txt)
-static int g_refine_lanes = 16;
+constexpr int kRefineLanesDefault = 16;
+// window-centre binning: 0 = off (pixel order), else 16 sx + sy for
+// 2^sx x 2^sy pixel tiles (k_refine_bin)
+constexpr int kRefineSortDefault = 0;
+static int g_refine_lanes = kRefineLanesDefault;
 static int g_refine_pf = 4;
+static int g_refine_sort = kRefineSortDefault;
+// (any other value, e.g. -1: the default)
 extern "C" void s3m_refine_set_lanes(int lanes) {
-  g_refine_lanes = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 32 || lanes == 64)
-                       ? lanes : 16;
+  g_refine_lanes = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 ||
+                    lanes == 32 || lanes == 64)
+                       ? lanes : kRefineLanesDefault;
 }
 extern "C" void s3m_refine_set_prefetch(int pf) {
   g_refine_pf = (pf == 2 || pf == 3 || pf == 6) ? pf : 4;
 }
+extern "C" void s3m_refine_set_sort(int mode) {
+  const int sx = mode >> 4, sy = mode & 15;
+  g_refine_sort = mode == 0 ? 0 : (mode > 0 && sx <= 6 && sy <= 6) ? mode : kRefineSortDefault;
+}
 
 }  // extern "C"
+
+// Device scratch of the binning, one per (device, stream): tile counts
+// (kept zero between calls: the scan resets them), tile offsets, arrival
+// ranks and the visiting order.  Grown, never shrunk; outgrown buffers are
+// left allocated (work queued on the stream may still read them).
+struct RefineScratch {
+  int* cnt = nullptr;
+  int* off = nullptr;
+  int* rank = nullptr;
+  int* perm = nullptr;
+  int64_t queries = 0, tiles = 0;
+};
+static std::mutex g_scratch_mu;
+static std::map<std::pair<int, hipStream_t>, RefineScratch> g_scratch;
+
+static int refine_scratch(hipStream_t st, int64_t queries, int64_t tiles, RefineScratch* out) {
+  int dev = 0;
+  S3_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  RefineScratch& s = g_scratch[{dev, st}];
+  if (s.tiles < tiles) {
+    int64_t t = 4096;
+    while (t < tiles) t *= 2;
+    S3_HIP(hipMalloc(&s.cnt, t * sizeof(int)));
+    S3_HIP(hipMalloc(&s.off, t * sizeof(int)));
+    S3_HIP(hipMemsetAsync(s.cnt, 0, t * sizeof(int), st));
+    s.tiles = t;
+  }
+  if (s.queries < queries) {
+    int64_t q = 1 << 16;
+    while (q < queries) q *= 2;
+    S3_HIP(hipMalloc(&s.rank, q * sizeof(int)));
+    S3_HIP(hipMalloc(&s.perm, q * sizeof(int)));
+    s.queries = q;
+  }
+  *out = s;
+  return S3_OK;
+}
+
+// the visiting order of the b x n queries (k_refine_bin), or null when
+// binning is off or the batch is too small to gain from it
+static int refine_order(const int64_t* p1, int b, int h, int w, int n, hipStream_t st,
+                        const int** perm) {
+  *perm = nullptr;
+  if (g_refine_sort == 0 || (int64_t)b * n < 2048) return S3_OK;
+  const int sx = g_refine_sort >> 4, sy = g_refine_sort & 15;
+  const int tiles_x = (int)s3::cdiv(w, 1 << sx), tiles = tiles_x * (int)s3::cdiv(h, 1 << sy);
+  const int64_t total = (int64_t)b * tiles;
+  S3_REQUIRE(total < (1 << 26) && (int64_t)b * n < 0x7fffffff, "s3m_refine_matches: batch too large to bin");
+  RefineScratch s;
+  const int rc = refine_scratch(st, (int64_t)b * n, total, &s);
+  if (rc != S3_OK) return rc;
+  dim3 grid((unsigned)s3::cdiv(n, kBlock), (unsigned)b);
+  k_refine_bin<<<grid, kBlock, 0, st>>>(p1, s.cnt, s.rank, h, w, n, sx, sy, tiles_x, tiles);
+  k_refine_scan<<<1, kScanBlock, 0, st>>>(s.cnt, s.off, (int)total);
+  k_refine_scatter<<<grid, kBlock, 0, st>>>(p1, s.rank, s.off, s.perm, h, w, n, sx, sy, tiles_x,
+                                            tiles);
+  S3_LAUNCH_CHECK();
+  *perm = s.perm;
+  return S3_OK;
+}
 
 template <int LPQ>
 static void launch_refine_lane(const _Float16* d11, const _Float16* d21, const int64_t* p1,
                                int64_t* p1_new, int b, int h, int w, int n, int dilation_max,
-                               hipStream_t st) {
+                               const int* perm, hipStream_t st) {
   dim3 grid((unsigned)s3::cdiv((int64_t)n * LPQ, kBlock), (unsigned)b);
   switch (g_refine_pf) {
-    case 2: k_refine_lane<LPQ, 2><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max); break;
-    case 4: k_refine_lane<LPQ, 4><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max); break;
-    case 6: k_refine_lane<LPQ, 6><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max); break;
-    default: k_refine_lane<LPQ, 3><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max); break;
+    case 2: k_refine_lane<LPQ, 2><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max, perm); break;
+    case 4: k_refine_lane<LPQ, 4><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max, perm); break;
+    case 6: k_refine_lane<LPQ, 6><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max, perm); break;
+    default: k_refine_lane<LPQ, 3><<<grid, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max, perm); break;
   }
 }
 
 static void refine_lane(const _Float16* d11, const _Float16* d21, const int64_t* p1,
                         int64_t* p1_new, int b, int h, int w, int n, int dilation_max,
-                        hipStream_t st) {
+                        const int* perm, hipStream_t st) {
   if (g_refine_lanes == 4)
-    launch_refine_lane<4>(d11, d21, p1, p1_new, b, h, w, n, dilation_max, st);
+    launch_refine_lane<4>(d11, d21, p1, p1_new, b, h, w, n, dilation_max, perm, st);
   else if (g_refine_lanes == 2)
-    launch_refine_lane<2>(d11, d21, p1, p1_new, b, h, w, n, dilation_max, st);
+    launch_refine_lane<2>(d11, d21, p1, p1_new, b, h, w, n, dilation_max, perm, st);
   else
-    launch_refine_lane<1>(d11, d21, p1, p1_new, b, h, w, n, dilation_max, st);
+    launch_refine_lane<1>(d11, d21, p1, p1_new, b, h, w, n, dilation_max, perm, st);
 }
 
 // the per-lane kernel: radius 3, fdim 24, one image of D11 addressable
@@ -594,23 +743,30 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* 
   dim3 grid((unsigned)s3::cdiv(n, kBlock), (unsigned)b);
   auto d11 = reinterpret_cast<const _Float16*>(D11);
   auto d21 = reinterpret_cast<const _Float16*>(D21);
+  auto st = s3::as_stream(stream);
   const int side = 2 * radius + 1;
-  if (g_refine_lanes <= 4 && refine_lane_ok(h, w, fdim, radius)) {
-    refine_lane(d11, d21, p1, p1_new, b, h, w, n, dilation_max, s3::as_stream(stream));
-  } else if (side * side <= 64 && (fdim == 24 || fdim == 16 || fdim == 32)) {
+  const bool lane_k = g_refine_lanes <= 4 && refine_lane_ok(h, w, fdim, radius);
+  const bool coop_k = side * side <= 64 && (fdim == 24 || fdim == 16 || fdim == 32);
+  const int* perm = nullptr;
+  if (lane_k || coop_k) {
+    const int rc = refine_order(p1, b, h, w, n, st, &perm);
+    if (rc != S3_OK) return rc;
+  }
+  if (lane_k) {
+    refine_lane(d11, d21, p1, p1_new, b, h, w, n, dilation_max, perm, st);
+  } else if (coop_k) {
     const int lanes = g_refine_lanes <= 4 ? 16 : g_refine_lanes;   // other radius / fdim
     dim3 cg((unsigned)s3::cdiv((int64_t)n * lanes, kBlock), (unsigned)b);
     auto go = [&](auto tag) {
       constexpr int F = decltype(tag)::value;
-      auto st = s3::as_stream(stream);
       if (lanes == 8)
-        k_refine_coop<F, 8><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max);
+        k_refine_coop<F, 8><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max, perm);
       else if (lanes == 32)
-        k_refine_coop<F, 32><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max);
+        k_refine_coop<F, 32><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max, perm);
       else if (lanes == 64)
-        k_refine_coop<F, 64><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max);
+        k_refine_coop<F, 64><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max, perm);
       else
-        k_refine_coop<F, 16><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max);
+        k_refine_coop<F, 16><<<cg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, radius, dilation_max, perm);
     };
     if (fdim == 24) go(std::integral_constant<int, 24>{});
     else if (fdim == 16) go(std::integral_constant<int, 16>{});

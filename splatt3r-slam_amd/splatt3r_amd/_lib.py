@@ -48,6 +48,7 @@ SIGNATURES: dict[str, tuple] = {
     "s3m_refine_matches": (I32, [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P]),
     "s3m_refine_set_lanes": (None, [I32]),
     "s3m_refine_set_prefetch": (None, [I32]),
+    "s3m_refine_set_sort": (None, [I32]),
     "s3m_prep_iter_proj": (I32, [P, P, P, P, P, P, I32, I32, I32, P]),
     "s3m_occlusion": (I32, [P, P, P, P, P, P, I32, I32, I32, F32, P]),
     "s3m_pixel_to_lin": (I32, [P, P, I64, I32, P]),

@@ -547,21 +547,25 @@ class Frontend:
             chk.sizing.rerenders += 1
             self._stats["rerendered"] += 1
             img = chk.rerender()
-        self._deliver_image(img, index, prefix)
+            ev = None                    # the re-render is newer than ev
+        self._deliver_image(img, index, prefix, ev)
         return True
 
-    def _deliver_image(self, img, index, prefix):
+    def _deliver_image(self, img, index, prefix, ready=None):
+        """Hand one render over (PNG writer, device tensor or the pinned
+        read-back ring).  `ready`: an event recorded after the render on its
+        stream (None: recorded here, on the current stream)."""
         if img is not None:
             if self.render_writer is not None:
                 self.render_writer.submit(index, img, prefix)
                 self._last_render, self._rb_event = None, None
                 return
-            out = img[0, 0].clamp(0, 1).permute(1, 2, 0)
             if not self.readback:
-                self._last_render, self._rb_event = out, None
+                self._last_render, self._rb_event = img[0, 0].clamp(0, 1).permute(1, 2, 0), None
                 return
-            if self._rb_bufs is None or self._rb_bufs[0].shape != out.shape:
-                self._rb_bufs = [torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
+            shape = (img.shape[-2], img.shape[-1], img.shape[-3])
+            if self._rb_bufs is None or tuple(self._rb_bufs[0].shape) != shape:
+                self._rb_bufs = [torch.empty(shape, dtype=img.dtype, pin_memory=True)
                                  for _ in range(self._RB_RING)]
                 self._rb_events = [None] * self._RB_RING
             k = self._rb_i
@@ -569,9 +573,23 @@ class Frontend:
             if self._rb_events[k] is not None:      # copy of _RB_RING renders ago
                 self._rb_events[k].synchronize()
             host = self._rb_bufs[k]
-            host.copy_(out, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
+            # The read-back runs on the aux stream behind the render only.
+            # At step start the main stream holds the next frames' queued
+            # work (a decode-ahead pair replay, ~6 ms), and a device-to-host
+            # copy issued there was caught holding the host until the stream
+            # reached it (one step in 6 runs: the 6 ms idle gap of
+            # profiles/r05h_stall_trace.log, stack in _deliver_image).
+            st = self.aux_stream if self.aux_stream is not None else torch.cuda.current_stream(
+                self.device)
+            if ready is None:
+                ready = torch.cuda.Event()
+                ready.record(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(st):
+                st.wait_event(ready)
+                host.copy_(img[0, 0].clamp(0, 1).permute(1, 2, 0), non_blocking=True)
+                img.record_stream(st)
+                ev = torch.cuda.Event()
+                ev.record(st)
             self._rb_events[k] = ev
             self._last_render, self._rb_event = host, ev
 

@@ -135,15 +135,17 @@ def test_hip_refine_bitexact_vs_oracle(f):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sort", [0, 0x33])
 @pytest.mark.parametrize("lanes,pf", [(1, 4), (1, 6), (2, 2), (2, 4), (4, 3), (16, 3)])
 @pytest.mark.parametrize("f,radius,dil", [(24, 3, 5), (24, 2, 3), (32, 1, 2), (24, 4, 2), (8, 3, 5)])
-def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil, lanes, pf):
+def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil, lanes, pf, sort):
     """Quantised descriptors make many equal fp16 scores: every kernel must
     keep the first candidate in the reference's scan order.  lanes 1 / 2 / 4
     = k_refine_lane with 1 / 2 / 4 lanes per query (radius 3, f 24; pf its
     load distance), 16 = k_refine_coop (the default); radius 4 (81
     candidates) and fdim 8 take the generic per-lane kernel.  Query points
-    up to 3 pixels off the image exercise the masked window slots."""
+    up to 3 pixels off the image exercise the masked window slots.  sort:
+    queries visited in window-centre tile order (8 x 8 tiles) or pixel order."""
     import mast3r_slam_backends as be
     from splatt3r_amd import _lib
     rng = np.random.default_rng(100 + f + radius)
@@ -155,12 +157,44 @@ def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil, lanes, pf):
     ref = oracle.refine_matches(D11, D21, p1, radius, dil)
     _lib.lib().s3m_refine_set_lanes(lanes)
     _lib.lib().s3m_refine_set_prefetch(pf)
+    _lib.lib().s3m_refine_set_sort(sort)
     try:
         (out,) = be.refine_matches(_to(D11), _to(D21), _to(p1), radius, dil)
     finally:
-        _lib.lib().s3m_refine_set_lanes(16)
+        _lib.lib().s3m_refine_set_lanes(-1)
         _lib.lib().s3m_refine_set_prefetch(4)
+        _lib.lib().s3m_refine_set_sort(-1)
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sort", [0x11, 0x60, 0x06, 0x42, 0x66])
+@pytest.mark.parametrize("lanes", [1, 4, 16])
+def test_hip_refine_tile_orders_vs_oracle(sort, lanes):
+    """Window-centre binning with lopsided tiles (2x2, 64x1, 1x64, 16x4,
+    64x64: one tile per image), three batches of different query spread
+    (one batch's centres all in one tile), off-image centres clamped into
+    the edge tiles, and a second call on the same stream (the scan re-zeroes
+    the tile counts): every order gives the oracle's bits."""
+    import mast3r_slam_backends as be
+    from splatt3r_amd import _lib
+    rng = np.random.default_rng(sort + lanes)
+    b, h, w, f = 3, 37, 61, 24
+    D11 = (rng.integers(-2, 3, size=(b, h, w, f)) * 0.125).astype(np.float16)
+    D21 = (rng.integers(-2, 3, size=(b, h * w, f)) * 0.125).astype(np.float16)
+    p1 = np.stack([rng.integers(-3, w + 3, size=(b, h * w)),
+                   rng.integers(-3, h + 3, size=(b, h * w))], -1).astype(np.int64)
+    p1[1] = (5, 7)                                  # batch 1: one window centre
+    ref = oracle.refine_matches(D11, D21, p1, 3, 5)
+    _lib.lib().s3m_refine_set_lanes(lanes)
+    _lib.lib().s3m_refine_set_sort(sort)
+    try:
+        for _ in range(2):
+            (out,) = be.refine_matches(_to(D11), _to(D21), _to(p1), 3, 5)
+            np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    finally:
+        _lib.lib().s3m_refine_set_lanes(-1)
+        _lib.lib().s3m_refine_set_sort(-1)
 
 
 @pytest.mark.gpu
@@ -193,10 +227,25 @@ def _tracker_like_init(h, w, rng, shift=(1, 2), jitter=2):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lanes,sort", [(None, None), (16, 0), (1, 0x33), (2, 0x42)])
 @pytest.mark.parametrize("h,w", [(384, 512), (320, 512)])
-def test_hip_refine_full_size_tracker_init_vs_oracle(h, w):
+def test_hip_refine_full_size_tracker_init_vs_oracle(h, w, lanes, sort):
     """refine_matches at the C2 / C4 frame sizes the tracker runs every
-    frame, from tracker-like starting pixels (f = 24, radius 3, dilation 5)."""
+    frame, from tracker-like starting pixels (f = 24, radius 3, dilation 5):
+    the default kernel and order (None), and other lanes / window-centre
+    tile orders."""
+    from splatt3r_amd import _lib
+    if lanes is not None:
+        _lib.lib().s3m_refine_set_lanes(lanes)
+        _lib.lib().s3m_refine_set_sort(sort)
+    try:
+        _refine_full_size(h, w)
+    finally:
+        _lib.lib().s3m_refine_set_lanes(-1)
+        _lib.lib().s3m_refine_set_sort(-1)
+
+
+def _refine_full_size(h, w):
     import mast3r_slam_backends as be
     rng = np.random.default_rng(h + w)
     D11 = unit_desc(1, h, w, 24, rng)
