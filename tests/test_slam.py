@@ -559,3 +559,83 @@ def test_sync_free_render_matches_two_call_render():
     # delivery lagging behind the loop (no read between frames): same last image
     _, r2, s2 = run(True, per_frame=False)
     assert torch.equal(r2[-1], r0[-1]) and s2["rendered"] == n
+
+
+def test_readback_copy_waits_on_the_render_event_on_the_aux_stream(monkeypatch):
+    """VERDICT r04 item 3 (the 6 ms host stall): the render read-back's
+    device-to-host copy, issued at the next step's start on the main stream
+    behind the queued decode-ahead replay, held the host until the stream
+    reached it (profiles/r05h_stall_trace.log).  _deliver_image issues it on
+    the aux stream, ordered after the render's own event only (never a
+    wait_stream on the main stream), and the ring slot's event is recorded
+    on that stream.  CPU stand-ins for the streams and events."""
+    from splatt3r_amd.slam import Frontend
+    log = []
+
+    class _Stream:
+        def __init__(self, name):
+            self.name = name
+
+        def wait_event(self, ev):
+            log.append((self.name, "wait_event", ev.tag))
+
+        def wait_stream(self, other):
+            log.append((self.name, "wait_stream", other.name))
+
+    class _Event:
+        n = 0
+
+        def __init__(self, *a, **k):
+            _Event.n += 1
+            self.tag = f"ev{_Event.n}"
+
+        def record(self, st=None):
+            log.append(((st or cur[-1]).name, "record", self.tag))
+
+        def synchronize(self):
+            pass
+
+    main, aux = _Stream("main"), _Stream("aux")
+    cur = [main]
+
+    class _Ctx:
+        def __init__(self, st):
+            self.st = st
+
+        def __enter__(self):
+            cur.append(self.st)
+
+        def __exit__(self, *a):
+            cur.pop()
+
+    monkeypatch.setattr(torch.cuda, "stream", _Ctx)
+    monkeypatch.setattr(torch.cuda, "Event", _Event)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda device=None: cur[-1])
+    monkeypatch.setattr(torch.Tensor, "record_stream",
+                        lambda self, st: log.append((st.name, "record_stream", None)))
+    real_copy = torch.Tensor.copy_
+
+    def copy(self, src, non_blocking=False):
+        log.append((cur[-1].name, "copy", non_blocking))
+        return real_copy(self, src)
+
+    monkeypatch.setattr(torch.Tensor, "copy_", copy)
+    fe = Frontend.__new__(Frontend)
+    fe.render_writer, fe.readback, fe.device = None, True, torch.device("cpu")
+    fe.aux_stream, fe._RB_RING, fe._rb_i = aux, 2, 0
+    fe._rb_bufs = [torch.empty(6, 8, 3) for _ in range(2)]
+    fe._rb_events = [None, None]
+    img = torch.rand(1, 1, 3, 6, 8) * 2
+    ready = _Event()
+    fe._deliver_image(img, 0, "gs", ready)
+    assert ("aux", "wait_event", ready.tag) in log
+    assert not any(op == "wait_stream" for _, op, _ in log)
+    assert [s for s, op, _ in log if op == "copy"] == ["aux"]
+    assert ("aux", "copy", True) in log
+    rec = [e for e in log if e[1] == "record"]
+    assert rec and rec[-1][0] == "aux" and fe._rb_events[0].tag == rec[-1][2]
+    torch.testing.assert_close(fe._last_render, img[0, 0].clamp(0, 1).permute(1, 2, 0))
+    # without a render event: one is recorded on the current (main) stream
+    log.clear()
+    fe._deliver_image(img, 1, "gs")
+    assert log[0][:2] == ("main", "record") and log[1] == ("aux", "wait_event", log[0][2])
