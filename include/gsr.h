@@ -111,9 +111,16 @@ int gsr_mark_visible(int64_t P, const float* means3D, const float* viewmatrix,
 /* Instrumentation for bench.py: per-phase device time (ms) of the last
  * gsr_preprocess + gsr_render on the calling thread, measured with HIP
  * events on the caller's stream when enabled.  phases[0..4] =
- * preprocess, scan, duplicate+sort, ranges, blend. */
+ * preprocess, (reduce, fused: ~0), depth sort (per-tile binning: tile
+ * counts + scan), binning (per-tile: fill + per-tile sort), blend. */
 void gsr_set_timing(int enabled);
 int gsr_last_timing(float* phases_ms, int n);
+
+/* Forward binning (A/B hook, not on the product path): 0 = global depth
+ * sort + tile sort (the default), 1 = per-tile binning (instances binned by
+ * tile in Gaussian order, each tile's list depth-sorted in LDS; slower at
+ * C3).  Identical output; any other value restores the default. */
+void gsr_set_binning(int mode);
 
 #ifdef __cplusplus
 }

@@ -145,12 +145,14 @@ struct ImageState {
   uint2* ranges;       // [tiles]
   uint32_t* n_contrib; // [H*W]
   float* final_T;      // [H*W]
+  uint32_t* cursor;    // [tiles] per-tile binning: counts -> fill cursors
 };
 ImageState carve_image(void* base, int H, int W, size_t* total = nullptr) {
   Carver c{static_cast<char*>(base)};
   int tiles = ((W + BX - 1) / BX) * ((H + BY - 1) / BY);
   ImageState s;
   s.ranges = c.take<uint2>(tiles);
+  s.cursor = c.take<uint32_t>(tiles);
   s.n_contrib = c.take<uint32_t>((size_t)H * W);
   s.final_T = c.take<float>((size_t)H * W);
   if (total) *total = c.off;
@@ -491,7 +493,6 @@ k_rs_hist(int64_t n, const K* __restrict__ keys, Digit dg_in, int64_t nseg,
   const int bins = 1 << dg.bits;
   for (int d = threadIdx.x; d < bins; d += kSortThreads) cnt[d] = 0u;
   __syncthreads();
-  const int lane = threadIdx.x & 63;
   const int64_t s = blockIdx.x;
   const int64_t i0 = s * kSegItems;
   uint32_t key[kSortPerLane];
@@ -502,11 +503,9 @@ k_rs_hist(int64_t n, const K* __restrict__ keys, Digit dg_in, int64_t nseg,
   }
 #pragma unroll
   for (int j = 0; j < kSortPerLane; ++j) {
-    const bool ok = i0 + j * kSortThreads + threadIdx.x < n;
-    const uint32_t d = dg(key[j]);
-    // one LDS atomic per distinct digit of the window
-    const uint64_t peers = match_peers(d, ok, dg.bits);
-    if (ok && (peers & lanemask_lt(lane)) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(peers));
+    // counts do not depend on the order: one LDS atomic per item (a ballot
+    // match per window costs a VALU op per digit bit)
+    if (i0 + j * kSortThreads + threadIdx.x < n) atomicAdd(&cnt[dg(key[j])], 1u);
   }
   __syncthreads();
   for (int d = threadIdx.x; d < bins; d += kSortThreads) hist[(size_t)d * nseg + s] = cnt[d];
@@ -547,12 +546,8 @@ k_rs_scatter(int64_t n, const K* __restrict__ kin, const V* __restrict__ vin,
     val[j] = i < n ? (vin ? vin[i] : (V)i) : V(0);
   }
 #pragma unroll
-  for (int j = 0; j < kSortPerLane; ++j) {
-    const bool ok = base_w + j * 64 + lane < n;
-    const uint32_t d = dg(key[j]);
-    const uint64_t peers = match_peers(d, ok, dg.bits);
-    if (ok && (peers & lanemask_lt(lane)) == 0) atomicAdd(&cnt[w][d], (uint32_t)__popcll(peers));
-  }
+  for (int j = 0; j < kSortPerLane; ++j)   // counts: order-free, one LDS atomic per item
+    if (base_w + j * 64 + lane < n) atomicAdd(&cnt[w][dg(key[j])], 1u);
   __syncthreads();
   // phase B: local slots (digit-major within the segment) and the global
   // offset of each digit's run; bins <= 2 * kSortThreads
@@ -841,6 +836,459 @@ k_red_finalize(const Reduce* __restrict__ red, uint32_t cap, int key_bits,
   info[0] = status;
   info[1] = (int64_t)total;
   info[2] = bits;
+}
+
+// -------------------------------------------------- per-tile binning ----
+//
+// An alternative binning, selected by
+// gsr_set_binning(1); measured slower than the global sorts and therefore not
+// the default (C3 forward 1.22 vs 0.86 ms, profiles/r05l_*): sorting the R
+// instances by depth inside their tiles ranks 3.8x more items per depth pass
+// than sorting the P Gaussians once (R = 15.8M, P = 4.19M), the ballot rank
+// costs a VALU op per digit bit per item, and the fill's scattered 4-B
+// writes land in partial lines.  Instead of sorting all P Gaussians by depth
+// and then all R instances by tile (3 + 2 global LSD passes and a gather of
+// the duplication records into depth order), the instances are binned by
+// tile straight from the Gaussians in index order and every tile sorts its
+// own list in LDS:
+//
+//   k_tile_count  per-tile instance counts (a workgroup of 1,024 Gaussians
+//                 counts into an LDS histogram, then one global atomic per
+//                 touched tile: Splatt3R's Gaussians come in pixel order, so a
+//                 workgroup touches few tiles)
+//   k_tile_scan   tile offsets -> ranges and fill cursors (one workgroup)
+//   k_tile_fill   (depth key, index) per instance into its tile's range: LDS
+//                 counts, one global cursor reservation per (workgroup, tile),
+//                 LDS ranks (arrival order inside the tile)
+//   k_tile_sort   one workgroup per tile: a stable LSD radix sort of the
+//                 tile's list by depth key in LDS (<= 16,384 instances; larger
+//                 tiles run the same passes chunk by chunk through the binning
+//                 buffers), 8-bit digits ranked exactly as k_rs_scatter does.
+//                 The fill order is arbitrary, so runs of equal depth keys
+//                 are put in index order (in place for runs of <= 32, else by
+//                 index passes + depth passes): the order is always (depth
+//                 key, Gaussian index), the reference's (tile, depth, index)
+//                 order of duplicateWithKeys + SortPairs.
+//
+// The sorted list lands in the buffer tile_sort_buffer() names, so the
+// backward (and the two-call render) read it as before.
+constexpr int kBinThreads = 256, kBinPer = 4;     // Gaussians per thread
+constexpr int kTileLdsMax = 8192;                 // tiles counted in LDS (fill: 64 KiB)
+constexpr int kTSThreads = 1024, kTSWaves = kTSThreads / 64, kTSIpt = 16;
+constexpr int kTSCap = kTSThreads * kTSIpt;        // instances sorted in LDS
+
+// the kept tiles of one duplication record, in k_duplicate's order
+template <typename F>
+__device__ __forceinline__ void for_each_tile(const uint4 d, int gx, F&& f) {
+  const int rw = (int)(d.y & 0xFFFFu), rh = (int)(d.y >> 16);
+  if (rw * rh == 0) return;                       // culled
+  const int x0 = (int)(d.x & 0xFFFFu), y0 = (int)(d.x >> 16);
+  if (rw * rh <= 64) {
+    uint64_t m = (uint64_t)d.z | ((uint64_t)d.w << 32);
+    while (m) {
+      const int pos = __builtin_ctzll(m);
+      m &= m - 1;
+      f((y0 + pos / rw) * gx + x0 + pos % rw);
+    }
+  } else {
+    for (int j = 0; j < rw * rh; ++j) f((y0 + j / rw) * gx + x0 + j % rw);
+  }
+}
+
+// A workgroup bins `per_wg` consecutive Gaussians (a multiple of
+// kBinThreads * kBinPer, in batches of kBinPer per thread): with the C3
+// microbench's uniformly scattered Gaussians every workgroup touches every
+// tile, so the global atomics per launch are (workgroups x tiles) and the
+// workgroups are made few and large.
+__global__ void __launch_bounds__(kBinThreads)
+k_tile_count(int64_t P, int64_t per_wg, int gx, int ntiles, const uint4* __restrict__ dup,
+             uint32_t* __restrict__ counts) {
+  extern __shared__ uint32_t s_hist[];
+  for (int t = threadIdx.x; t < ntiles; t += kBinThreads) s_hist[t] = 0u;
+  __syncthreads();
+  const int64_t g0 = (int64_t)blockIdx.x * per_wg, g1 = min(P, g0 + per_wg);
+  for (int64_t b0 = g0; b0 < g1; b0 += kBinThreads * kBinPer) {
+    uint4 d[kBinPer];
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+      const int64_t i = b0 + k * kBinThreads + threadIdx.x;
+      d[k] = i < g1 ? dup[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k)
+      for_each_tile(d[k], gx, [&](int t) { atomicAdd(&s_hist[t], 1u); });
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < ntiles; t += kBinThreads)
+    if (s_hist[t]) atomicAdd(&counts[t], s_hist[t]);
+}
+
+// counts -> offsets in place (the fill cursors) and ranges clipped to the
+// binning capacity
+__global__ void __launch_bounds__(1024)
+k_tile_scan(int ntiles, uint32_t* __restrict__ cursor, uint2* __restrict__ ranges, uint32_t cap) {
+  __shared__ uint32_t s_w[16];
+  uint32_t carry = 0;
+  for (int c0 = 0; c0 < ntiles; c0 += 1024) {
+    const int c = c0 + threadIdx.x;
+    const uint32_t v = c < ntiles ? cursor[c] : 0u;
+    uint32_t total = 0;
+    const uint32_t ex = block_excl_scan<1024>(v, s_w, &total);
+    if (c < ntiles) {
+      const uint32_t off = carry + ex;
+      cursor[c] = off;
+      ranges[c] = make_uint2(min(off, cap), (uint32_t)min((uint64_t)off + v, (uint64_t)cap));
+    }
+    carry += total;
+  }
+}
+
+__global__ void __launch_bounds__(kBinThreads)
+k_tile_fill(int64_t P, int64_t per_wg, int gx, int ntiles, const uint4* __restrict__ dup,
+            const uint32_t* __restrict__ dkey, uint32_t* __restrict__ cursor,
+            uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint32_t cap) {
+  extern __shared__ uint32_t s_mem[];
+  uint32_t* s_cnt = s_mem;
+  uint32_t* s_base = s_mem + ntiles;
+  for (int t = threadIdx.x; t < ntiles; t += kBinThreads) s_cnt[t] = 0u;
+  __syncthreads();
+  const int64_t g0 = (int64_t)blockIdx.x * per_wg, g1 = min(P, g0 + per_wg);
+  for (int64_t b0 = g0; b0 < g1; b0 += kBinThreads * kBinPer) {
+    uint4 d[kBinPer];
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+      const int64_t i = b0 + k * kBinThreads + threadIdx.x;
+      d[k] = i < g1 ? dup[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k)
+      for_each_tile(d[k], gx, [&](int t) { atomicAdd(&s_cnt[t], 1u); });
+  }
+  __syncthreads();
+  // one cursor reservation per touched tile
+  for (int t = threadIdx.x; t < ntiles; t += kBinThreads) {
+    const uint32_t c = s_cnt[t];
+    if (c) {
+      s_base[t] = atomicAdd(&cursor[t], c);
+      s_cnt[t] = 0u;
+    }
+  }
+  __syncthreads();
+  for (int64_t b0 = g0; b0 < g1; b0 += kBinThreads * kBinPer) {
+    uint4 d[kBinPer];
+    uint32_t key[kBinPer];
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+      const int64_t i = b0 + k * kBinThreads + threadIdx.x;
+      d[k] = i < g1 ? dup[i] : make_uint4(0u, 0u, 0u, 0u);
+      key[k] = i < g1 ? dkey[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+      const uint32_t i = (uint32_t)(b0 + k * kBinThreads + threadIdx.x);
+      for_each_tile(d[k], gx, [&](int t) {
+        const uint32_t pos = s_base[t] + atomicAdd(&s_cnt[t], 1u);
+        if (pos < cap) {
+          kout[pos] = key[k];
+          vout[pos] = i;
+        }
+      });
+    }
+  }
+}
+
+// One radix pass of k_tile_sort: digits of the depth key (Digit) or of the
+// Gaussian index (shift / bits)
+struct TsPass {
+  bool index;
+  int shift, bits;
+};
+
+__device__ __forceinline__ uint32_t ts_digit(const TsPass& ps, const Digit& dg, uint32_t key,
+                                             uint32_t val) {
+  if (ps.index) return (val >> ps.shift) & ((1u << ps.bits) - 1u);
+  Digit d = dg;
+  d.shift = ps.shift;
+  d.bits = ps.bits;
+  return d(key);
+}
+
+struct TsLds {
+  uint32_t k[kTSCap];
+  uint32_t v[kTSCap];
+  uint32_t cnt[kTSWaves][256];  // per (wave, digit) counts -> first slots
+  uint32_t run[256];            // chunked passes: next slot per digit
+  uint32_t w[kTSWaves];
+};
+
+// per-(wave, digit) counts of one chunk's items (added to t.cnt)
+__device__ __forceinline__ void ts_count(TsLds& t, const TsPass& ps, const Digit& dg,
+                                         const uint32_t (&key)[kTSIpt],
+                                         const uint32_t (&val)[kTSIpt], int ipt, int m,
+                                         int base_w) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < kTSIpt; ++j)   // order-free: one LDS atomic per item
+    if (j < ipt && base_w + j * 64 + lane < m) atomicAdd(&t.cnt[w][ts_digit(ps, dg, key[j], val[j])], 1u);
+}
+
+// slots of one chunk's items in item order (t.cnt holds each (wave, digit)'s
+// first slot and is advanced); put(j, slot) stores item j
+template <typename Put>
+__device__ __forceinline__ void ts_rank(TsLds& t, const TsPass& ps, const Digit& dg,
+                                        const uint32_t (&key)[kTSIpt],
+                                        const uint32_t (&val)[kTSIpt], int ipt, int m,
+                                        int base_w, Put&& put) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < kTSIpt; ++j) {
+    if (j < ipt) {
+      const bool ok = base_w + j * 64 + lane < m;
+      const uint32_t d = ts_digit(ps, dg, key[j], val[j]);
+      const uint64_t peers = match_peers(d, ok, ps.bits);
+      if (ok) {
+        const uint32_t b = t.cnt[w][d];
+        put(j, b + (uint32_t)__popcll(peers & lanemask_lt(lane)));
+        if ((peers >> lane) == 1ull) t.cnt[w][d] = b + (uint32_t)__popcll(peers);
+      }
+      wave_lds_sync();
+    }
+  }
+}
+
+__device__ __forceinline__ void ts_zero_cnt(TsLds& t) {
+  for (int k = threadIdx.x; k < kTSWaves * 256; k += kTSThreads) (&t.cnt[0][0])[k] = 0u;
+}
+
+// digit-major first slots from the per-wave counts, starting at run[] (or
+// at the exclusive scan of the digit totals when `scan`)
+__device__ __forceinline__ void ts_offsets(TsLds& t, bool scan) {
+  const int d = threadIdx.x;
+  uint32_t tot = 0;
+  if (d < 256) {
+#pragma unroll
+    for (int k = 0; k < kTSWaves; ++k) tot += t.cnt[k][d];
+  }
+  uint32_t b = 0;
+  if (scan) b = block_excl_scan<kTSThreads>(d < 256 ? tot : 0u, t.w);
+  if (d < 256) {
+    if (!scan) b = t.run[d];
+#pragma unroll
+    for (int k = 0; k < kTSWaves; ++k) {
+      const uint32_t c = t.cnt[k][d];
+      t.cnt[k][d] = b;
+      b += c;
+    }
+    t.run[d] = b;
+  }
+}
+
+__global__ void __launch_bounds__(kTSThreads)
+k_tile_sort(int ntiles, const uint2* __restrict__ ranges, uint32_t* __restrict__ kA,
+            uint32_t* __restrict__ vA, uint32_t* __restrict__ kB, uint32_t* __restrict__ vB,
+            Digit dg_in, int dbits, int ibits) {
+  __shared__ TsLds t;
+  const Digit dg = dg_in.live();
+  const int tile = xcd_tile(blockIdx.x, ntiles);
+  const uint2 r = ranges[tile];
+  const int n = (int)(r.y - r.x);
+  const int64_t lo = r.x;
+  if (n <= 1) {
+    if (n == 1 && threadIdx.x == 0) vB[lo] = vA[lo];
+    return;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // pass plan: depth digits; on a tie, index digits then depth digits again
+  auto plan = [](int bits, int p, int& shift, int& width) {
+    const int passes = max(1, (bits + 7) / 8);
+    width = (bits + passes - 1) / passes;
+    shift = p * width;
+    return passes;
+  };
+  const int dpass = max(1, (dbits + 7) / 8), ipass = max(1, (ibits + 7) / 8);
+  auto pass_of = [&](int q, bool tie) -> TsPass {
+    int shift, width;
+    if (!tie || q >= ipass + dpass) {
+      const int p = tie ? q - ipass - dpass : q;
+      plan(dbits, p, shift, width);
+      return {false, shift, min(dbits, shift + width) - shift};
+    }
+    if (q < dpass) {                      // (the first depth passes: redone)
+      plan(dbits, q, shift, width);
+      return {false, shift, min(dbits, shift + width) - shift};
+    }
+    plan(ibits, q - dpass, shift, width);
+    return {true, shift, min(ibits, shift + width) - shift};
+  };
+
+  if (n <= kTSCap) {
+    // ---- LDS-resident: items in registers, each pass ranks and stages
+    const int ipt = (n + kTSThreads - 1) / kTSThreads;
+    const int base_w = w * 64 * ipt;
+    uint32_t key[kTSIpt], val[kTSIpt];
+#pragma unroll
+    for (int j = 0; j < kTSIpt; ++j) {
+      const int s = base_w + j * 64 + lane;
+      const bool ok = j < ipt && s < n;
+      key[j] = ok ? kA[lo + s] : 0u;
+      val[j] = ok ? vA[lo + s] : 0u;
+    }
+    bool tie = false;
+    int total = dpass;
+    for (int q = 0; q < total; ++q) {
+      const TsPass ps = pass_of(q, tie);
+      ts_zero_cnt(t);
+      __syncthreads();
+      ts_count(t, ps, dg, key, val, ipt, n, base_w);
+      __syncthreads();
+      ts_offsets(t, true);
+      __syncthreads();
+      ts_rank(t, ps, dg, key, val, ipt, n, base_w, [&](int j, uint32_t sl) {
+        t.k[sl] = key[j];
+        t.v[sl] = val[j];
+      });
+      __syncthreads();
+      bool eq = false;
+#pragma unroll
+      for (int j = 0; j < kTSIpt; ++j) {
+        const int s = base_w + j * 64 + lane;
+        if (j < ipt && s < n) {
+          key[j] = t.k[s];
+          val[j] = t.v[s];
+          eq |= q == total - 1 && !tie && s + 1 < n && t.k[s + 1] == key[j];
+        }
+      }
+      // equal depth keys after the depth passes keep their (arbitrary) fill
+      // order: a run of <= 32 equal keys is put in index order in place by
+      // the thread holding its first item; a longer run sends the tile
+      // through the index passes and the depth passes again
+      if (q == total - 1 && !tie && __syncthreads_or(eq)) {
+        bool longrun = false;
+#pragma unroll 1
+        for (int j = 0; j < ipt; ++j) {
+          const int s = base_w + j * 64 + lane;
+          const uint32_t kj = s < n ? t.k[s] : 0u;
+          if (s + 1 < n && t.k[s + 1] == kj && (s == 0 || t.k[s - 1] != kj)) {
+            int L = 2;
+            while (L <= 32 && s + L < n && t.k[s + L] == kj) ++L;
+            if (L > 32) {
+              longrun = true;
+            } else {
+              for (int a = s + 1; a < s + L; ++a) {
+                const uint32_t x = t.v[a];
+                int b = a - 1;
+                while (b >= s && t.v[b] > x) {
+                  t.v[b + 1] = t.v[b];
+                  --b;
+                }
+                t.v[b + 1] = x;
+              }
+            }
+          }
+        }
+        if (__syncthreads_or(longrun)) {
+          tie = true;
+          total = dpass + ipass + dpass;
+        } else {
+#pragma unroll
+          for (int j = 0; j < kTSIpt; ++j) {
+            const int s = base_w + j * 64 + lane;
+            if (j < ipt && s < n) val[j] = t.v[s];
+          }
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < kTSIpt; ++j) {
+      const int s = base_w + j * 64 + lane;
+      if (j < ipt && s < n) vB[lo + s] = val[j];
+    }
+    return;
+  }
+
+  // ---- larger tiles: the same passes chunk by chunk, ping-pong between
+  // (kA, vA) and (kB, vB) over the tile's range
+  uint32_t* ks = kA + lo;
+  uint32_t* vs = vA + lo;
+  uint32_t* kd = kB + lo;
+  uint32_t* vd = vB + lo;
+  bool tie = false;
+  int total = dpass;
+  for (int q = 0; q < total; ++q) {
+    const TsPass ps = pass_of(q, tie);
+    // sweep 1: digit totals -> first slot of every digit
+    ts_zero_cnt(t);
+    __syncthreads();
+    for (int c0 = 0; c0 < n; c0 += kTSCap) {
+      const int m = min(kTSCap, n - c0);
+      const int ipt = (m + kTSThreads - 1) / kTSThreads, base_w = w * 64 * ipt;
+      uint32_t key[kTSIpt], val[kTSIpt];
+#pragma unroll
+      for (int j = 0; j < kTSIpt; ++j) {
+        const int s = base_w + j * 64 + lane;
+        const bool ok = j < ipt && s < m;
+        key[j] = ok ? ks[c0 + s] : 0u;
+        val[j] = ok ? vs[c0 + s] : 0u;
+      }
+      ts_count(t, ps, dg, key, val, ipt, m, base_w);
+    }
+    __syncthreads();
+    {
+      const int d = threadIdx.x;
+      uint32_t tot = 0;
+      if (d < 256) {
+#pragma unroll
+        for (int k = 0; k < kTSWaves; ++k) tot += t.cnt[k][d];
+      }
+      const uint32_t b = block_excl_scan<kTSThreads>(d < 256 ? tot : 0u, t.w);
+      if (d < 256) t.run[d] = b;
+    }
+    __syncthreads();
+    // sweep 2: every chunk in order, slots continuing from run[]
+    for (int c0 = 0; c0 < n; c0 += kTSCap) {
+      const int m = min(kTSCap, n - c0);
+      const int ipt = (m + kTSThreads - 1) / kTSThreads, base_w = w * 64 * ipt;
+      uint32_t key[kTSIpt], val[kTSIpt];
+#pragma unroll
+      for (int j = 0; j < kTSIpt; ++j) {
+        const int s = base_w + j * 64 + lane;
+        const bool ok = j < ipt && s < m;
+        key[j] = ok ? ks[c0 + s] : 0u;
+        val[j] = ok ? vs[c0 + s] : 0u;
+      }
+      ts_zero_cnt(t);
+      __syncthreads();
+      ts_count(t, ps, dg, key, val, ipt, m, base_w);
+      __syncthreads();
+      ts_offsets(t, false);
+      __syncthreads();
+      ts_rank(t, ps, dg, key, val, ipt, m, base_w, [&](int j, uint32_t sl) {
+        kd[sl] = key[j];
+        vd[sl] = val[j];
+      });
+      __syncthreads();
+    }
+    __threadfence_block();
+    __syncthreads();
+    uint32_t* tk = ks;
+    ks = kd;
+    kd = tk;
+    uint32_t* tv = vs;
+    vs = vd;
+    vd = tv;
+    if (q == total - 1 && !tie) {
+      bool eq = false;
+      for (int s = threadIdx.x; s + 1 < n; s += kTSThreads) eq |= ks[s] == ks[s + 1];
+      if (__syncthreads_or(eq)) {
+        tie = true;
+        total = dpass + ipass + dpass;
+      }
+    }
+  }
+  // the sorted values are in vs; the output range is vB's
+  if (vs != vB + lo)
+    for (int s = threadIdx.x; s < n; s += kTSThreads) vB[lo + s] = vs[s];
 }
 
 // --------------------------------------------------------------- blend ----
@@ -1288,6 +1736,10 @@ struct Timing {
 };
 thread_local Timing g_timing;
 
+// forward binning: 1 = per-tile binning + LDS depth sort, 0 = the global
+// depth sort + tile sort (the default; gsr_set_binning, A/B hook)
+int g_binning = 0;
+
 // depth-key range of the last gsr_preprocess on this thread (read back with
 // num_rendered), keyed by its geometry buffer
 struct KeyRange {
@@ -1333,6 +1785,8 @@ size_t gsr_image_bytes(int height, int width) { return image_bytes(height, width
 size_t gsr_binning_bytes(int64_t R) { return binning_bytes(R > 0 ? R : 1); }
 
 void gsr_set_timing(int enabled) { g_timing.enabled = enabled != 0; }
+
+void gsr_set_binning(int mode) { g_binning = mode == 1 ? 1 : 0; }
 
 int gsr_last_timing(float* phases_ms, int n) {
   if (!g_timing.valid) return S3_ERR_INVALID;
@@ -1413,11 +1867,32 @@ int render_impl(const gsr_settings* s, int64_t P, int64_t R, void* geom, void* b
   BinningState b = carve_binning(binning, R);
   ImageState im = carve_image(image, H, W);
   tmark(3, st);
-  S3_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * ntiles, st));
   const uint32_t* point_list = b.vals[0];
   const uint32_t* dn = dyn ? dyn + 2 : nullptr;
   const uint32_t cap = dyn ? (uint32_t)R : 0xFFFFFFFFu;
-  if (R > 0) {
+  if (R > 0 && g_binning == 1 && ntiles <= kTileLdsMax) {
+    // per-tile binning + LDS depth sort (see "per-tile binning")
+    const int o = tile_sort_buffer(ntiles), f = o ^ 1;
+    S3_HIP(hipMemsetAsync(im.cursor, 0, sizeof(uint32_t) * ntiles, st));
+    // ~512 workgroups (few global atomics per tile), each a whole number of
+    // kBinThreads x kBinPer batches
+    const int64_t batch = kBinThreads * kBinPer;
+    const int64_t per_wg = batch * std::max<int64_t>(1, s3::cdiv(s3::cdiv(P, 512), batch));
+    const unsigned bb = (unsigned)s3::cdiv(P, per_wg);
+    k_tile_count<<<bb, kBinThreads, sizeof(uint32_t) * ntiles, st>>>(P, per_wg, gx, ntiles,
+                                                                      g.dup, im.cursor);
+    k_tile_scan<<<1, 1024, 0, st>>>(ntiles, im.cursor, im.ranges, cap);
+    tmark(4, st);
+    k_tile_fill<<<bb, kBinThreads, 2 * sizeof(uint32_t) * ntiles, st>>>(
+        P, per_wg, gx, ntiles, g.dup, g.dkey[0], im.cursor, b.keys[f], b.vals[f], cap);
+    const Digit dg{kmin, span, 0, 1, dyn};
+    k_tile_sort<<<ntiles, kTSThreads, 0, st>>>(ntiles, im.ranges, b.keys[f], b.vals[f], b.keys[o],
+                                               b.vals[o], dg, bits,
+                                               std::max(1, bit_length((uint64_t)(P - 1))));
+    S3_LAUNCH_CHECK();
+    point_list = b.vals[o];
+  } else if (R > 0) {
+    S3_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * ntiles, st));
     const int dsrc = radix_sort<uint32_t, uint32_t>(P, g.dkey, g.dval, kmin, span, bits, false,
                                                     g.dhist, g.dtot, st, true, dyn);
     const uint32_t* order = g.dval[dsrc];
@@ -1454,6 +1929,7 @@ int render_impl(const gsr_settings* s, int64_t P, int64_t R, void* geom, void* b
     point_list = b.vals[tsrc];
     S3_LAUNCH_CHECK();
   } else {
+    S3_HIP(hipMemsetAsync(im.ranges, 0, sizeof(uint2) * ntiles, st));
     tmark(4, st);
   }
   tmark(5, st);

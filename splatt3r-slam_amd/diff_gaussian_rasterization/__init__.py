@@ -63,6 +63,7 @@ _lib.register({
     "gsr_forward_deferred": (ctypes.c_int, [_SP, ctypes.c_int64, ctypes.c_int] + [P_] * 7 +
                              [P_, P_, P_, ctypes.c_int64, ctypes.c_int, P_, P_, P_, P_]),
     "gsr_set_timing": (None, [ctypes.c_int]),
+    "gsr_set_binning": (None, [ctypes.c_int]),
     "gsr_last_timing": (ctypes.c_int, [P_, ctypes.c_int]),
 })
 

@@ -213,18 +213,26 @@ def _restage(sc, z):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("binning", ["tile", "global"])
 @pytest.mark.parametrize("case", ["plane", "two_depths", "wide_range", "all_culled", "tail_4097",
                                   "tail_8193", "tiles_3600", "tiles_8160", "tiles_8832",
-                                  "big_splats", "ragged_1x1"])
-def test_hip_binning_edge_cases_bitexact_vs_oracle(case):
-    """The hand-written depth / tile sorts (raster.hip "sorting"): equal
-    depths (stability by index), a 1-2 pass key width, a 4-pass key width,
-    nothing visible (R = 0), segment tails (4096 and 8192 items), tile ids
-    of 12, 13 and 14 bits, splats whose rect exceeds the 64-tile mask (plain
-    rect enumeration), and a ragged 1-tile image -- bit-exact against the
-    oracle."""
+                                  "big_splats", "ragged_1x1", "one_tile_20k", "one_tile_20k_plane"])
+def test_hip_binning_edge_cases_bitexact_vs_oracle(case, binning):
+    """Both forward binnings (the global depth + tile sorts of raster.hip
+    "sorting", the default, and "per-tile binning"): equal depths (ties resolved
+    by Gaussian index: the per-tile sort's index passes), a 1-2 pass key
+    width, a 4-pass key width, nothing visible (R = 0), segment tails (4096
+    and 8192 items), tile ids of 12, 13 and 14 bits (8,832 tiles: past the
+    per-tile path's 8,192, so the global path runs), splats whose rect
+    exceeds the 64-tile mask (plain rect enumeration), a ragged 1-tile image,
+    and ~20k instances in one tile (past the 16,384 sorted in LDS: the
+    chunked passes), with distinct and with equal depths -- bit-exact against
+    the oracle."""
+    from splatt3r_amd import _lib
     rng = np.random.default_rng(7)
     P, H, W, fx = 3000, 48, 64, 60.0
+    if case.startswith("one_tile_20k"):
+        P, H, W, fx = 20000, 16, 16, 15.0
     if case == "tail_4097":
         P = 4097
     if case == "tail_8193":
@@ -254,7 +262,13 @@ def test_hip_binning_edge_cases_bitexact_vs_oracle(case):
         # in front of the 0.2 near-plane cull even after the settings'
         # scale-invariant rescale of the means
         sc = _restage(sc, np.full(P, 1e-5, np.float32))
-    rs, scale, img, radii, kw = _gpu_render(sc, "colors")
+    elif case == "one_tile_20k_plane":
+        sc = _restage(sc, np.full(P, 3.0, np.float32))
+    _lib.lib().gsr_set_binning(1 if binning == "tile" else 0)
+    try:
+        rs, scale, img, radii, kw = _gpu_render(sc, "colors")
+    finally:
+        _lib.lib().gsr_set_binning(-1)
     sd = settings_to_dict(rs)
     ref = oracle.raster(sd, sc["means"] * scale, sc["opacities"],
                         colors_precomp=np.clip(sc["shs"][:, 0, :] + 0.5, 0, 1),
@@ -263,6 +277,9 @@ def test_hip_binning_edge_cases_bitexact_vs_oracle(case):
     np.testing.assert_array_equal(img.detach().cpu().numpy(), ref["color"])
     if case == "all_culled":
         assert int(radii.max()) == 0
+    if case.startswith("one_tile_20k"):
+        import diff_gaussian_rasterization as dgr
+        assert dgr.last_num_rendered > 16384
 
 
 @pytest.mark.gpu

@@ -102,9 +102,15 @@ def main():
     ap.add_argument("--P", type=int, default=4_194_304)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--no-backward", action="store_true")
+    ap.add_argument("--binning", choices=["tile", "global"], default="tile",
+                    help="forward binning (gsr_set_binning)")
     a = ap.parse_args()
+    from splatt3r_amd import _lib
+    _lib.lib().gsr_set_binning(1 if a.binning == "tile" else 0)
     t0 = time.time()
-    print(json.dumps(run(a.P, a.iters, backward=not a.no_backward)))
+    out = run(a.P, a.iters, backward=not a.no_backward)
+    out["binning"] = a.binning
+    print(json.dumps(out))
     print(f"# wall {time.time() - t0:.1f}s")
 
 
