@@ -1079,7 +1079,8 @@ def main(argv=None):
         r = raster_run(4_194_304, iters=5, warmup=2, backward=True, device=dev)
         result["raster_c3"] = {k: r[k] for k in ("P", "fwd_ms", "msplats_per_s", "fwd_GBps",
                                                  "phases_ms", "bwd_ms", "bwd_GBps",
-                                                 "num_rendered", "visible")}
+                                                 "num_rendered", "visible", "fwd_deferred_ms",
+                                                 "deferred_equal")}
         result["raster_c3"]["hbm_frac"] = r["fwd_GBps"] / PEAK_HBM_GBPS
         # BASELINE config 3 is forward + backward
         result["raster_c3"]["fwd_bwd_ms"] = r["fwd_ms"] + r["bwd_ms"]

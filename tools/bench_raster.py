@@ -70,6 +70,26 @@ def run(P=4_194_304, iters=10, warmup=3, backward=True, device="cuda"):
         f_ms.append(ev[0].elapsed_time(ev[1]))
         phases.append(last_timing())
     set_timing(False)
+    # the sync-free forward (gsr_forward_deferred: no host read of the
+    # instance count between preprocess and binning; the SLAM frame loop's
+    # render path), sized from the two-call forward, image checked equal
+    cap = int(dgr.last_num_rendered) + 1024
+    col, _, info = dgr.rasterize_deferred(rs, leaf["means3D"].detach(), leaf["opacities"].detach(),
+                                          shs=leaf["shs"].detach(),
+                                          cov3D_precomp=leaf["cov3D_precomp"].detach(),
+                                          capacity=cap, key_bits=32)
+    kb = int(info[2])
+    d_ms = []
+    for _ in range(iters):
+        ev[0].record()
+        col, _, info = dgr.rasterize_deferred(rs, leaf["means3D"].detach(),
+                                              leaf["opacities"].detach(), shs=leaf["shs"].detach(),
+                                              cov3D_precomp=leaf["cov3D_precomp"].detach(),
+                                              capacity=cap, key_bits=kb)
+        ev[1].record()
+        torch.cuda.synchronize()
+        d_ms.append(ev[0].elapsed_time(ev[1]))
+    deferred_ok = int(info[0]) == 0 and bool(torch.equal(col, img.detach().reshape(col.shape)))
     b_ms = []
     if backward:
         for _ in range(iters):
@@ -90,7 +110,8 @@ def run(P=4_194_304, iters=10, warmup=3, backward=True, device="cuda"):
     out = dict(P=P, H=H, W=W, fwd_ms=fwd, msplats_per_s=P / (fwd * 1e-3) / 1e6,
                fwd_GBps=fwd_bytes(P, H, W) / (fwd * 1e-3) / 1e9,
                phases_ms=dict(zip(["preprocess", "reduce", "depth_sort", "binning", "blend"], ph)),
-               num_rendered=int(dgr.last_num_rendered), visible=int((radii > 0).sum()))
+               num_rendered=int(dgr.last_num_rendered), visible=int((radii > 0).sum()),
+               fwd_deferred_ms=float(np.median(d_ms)), deferred_equal=deferred_ok)
     if backward:
         bwd = float(np.median(b_ms))
         out.update(bwd_ms=bwd, bwd_GBps=bwd_bytes(P, H, W) / (bwd * 1e-3) / 1e9)
@@ -102,7 +123,7 @@ def main():
     ap.add_argument("--P", type=int, default=4_194_304)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--no-backward", action="store_true")
-    ap.add_argument("--binning", choices=["tile", "global"], default="tile",
+    ap.add_argument("--binning", choices=["tile", "global"], default="global",
                     help="forward binning (gsr_set_binning)")
     a = ap.parse_args()
     from splatt3r_amd import _lib
