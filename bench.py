@@ -882,7 +882,7 @@ def main(argv=None):
         # is not armed)
         import faulthandler
         lim = float(os.environ["S3_STALL_TRACE"]) * 1e-3
-        prev = fe.tracker.mark if phases is not None else None
+        prev = getattr(fe.tracker, "mark", None)
 
         def _mark(name, prev=prev):
             if prev is not None:
@@ -893,6 +893,28 @@ def main(argv=None):
             elif name == "spec_queued":
                 faulthandler.cancel_dump_traceback_later()
         fe.tracker.mark = _mark
+    hev = None
+    if os.environ.get("S3_HOST_EVENTS"):
+        # diagnostic: every host phase mark also records a timing event on an
+        # idle stream (it completes when the host records it: host time on
+        # the device clock), and the tracker marks the device time its first
+        # GN chunk ends (gpu_mark on the main stream)
+        hev, idle = [], torch.cuda.Stream(dev)
+        prev_h = getattr(fe.tracker, "mark", None)
+
+        def _hmark(name, prev=prev_h):
+            if prev is not None:
+                prev(name)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(idle)
+            hev.append((len(host_ms), "host:" + name, e))
+
+        def _gmark(name):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(dev))
+            hev.append((len(host_ms), "gpu:" + name, e))
+        fe.tracker.mark = _hmark
+        fe.tracker.gpu_mark = _gmark
     ms0 = torch.cuda.memory_stats(dev)
     for i in range(a.warmup + 1, nfr):
         h0 = time.perf_counter()
@@ -918,8 +940,21 @@ def main(argv=None):
     if os.environ.get("S3_STALL_TRACE"):
         import faulthandler
         faulthandler.cancel_dump_traceback_later()
-    if phases is not None or os.environ.get("S3_STALL_TRACE"):
+    if phases is not None or os.environ.get("S3_STALL_TRACE") or hev is not None:
         fe.tracker.mark = None
+    if hev is not None:
+        fe.tracker.gpu_mark = None
+        if crit is not None and ev_t0 is not None:
+            # per step: [(mark, ms after the timed region's start on the device clock)]
+            steps = {}
+            for k, name, e in hev:
+                steps.setdefault(k, []).append((name, round(ev_t0.elapsed_time(e), 3)))
+            mains = [(i, e0, e1) for tag, i, e0, e1 in fe.spans if tag == "main"]
+            for n, (i, e0, e1) in enumerate(mains):
+                if n in steps:
+                    steps[n] += [("chain_start", round(ev_t0.elapsed_time(e0), 3)),
+                                 ("chain_end", round(ev_t0.elapsed_time(e1), 3))]
+            crit["host_device_marks"] = steps
     if phases is not None:
         if crit is not None:
             by = {}

@@ -29,6 +29,7 @@ encoded exactly once from its own image, with M = 768k-row GEMMs.
 from __future__ import annotations
 
 import contextlib
+import os
 import queue
 import threading
 import time
@@ -91,6 +92,11 @@ def lookahead_batches(i: int, next_enc: int, n_next: int, enc_batch: int, enc_ah
         next_enc += c
     return out
 
+
+
+# diagnostic only (timeline A/B): S3_DIAG_SKIP="world,render" leaves the
+# speculative world records / render out of the tracked frame
+_DIAG_SKIP = set(filter(None, os.environ.get("S3_DIAG_SKIP", "").split(",")))
 
 class _RenderTicket:
     """A render queued on the render worker: `keep(finish)` hands the image
@@ -456,16 +462,23 @@ class Frontend:
             saved = frame.T_WC
             frame.T_WC = T_WC
             try:
-                recs = self._world_records_aux(frame)
-                if not self.render:
+                # the render first: it is on the main stream, right behind
+                # the GN chunk; the aux stream's world records after it
+                if not self.render or "render" in _DIAG_SKIP:
                     img = None
                 elif self._rworker is not None:
                     img = self._render_task(frame, ref, T_WC)      # a ticket
                 else:
                     img = splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=T_WC,
                                           sizing=self.sizing)
+                recs = None if "world" in _DIAG_SKIP else self._world_records_aux(frame)
             finally:
                 frame.T_WC = saved
+            # earlier frames' finished renders are handed over here, while
+            # the host is about to wait for the GN chunk anyway, instead of
+            # at the next step's start, where the read-back issue delays the
+            # next frame's first launches
+            self._deliver(block=False)
             return recs, img
         return hook
 
@@ -586,7 +599,13 @@ class Frontend:
                 ready.record(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(st):
                 st.wait_event(ready)
-                host.copy_(img[0, 0].clamp(0, 1).permute(1, 2, 0), non_blocking=True)
+                # made contiguous on the device first: a device-to-host
+                # copy_ from a non-contiguous source goes through a
+                # synchronous .to(cpu) inside torch, which held the host until
+                # the stream drained (every frame on the aux stream, ~0.25 ms;
+                # on the main stream the 6 ms stall of profiles/r05h)
+                hwc = img[0, 0].clamp(0, 1).permute(1, 2, 0).contiguous()
+                host.copy_(hwc, non_blocking=True)
                 img.record_stream(st)
                 ev = torch.cuda.Event()
                 ev.record(st)

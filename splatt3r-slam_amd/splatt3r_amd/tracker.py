@@ -281,6 +281,9 @@ class FrameTracker:
         # runs the post-GN glue and issues the next launches
         gn_done = torch.cuda.Event()
         gn_done.record(torch.cuda.current_stream(ne.device))
+        gpu_mark = getattr(self, "gpu_mark", None)   # device-time marker (diagnostic)
+        if gpu_mark:
+            gpu_mark("gn_end")
         if mark:
             mark("gn_queued")
         if before_sync is not None:
