@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 5: stall watch after the read-back fixes: the host stall with the
+# S3_STALL_TRACE watchdog (Python stacks of every thread when an issue phase
+# of a step exceeds 3 ms) and the per-gap encoder alignment
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+
+OFF="--no-e2e --no-pairs --no-backend --no-map --no-c3 --no-cpu-baseline --no-live"
+: > gpurun_out/r05x_stall.log
+for n in 1 2 3 4 5 6 7 8; do
+  S3_STALL_TRACE=3 S3_HOST_PHASES=1 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 $OFF > gpurun_out/r05x_one.log 2> gpurun_out/r05x_err_$n.log || { tail -20 gpurun_out/r05x_err_$n.log; exit 1; }
+  grep '^{' gpurun_out/r05x_one.log | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); c=d['critical_path']
+h=c['host_step_ms']; k=max(range(len(h)), key=lambda i: h[i])
+print('run $n', round(d['value'],1), 'other', round(c['main_other_ms'],3), 'idle', round(c['main_idle_ms'],3), 'big_gaps', c['big_gaps'], 'worst step', k, h[k], 'phases', c['host_phases_ms'].get(str(k)))" | tee -a gpurun_out/r05x_stall.log
+  echo "run $n stack dumps: $(grep -c 'most recent call first' gpurun_out/r05x_err_$n.log || true)" | tee -a gpurun_out/r05x_stall.log
+done
