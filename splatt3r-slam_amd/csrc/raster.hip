@@ -774,6 +774,47 @@ k_ranges(int64_t R, const K* __restrict__ keys, uint2* __restrict__ ranges,
   if (i == R - 1) ranges[cur].y = (uint32_t)R;
 }
 
+// k_ranges for 16-bit tile keys, 8 keys per thread: one 16-B load per
+// thread (the previous key from the neighbouring lane), 8x fewer threads
+__global__ void __launch_bounds__(kThreads)
+k_ranges16(int64_t R, const uint16_t* __restrict__ keys, uint2* __restrict__ ranges,
+           const uint32_t* __restrict__ dn) {
+  R = live_n(R, dn);
+  const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  uint16_t k[8];
+  if (i0 + 8 <= R) {
+    const uint4 v = *reinterpret_cast<const uint4*>(keys + i0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      k[2 * e] = (uint16_t)(w[e] & 0xFFFFu);
+      k[2 * e + 1] = (uint16_t)(w[e] >> 16);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) k[e] = i0 + e < R ? keys[i0 + e] : (uint16_t)0;
+  }
+  // the key before i0: the neighbouring lane's last key, or a load at a
+  // wave's first lane
+  const int lane = threadIdx.x & 63;
+  uint32_t prev = (uint32_t)__shfl_up((int)k[7], 1, 64);
+  if (lane == 0 && i0 > 0 && i0 <= R) prev = keys[i0 - 1];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int64_t i = i0 + e;
+    if (i >= R) break;
+    const uint32_t cur = k[e];
+    const uint32_t pk = e == 0 ? prev : (uint32_t)k[e - 1];
+    if (i == 0) {
+      ranges[cur].x = 0;
+    } else if (cur != pk) {
+      ranges[pk].y = (uint32_t)i;
+      ranges[cur].x = (uint32_t)i;
+    }
+    if (i == R - 1) ranges[cur].y = (uint32_t)R;
+  }
+}
+
 // One stable LSD sort: passes over `bits` bits of (key - kmin), each of
 // <= kMaxDigitBits.  Returns the index (0/1) of the ping-pong buffers that
 // hold the result.
@@ -1300,6 +1341,12 @@ k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
   __shared__ float4 s_r0[BS];
   __shared__ float4 s_r1[BS];  // (conic.c, opacity, r, g)
   __shared__ float s_b[BS];
+  // per staged Gaussian: a power below which alpha < 1/255 for certain, so
+  // the exponential is skipped for the pixels it cannot reach (the same
+  // pairs the alpha test skips: alpha = op * fexp(power) <= op * e^power *
+  // (1 + 4 ulp) < e^-0.01 / 255 < 1/255 below this power; the image does
+  // not change, tests/test_raster.py bit-exact cases)
+  __shared__ float s_cut[BS];
   const int tile = xcd_tile(blockIdx.x, ntiles);
   const int tx = tile % gx, ty = tile / gx;
   const int lx = threadIdx.x % BX, ly = threadIdx.x / BX;
@@ -1322,6 +1369,7 @@ k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
       s_r0[threadIdx.x] = g.rec0[id];
       s_r1[threadIdx.x] = g.rec1[id];
       s_b[threadIdx.x] = g.blue[id];
+      s_cut[threadIdx.x] = -__logf(255.0f * s_r1[threadIdx.x].y) - 0.01f;
     }
     __syncthreads();
     const int n = todo < BS ? todo : BS;
@@ -1332,6 +1380,7 @@ k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
       if (power > 0.0f) continue;
+      if (power < s_cut[j]) continue;
       const float alpha = fminf(0.99f, b.y * fexp(power));
       if (alpha < 1.0f / 255.0f) continue;
       const float test_T = T * (1.0f - alpha);
@@ -1914,8 +1963,8 @@ int render_impl(const gsr_settings* s, int64_t P, int64_t R, void* geom, void* b
                                                              cap);
       tsrc = radix_sort<uint16_t, uint32_t>(R, k16, b.vals, 0u, 0xFFFFFFFFu, tbits, true, b.hist,
                                             b.tot, st, false, nullptr, dn);
-      k_ranges<uint16_t><<<(unsigned)s3::cdiv(R, kThreads), kThreads, 0, st>>>(R, k16[tsrc],
-                                                                             im.ranges, dn);
+      k_ranges16<<<(unsigned)s3::cdiv(s3::cdiv(R, 8), kThreads), kThreads, 0, st>>>(
+          R, k16[tsrc], im.ranges, dn);
     } else {
       k_duplicate<uint32_t><<<dup_blocks, kThreads, 0, st>>>(P, gx, order, g.dup_sorted,
                                                              g.cnt_seg, nwseg, b.keys[0], b.vals[0],
