@@ -1341,12 +1341,6 @@ k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
   __shared__ float4 s_r0[BS];
   __shared__ float4 s_r1[BS];  // (conic.c, opacity, r, g)
   __shared__ float s_b[BS];
-  // per staged Gaussian: a power below which alpha < 1/255 for certain, so
-  // the exponential is skipped for the pixels it cannot reach (the same
-  // pairs the alpha test skips: alpha = op * fexp(power) <= op * e^power *
-  // (1 + 4 ulp) < e^-0.01 / 255 < 1/255 below this power; the image does
-  // not change, tests/test_raster.py bit-exact cases)
-  __shared__ float s_cut[BS];
   const int tile = xcd_tile(blockIdx.x, ntiles);
   const int tx = tile % gx, ty = tile / gx;
   const int lx = threadIdx.x % BX, ly = threadIdx.x / BX;
@@ -1369,7 +1363,6 @@ k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
       s_r0[threadIdx.x] = g.rec0[id];
       s_r1[threadIdx.x] = g.rec1[id];
       s_b[threadIdx.x] = g.blue[id];
-      s_cut[threadIdx.x] = -__logf(255.0f * s_r1[threadIdx.x].y) - 0.01f;
     }
     __syncthreads();
     const int n = todo < BS ? todo : BS;
@@ -1380,7 +1373,6 @@ k_blend(int W, int H, int gx, int ntiles, const uint2* __restrict__ ranges,
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
       if (power > 0.0f) continue;
-      if (power < s_cut[j]) continue;
       const float alpha = fminf(0.99f, b.y * fexp(power));
       if (alpha < 1.0f / 255.0f) continue;
       const float test_T = T * (1.0f - alpha);
