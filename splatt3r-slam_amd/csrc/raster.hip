@@ -71,7 +71,7 @@ struct GeomState {
   float4* rec1;  // conic.c, opacity, rgb.r, rgb.g (the blend's staged record)
   float* blue;   // [P] rgb.b (r, g ride in rec1)
   float* cov3D;  // [P,6] (scale/rotation path)
-  uint8_t* clamped;  // [P,3]
+  uint8_t* clamped;  // [P]: bit ch = colour channel ch clamped at 0 (SH path)
   // duplication record per Gaussian: x = x0 | y0 << 16, y = rect w | h << 16,
   // z/w = kept-tile mask (bit (y - y0) * w + (x - x0)) for rects of 2..64
   // tiles; one 16-B gather serves the depth-ordered passes
@@ -95,7 +95,7 @@ GeomState carve_geom(void* base, int64_t P, size_t* total = nullptr) {
   g.rec1 = c.take<float4>(P);
   g.blue = c.take<float>(P);
   g.cov3D = c.take<float>(P * 6);
-  g.clamped = c.take<uint8_t>(P * 3);
+  g.clamped = c.take<uint8_t>(P);
   g.dup = c.take<uint4>(P);
   g.red = c.take<Reduce>(1);
   g.dkey[0] = c.take<uint32_t>(P);
@@ -242,20 +242,26 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
   if (colors_pre) {
     rgb[0] = colors_pre[i * 3 + 0]; rgb[1] = colors_pre[i * 3 + 1]; rgb[2] = colors_pre[i * 3 + 2];
   } else {
-    float dx = mx - campos[0], dy = my - campos[1], dz = mz - campos[2];
-    float len = sqrtf(dx * dx + dy * dy + dz * dz);
-    dx = dx / len; dy = dy / len; dz = dz / len;
     float B[16];
-    sh_basis(cam.D, dx, dy, dz, B);
+    if (cam.D == 0) {
+      B[0] = SH_C0;   // degree 0: the view direction does not enter
+    } else {
+      float dx = mx - campos[0], dy = my - campos[1], dz = mz - campos[2];
+      float len = sqrtf(dx * dx + dy * dy + dz * dz);
+      dx = dx / len; dy = dy / len; dz = dz / len;
+      sh_basis(cam.D, dx, dy, dz, B);
+    }
     const int nb = (cam.D + 1) * (cam.D + 1);
     const float* sh = shs + i * (int64_t)cam.M * 3;
+    uint32_t cl = 0;
     for (int ch = 0; ch < 3; ++ch) {
       float acc = B[0] * sh[ch];
       for (int k = 1; k < nb; ++k) acc = acc + B[k] * sh[k * 3 + ch];
       acc = acc + 0.5f;
-      g.clamped[i * 3 + ch] = acc < 0.0f;
+      cl |= (uint32_t)(acc < 0.0f) << ch;
       rgb[ch] = fmaxf(acc, 0.0f);
     }
+    g.clamped[i] = (uint8_t)cl;       // one byte store instead of three
   }
   g.blue[i] = rgb[2];
   radii[i] = r;
@@ -1701,7 +1707,7 @@ k_preprocess_backward(int64_t P, Cam cam, const float* __restrict__ means,
     float* dsh = dL_dsh + i * (int64_t)cam.M * 3;
     float drgb[3];
     for (int ch = 0; ch < 3; ++ch)
-      drgb[ch] = g.clamped[i * 3 + ch] ? 0.0f : dL_dcolor[i * 3 + ch];
+      drgb[ch] = ((g.clamped[i] >> ch) & 1u) ? 0.0f : dL_dcolor[i * 3 + ch];
     for (int k = 0; k < cam.M; ++k)
       for (int ch = 0; ch < 3; ++ch) dsh[k * 3 + ch] = k < nb ? B[k] * drgb[ch] : 0.0f;
     float ddx = 0.f, ddy = 0.f, ddz = 0.f;
