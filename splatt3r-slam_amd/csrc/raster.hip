@@ -70,7 +70,6 @@ struct GeomState {
   float4* rec0;  // x, y, conic.a, conic.b
   float4* rec1;  // conic.c, opacity, rgb.r, rgb.g (the blend's staged record)
   float* blue;   // [P] rgb.b (r, g ride in rec1)
-  float* cov3D;  // [P,6] (scale/rotation path)
   uint8_t* clamped;  // [P]: bit ch = colour channel ch clamped at 0 (SH path)
   // duplication record per Gaussian: x = x0 | y0 << 16, y = rect w | h << 16,
   // z/w = kept-tile mask (bit (y - y0) * w + (x - x0)) for rects of 2..64
@@ -94,7 +93,6 @@ GeomState carve_geom(void* base, int64_t P, size_t* total = nullptr) {
   g.rec0 = c.take<float4>(P);
   g.rec1 = c.take<float4>(P);
   g.blue = c.take<float>(P);
-  g.cov3D = c.take<float>(P * 6);
   g.clamped = c.take<uint8_t>(P);
   g.dup = c.take<uint4>(P);
   g.red = c.take<Reduce>(1);
@@ -220,9 +218,9 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
 #pragma unroll
     for (int k = 0; k < 6; ++k) cov3[k] = cov_pre[i * 6 + k];
   } else {
+    // not stored: the backward recomputes it from the same inputs (bit for
+    // bit), 24 B per Gaussian less written by every forward
     cov3d_from_scale_rot(scales + i * 3, cam.scale_mod, rots + i * 4, cov3);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) g.cov3D[i * 6 + k] = cov3[k];
   }
   Ewa e = ewa_project(mx, my, mz, cov3, vm, cam.fx, cam.fy, cam.tanfx, cam.tanfy);
   const float a = e.a + 0.3f, b = e.b, c = e.c + 0.3f;
@@ -267,21 +265,17 @@ preprocess_one(int64_t i, Cam cam, const float* __restrict__ means,
   radii[i] = r;
   g.rec0[i] = make_float4(px, py, c * det_inv, -b * det_inv);
   g.rec1[i] = make_float4(a * det_inv, opac[i], rgb[0], rgb[1]);
-  // tiles the blend can actually use (tile_hit); the reference lists every
-  // tile of the rect, whose extra entries are all skipped per pixel
-  // rects of <= 64 tiles: keep only the tiles the blend can use (tile_cull /
-  // tile_hit, raster_math.hpp) as a bit mask; larger rects keep every tile
+  // tiles the blend can actually use; the reference lists every tile of the
+  // rect, whose extra entries are all skipped per pixel.  Rects of <= 64
+  // tiles keep only the tiles the blend can use (tile_cull /
+  // tile_mask_rows, raster_math.hpp) as a bit mask; larger rects keep every tile
   const int rw = x1 - x0, area = rw * (y1 - y0);
   uint64_t mask = area == 1 ? 1ull : ~0ull;
   uint32_t n = (uint32_t)area;
   if (area > 1 && area <= 64) {
     const float cA = c * det_inv, cB = -b * det_inv, cC = a * det_inv;
     const TileCull tc = tile_cull(px, py, cA, cB, cC, opac[i], x0, y0, x1, y1);
-    mask = 0;
-    for (int y = tc.y0; y < tc.y1; ++y)
-      for (int x = tc.x0; x < tc.x1; ++x)
-        if (tile_hit(tc, px, py, cA, cB, cC, x, y, cam.W, cam.H))
-          mask |= 1ull << ((y - y0) * rw + (x - x0));
+    mask = tile_mask_rows(tc, px, py, cA, cB, cC, x0, y0, rw, y1 - y0, cam.H);
     n = (uint32_t)__popcll(mask);
   }
   g.dup[i] = make_uint4((uint32_t)x0 | ((uint32_t)y0 << 16),
@@ -1639,7 +1633,13 @@ k_preprocess_backward(int64_t P, Cam cam, const float* __restrict__ means,
     return;
   }
   const float mx = means[i * 3 + 0], my = means[i * 3 + 1], mz = means[i * 3 + 2];
-  const float* cov3 = cov_pre ? cov_pre + i * 6 : g.cov3D + i * 6;
+  float cov3[6];   // the forward's 3-D covariance, recomputed (not stored)
+  if (cov_pre) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) cov3[k] = cov_pre[i * 6 + k];
+  } else {
+    cov3d_from_scale_rot(scales + i * 3, cam.scale_mod, rots + i * 4, cov3);
+  }
   Ewa e = ewa_project(mx, my, mz, cov3, vm, cam.fx, cam.fy, cam.tanfx, cam.tanfy);
   const float a = e.a + 0.3f, b = e.b, c = e.c + 0.3f;
   const float dcx = dL_dconic[i * 4 + 0], dcy = dL_dconic[i * 4 + 1], dcz = dL_dconic[i * 4 + 3];

@@ -133,6 +133,50 @@ GSR_HD bool tile_hit(const TileCull& t, float mx, float my, float A, float B, fl
   return qmin * t.shrink <= t.thr;
 }
 
+// Kept-tile mask of a reference rect of <= 64 tiles (bit (ty - ry0) * rw +
+// (tx - rx0)), one tile row at a time instead of tile_hit per tile.  Over
+// a row's v band (v = my - y, y in the row's continuous pixel range) the
+// ellipse q <= T covers one u interval [umin, umax] (u = mx - x): the slice
+// at v spans u = (-B v -+ sqrt(A T - det v^2)) / A, the right end concave
+// and the left end convex in v, so their extremes over the band sit at the
+// tangent points v = -/+ B sqrt(T / (C det)) clamped into it.  A tile of
+// the row meets the ellipse iff its u range meets [umin, umax], i.e. its
+// columns form one run.  Same criterion as tile_hit (q_min over the tile's
+// continuous rect <= thr / shrink), with T inflated by 1e-3 and the run
+// widened by 0.01 px against rounding (keeping a tile is always safe; the
+// last column is not clipped to W - 1, which only keeps more).
+// tests/test_raster.py checks the mask holds every tile tile_hit keeps.
+GSR_HD uint64_t tile_mask_rows(const TileCull& t, float mx, float my, float A, float B, float C,
+                               int rx0, int ry0, int rw, int rh, int H) {
+  const int area = rw * rh;
+  const uint64_t all = area >= 64 ? ~0ull : (1ull << area) - 1ull;
+  if (t.mode == 1) return all;
+  if (t.mode == 2) return 0ull;
+  const float T = t.thr / t.shrink * 1.001f;
+  const float det = A * C - B * B;   // > 0: rho < 0.99 in mode 0
+  const float vm = sqrtf(T * A / det);          // |v| reach of the ellipse
+  const float vs = B * sqrtf(T / (C * det));    // v of the leftmost point
+  const float AT = A * T;
+  uint64_t mask = 0ull;
+  for (int ty = t.y0; ty < t.y1; ++ty) {
+    const float yt0 = (float)(ty * BY), yt1 = fminf(yt0 + (BY - 1), (float)(H - 1));
+    const float vb0 = fmaxf(my - yt1, -vm), vb1 = fminf(my - yt0, vm);
+    if (vb0 > vb1) continue;
+    const float vr = fminf(fmaxf(-vs, vb0), vb1), vl = fminf(fmaxf(vs, vb0), vb1);
+    const float umax = (-B * vr + sqrtf(fmaxf(AT - det * vr * vr, 0.0f))) * t.inv_a;
+    const float umin = (-B * vl - sqrtf(fmaxf(AT - det * vl * vl, 0.0f))) * t.inv_a;
+    // tiles tx with 16 tx <= mx - umin and 16 tx + 15 >= mx - umax
+    int c0 = (int)ceilf((mx - umax - 0.01f - (float)(BX - 1)) * (1.0f / BX));
+    int c1 = (int)floorf((mx - umin + 0.01f) * (1.0f / BX));
+    c0 = c0 > t.x0 ? c0 : t.x0;
+    c1 = c1 < t.x1 - 1 ? c1 : t.x1 - 1;
+    if (c0 > c1) continue;
+    const int n = c1 - c0 + 1;
+    mask |= (n >= 64 ? ~0ull : (1ull << n) - 1ull) << ((ty - ry0) * rw + (c0 - rx0));
+  }
+  return mask;
+}
+
 // p (3) through a column-major 4x4 stored as the reference passes it.
 GSR_HD void xform43(const float* m, float x, float y, float z, float* o) {
   o[0] = m[0] * x + m[4] * y + m[8] * z + m[12];

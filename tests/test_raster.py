@@ -112,6 +112,30 @@ def test_oracle_fexp_ulp_bound():
     assert 0.0 < (ulp > 0).mean() < 0.25
 
 
+def test_tile_mask_rows_keeps_every_hit(tmp_path):
+    """The preprocess's row-run tile mask (raster_math.hpp tile_mask_rows)
+    holds every tile the per-tile edge-minimum test (tile_hit) keeps, over
+    400k random ellipses / opacities / rects of 2..64 tiles, and keeps at
+    most 1 % more (the culling is conservative either way; images do not
+    depend on it, only num_rendered does).  Host code built by hipcc."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    here = os.path.dirname(os.path.abspath(__file__))
+    csrc = os.path.join(here, "..", "splatt3r-slam_amd", "csrc")
+    exe = str(tmp_path / "tile_mask_check")
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O2", "-std=c++17", "-ffp-contract=off",
+                    "-I", csrc, os.path.join(here, "native", "tile_mask_check.cpp"), "-o", exe],
+                   check=True, capture_output=True, timeout=600)
+    out = subprocess.run([exe, "400000"], check=True, capture_output=True, text=True, timeout=300)
+    n, hits, kept, miss = map(int, out.stdout.split())
+    assert n == 400000 and hits > 0
+    assert miss == 0, out.stdout
+    assert kept <= hits * 1.01, out.stdout
+
+
 def test_oracle_libm_exp_option_changes_only_low_bits():
     """oracle.raster(exp='libm') runs glibc expf in the blend: the image moves
     by rounding only (the exponential differs by <= 3 ulp)."""
