@@ -1,6 +1,8 @@
 // ABI bookkeeping: last-error buffer, version and arch queries.
 #include "common.hpp"
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 namespace s3 {
@@ -15,6 +17,22 @@ void set_error(const char* fmt, ...) {
 }
 
 void clear_error() { g_err[0] = 0; }
+
+hipError_t wait_event_spin(hipEvent_t ev) {
+  // the budget of the Python side's waits (splatt3r_amd/_lib.py wait_event)
+  static const double budget_us = [] {
+    const char* v = std::getenv("S3_SPIN_US");
+    return v ? std::atof(v) : 1000.0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+    const double us =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (us > budget_us) return hipEventSynchronize(ev);
+  }
+}
 
 }  // namespace s3
 

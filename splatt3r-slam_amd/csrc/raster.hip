@@ -1876,9 +1876,19 @@ int gsr_preprocess(const gsr_settings* s, int64_t P, int M, const float* means3D
   S3_LAUNCH_CHECK();
   tmark(1, st);
   tmark(2, st);
-  static thread_local Reduce red;
-  S3_HIP(hipMemcpyAsync(&red, g.red, sizeof(Reduce), hipMemcpyDeviceToHost, st));
-  S3_HIP(hipStreamSynchronize(st));
+  // read-back into a pinned slot (a pageable destination takes a staged
+  // copy) behind a polled event (a blocking wait adds its wake-up latency to
+  // every forward of the two-call API)
+  static thread_local Reduce* red_host = nullptr;
+  static thread_local hipEvent_t red_ev = nullptr;
+  if (!red_host) {
+    S3_HIP(hipHostMalloc(reinterpret_cast<void**>(&red_host), sizeof(Reduce), hipHostMallocDefault));
+    S3_HIP(hipEventCreateWithFlags(&red_ev, hipEventDisableTiming));
+  }
+  S3_HIP(hipMemcpyAsync(red_host, g.red, sizeof(Reduce), hipMemcpyDeviceToHost, st));
+  S3_HIP(hipEventRecord(red_ev, st));
+  S3_HIP(s3::wait_event_spin(red_ev));
+  const Reduce& red = *red_host;
   unsigned long long total = 0;
   uint32_t kmax = 0, kmin_inv = 0;
   for (int k = 0; k < kRedSlots; ++k) {
