@@ -1,5 +1,6 @@
 // ABI bookkeeping: last-error buffer, version and arch queries.
 #include "common.hpp"
+#include "host_wait.hpp"
 
 #include <chrono>
 #include <cstdlib>

@@ -12,10 +12,6 @@ namespace s3 {
 void set_error(const char* fmt, ...);
 void clear_error();
 
-// Host wait for a recorded event: polled (no blocking wake-up latency) for
-// up to S3_SPIN_US microseconds (default 1000), then a blocking synchronize.
-hipError_t wait_event_spin(hipEvent_t ev);
-
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -18,6 +18,7 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "host_wait.hpp"
 #include "gsr.h"
 #include "raster_math.hpp"
 
