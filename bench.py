@@ -1044,8 +1044,9 @@ def main(argv=None):
                       f"timing: {prof[dom][2]:.3f} ms/frame")
         achieved = fl / (ms * 1e-3) / 1e12
         tr = _pmc_traffic(dom)
-        # algorithmic bytes of the same (non-speculative) launches
-        ab = _algo_bytes(units, dom) * (fl / fl_run if fl_run else 1.0) / a.steps
+        # algorithmic bytes of the same (non-speculative) launches (units'
+        # weights are replays per frame: already per frame)
+        ab = _algo_bytes(units, dom) * (fl / fl_run if fl_run else 1.0)
         result["roofline"] = {
             "bound": "mfma", "kernel": f"s3n {dom} (all launches of one frame)",
             "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
