@@ -320,38 +320,49 @@ class Frontend:
             f.img.record_stream(self.enc_stream)
             self._queue[i + j] = (f, done)
 
-    def _pair_likely_kept(self, i) -> bool:
-        """Whether frame i + 1's slot is likely to be used: it is dropped when
-        frame i becomes a keyframe, i.e. when frame i's min(match_frac_k,
-        unique_frac_f) falls below match_frac_thresh (tracker.py:104-110).
-        Two estimates, either of which declines the pairing: the fraction
+    def _pair_mode(self, i):
+        """Which decode to pair with frame i's (decode-ahead): "same" --
+        frame i + 1 against the current keyframe, used when frame i is NOT
+        made a keyframe; "new" -- frame i + 1 against frame i itself, used
+        when frame i IS made a keyframe (the next frame is then tracked
+        against it, and its decoder inputs are already known: both frames'
+        encoder features); None -- decode frame i alone.  Frame i becomes a
+        keyframe when its min(match_frac_k, unique_frac_f) falls below
+        match_frac_thresh (tracker.py:104-110).  Two estimates: the fraction
         decays as the camera leaves the keyframe, so frame i's is linearly
         extrapolated from the last two frames tracked against the same
         keyframe; and the sequence's own rate of keyframes at frame i's
-        distance from the last keyframe (>= 4 samples), declined above 0.44
-        (a Bp = 2 replay costs ~1.56 Bp = 1 replays, profiles/r03f: pairing
-        pays while the slot is kept with probability > 0.56).  A wrong
-        guess costs speed only, never results."""
+        distance from the last keyframe (>= 4 samples).  A Bp = 2 replay
+        costs ~1.56 Bp = 1 replays (profiles/r03f), so a pairing pays while
+        its slot is used with probability > 0.56: "same" below a keyframe
+        rate of 0.44 unless the extrapolation says keyframe, "new" above
+        0.56, no pairing otherwise (the extrapolation alone, without a rate
+        estimate, declines: it guesses keyframes too often to pair on).
+        A wrong guess costs speed only, never results."""
         fr = self._kf_fracs
-        if len(fr) >= 2 and 2.0 * fr[-1] - fr[-2] < config["tracking"]["match_frac_thresh"]:
-            return False
         made, seen = self._kf_at_dist.get(i - self._last_kf_i, (0, 0))
-        return not (seen >= 4 and made > 0.44 * seen)
+        rate = made / seen if seen >= 4 else None
+        if len(fr) >= 2 and 2.0 * fr[-1] - fr[-2] < config["tracking"]["match_frac_thresh"]:
+            return "new" if rate is not None and rate > 0.56 else None
+        if rate is None or rate < 0.44:
+            return "same"
+        return "new" if rate > 0.56 else None
 
-    def _ahead_source(self, i):
-        """decode-ahead: the queued Frame i + 1 with its encoder ordered
-        before the current stream (called only when a decode is issued), or
-        None when the pairing predictor expects frame i to become a
-        keyframe."""
+    def _ahead_source(self, i, frame):
+        """decode-ahead: (the queued Frame i + 1 with its encoder ordered
+        before the current stream, the frame to decode it against: None =
+        the current keyframe, or Frame i), called only when a decode is
+        issued; None when the predictor declines the pairing."""
         def ahead():
             q = self._queue.get(i + 1)
             if q is None:
                 return None
-            if not self._pair_likely_kept(i):
+            mode = self._pair_mode(i)
+            if mode is None:
                 self.model.encoder.ahead_counts["declined"] += 1
                 return None
             torch.cuda.current_stream(self.device).wait_event(q[1])
-            return q[0]
+            return q[0], (frame if mode == "new" else None)
         return ahead
 
     def _take_prefetched(self, i, T_WC):
@@ -799,7 +810,7 @@ class Frontend:
                 else None
             add_new_kf, _, try_reloc = self.tracker.track(
                 frame, before_sync=hook,
-                ahead=self._ahead_source(i) if self.decode_ahead else None)
+                ahead=self._ahead_source(i, frame) if self.decode_ahead else None)
             # states.set_frame(frame) (main.py:455): the next frame starts from
             # the tracked pose, not from what the backend later writes into
             # the keyframe (the same object here, a shared-memory copy there)

@@ -213,10 +213,12 @@ def _decode_ahead(model, frame_i, frame_j, ahead):
     one replay of the Bp = 2 plan (M = 1536-row GEMMs per branch) instead of
     two Bp = 1 replays.  Slot 1 is kept (views of the plan's output buffers,
     valid until the plan's next replay: `PairPlan.runs`) and used by the next
-    call when that frame is tracked against the same keyframe; a new
-    keyframe in between discards it.  `ahead()` returns the next Frame
-    (encoded, its encoder ordered before the current stream) or None; it is
-    only called when a decode is issued."""
+    call when that frame is tracked against the keyframe it was decoded
+    against: the current keyframe, or frame_i when the predictor expects
+    frame_i to be made the next keyframe; otherwise it is discarded.
+    `ahead()` returns (next Frame -- encoded, its encoder ordered before the
+    current stream --, the Frame to decode it against or None for frame_j)
+    or None; it is only called when a decode is issued."""
     net = model.encoder
     cached = getattr(net, "_ahead_slot", None)
     net._ahead_slot = None
@@ -226,16 +228,26 @@ def _decode_ahead(model, frame_i, frame_j, ahead):
             net.ahead_counts["used"] += 1
             return _slot(pp.res[0], 1), _slot(pp.res[1], 1), _desc16(pp, 1)
         net.ahead_counts["dropped"] += 1
-    nxt = ahead() if ahead is not None else None
+    got = ahead() if ahead is not None else None
+    nxt, against = got if got is not None else (None, None)
+    # slot 1 decodes the next frame against the current keyframe (used when
+    # frame_i stays a tracked frame) or against frame_i itself (used when
+    # frame_i is made the next keyframe): the keyed keyframe must match
+    against = frame_j if against is None else against
     if (nxt is None or nxt.feat is None or nxt.img.shape != frame_i.img.shape
-            or nxt.feat.shape != frame_i.feat.shape):
+            or nxt.feat.shape != frame_i.feat.shape or against.feat is None
+            or against.feat.shape != frame_j.feat.shape):
         return _decode_alone(model, frame_i, frame_j)
     H, W = _hw(frame_i.img_true_shape)
     feat1 = torch.cat((frame_i.feat, nxt.feat))
     pos1 = torch.cat((frame_i.pos, nxt.pos))
-    r1, r2, pp = net.infer_pair(feat1, pos1, frame_j.feat.expand(2, -1, -1),
-                                frame_j.pos.expand(2, -1, -1), (H, W))
-    net._ahead_slot = (_ahead_key(nxt, frame_j), pp, pp.runs)
+    if against is frame_j:
+        feat2, pos2 = frame_j.feat.expand(2, -1, -1), frame_j.pos.expand(2, -1, -1)
+    else:
+        feat2 = torch.cat((frame_j.feat, against.feat))
+        pos2 = torch.cat((frame_j.pos, against.pos))
+    r1, r2, pp = net.infer_pair(feat1, pos1, feat2, pos2, (H, W))
+    net._ahead_slot = (_ahead_key(nxt, against), pp, pp.runs)
     net.ahead_counts["paired"] += 1
     return _slot(r1, 0), _slot(r2, 0), _desc16(pp, 0)
 

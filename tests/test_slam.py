@@ -103,13 +103,16 @@ def test_decode_ahead_frontend_matches_sequential():
 
 
 @pytest.mark.gpu
-def test_decode_ahead_dropped_slots_match_sequential():
+@pytest.mark.parametrize("mode", ["same", "new"])
+def test_decode_ahead_dropped_slots_match_sequential(mode):
     """The invalidation path of decode-ahead: the pairing predictor is
     overridden to always pair, on a sequence with enough motion to create
-    keyframes, so some slots are decoded against a keyframe that is replaced
-    before the next frame is tracked.  Those slots must be dropped (frame
-    tracked against the new keyframe), leaving poses, renders, keyframes and
-    counters bit-identical to the frame-by-frame frontend."""
+    keyframes.  mode "same": the next frame is decoded against the current
+    keyframe, so slots whose keyframe is replaced before the next frame is
+    tracked are dropped; "new": it is decoded against the tracked frame
+    itself, so only the slots of frames that become keyframes are used.
+    Either way poses, renders, keyframes and counters are bit-identical to
+    the frame-by-frame frontend."""
     from splatt3r_amd.slam import Frontend
     from splatt3r_amd.splatt3r_utils import load_splatt3r
     from splatt3r_amd.synthetic import tum_like_sequence
@@ -125,7 +128,7 @@ def test_decode_ahead_dropped_slots_match_sequential():
         fe = Frontend(model, device=dev, spatial_stride=4, render=True,
                       enc_batch=kb, enc_ahead=3 if kb > 1 else None, decode_ahead=ahead)
         if ahead:
-            fe._pair_likely_kept = lambda i: True
+            fe._pair_mode = lambda i: mode
         poses, renders = [], []
         c0 = dict(model.encoder.ahead_counts)
         for i in range(n):
