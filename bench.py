@@ -916,6 +916,19 @@ def main(argv=None):
         fe.tracker.mark = _hmark
         fe.tracker.gpu_mark = _gmark
     ms0 = torch.cuda.memory_stats(dev)
+    # Python garbage collections inside the timed region: (generation, step,
+    # pause ms) -- a host pause of the frame loop that the critical path
+    # would show as an idle gap
+    import gc
+    gc_log, gc_t = [], [0.0]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t[0] = time.perf_counter()
+        else:
+            gc_log.append((info.get("generation"), len(host_ms),
+                           round((time.perf_counter() - gc_t[0]) * 1e3, 3)))
+    gc.callbacks.append(_gc_cb)
     for i in range(a.warmup + 1, nfr):
         h0 = time.perf_counter()
         fe.step(i, frames[i], next_img=nxt(i))
@@ -923,6 +936,7 @@ def main(argv=None):
     fe.drain()                             # every frame's render issued
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
+    gc.callbacks.remove(_gc_cb)
     if hprof is not None:
         import io
         import pstats
@@ -964,6 +978,8 @@ def main(argv=None):
                                       for k, v in by.items()}
     if crit is not None:
         crit["host_step_ms"] = host_ms      # host time inside each Frontend.step
+        # garbage collections in the timed region: [generation, step, pause ms]
+        crit["gc_pauses"] = gc_log
         # device allocations (caching-allocator segments) made by the timed frames
         ms1 = torch.cuda.memory_stats(dev)
         crit["segments_allocated"] = {
