@@ -91,7 +91,18 @@ def camera_settings(extrinsics, intrinsics, near, far, image_shape, background_c
     tan_fov_y = (0.5 * fov_y).tan()
     projection_matrix = get_projection_matrix(near, far, fov_x, fov_y).transpose(1, 2)
     if projection_matrix.device != dev:
-        projection_matrix = projection_matrix.pin_memory().to(dev, non_blocking=True)
+        # intrinsics-only: the same few matrices every frame of a sequence,
+        # uploaded once per value and device (no per-frame pinned staging
+        # buffer and host-to-device copy on the frame's stream)
+        key = (str(dev), projection_matrix.dtype, tuple(projection_matrix.shape),
+               projection_matrix.contiguous().numpy().tobytes())
+        pm = _PROJ_CACHE.get(key)
+        if pm is None:
+            if len(_PROJ_CACHE) >= 64:
+                _PROJ_CACHE.clear()
+            pm = projection_matrix.to(dev)
+            _PROJ_CACHE[key] = pm
+        projection_matrix = pm
     view_matrix = torch.linalg.inv_ex(extrinsics)[0].transpose(1, 2)
     full_projection = view_matrix @ projection_matrix
     tx = tan_fov_x.tolist()
@@ -107,6 +118,7 @@ def camera_settings(extrinsics, intrinsics, near, far, image_shape, background_c
 
 
 _INTR_CACHE: dict = {}
+_PROJ_CACHE: dict = {}
 
 
 def camera_settings_sim3(T_context, T_target, K, image_shape, background_color, near=0.1,
