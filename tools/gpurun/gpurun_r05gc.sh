@@ -6,8 +6,8 @@ mkdir -p $D
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 OFF="--no-e2e --no-pairs --no-backend --no-map --no-c3 --no-cpu-baseline --no-live --no-kprof"
 : > $D/watch.log
-for st in 40 40 40 40 40 40; do
-  S3_HOST_PHASES=1 timeout -k 10 300 python3 bench.py --steps $st --warmup 5 $OFF > $D/one.log 2>&1 || { tail -20 $D/one.log; exit 1; }
+for st in 80 80 80 80 80 80; do
+  timeout -k 10 300 python3 bench.py --steps $st --warmup 5 $OFF > $D/one.log 2>&1 || { tail -20 $D/one.log; exit 1; }
   grep '^{' $D/one.log | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read()); c=d['critical_path']; h=c['host_step_ms']
 big=c['big_gaps']
