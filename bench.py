@@ -915,6 +915,8 @@ def main(argv=None):
             hev.append((len(host_ms), "gpu:" + name, e))
         fe.tracker.mark = _hmark
         fe.tracker.gpu_mark = _gmark
+    if os.environ.get("S3_WAIT_EVENTS"):   # device time of the waits on encoder batches (diagnostic)
+        fe.wait_log = []
     ms0 = torch.cuda.memory_stats(dev)
     # Python garbage collections inside the timed region: (generation, step,
     # pause ms) -- a host pause of the frame loop that the critical path
@@ -980,6 +982,12 @@ def main(argv=None):
         crit["host_step_ms"] = host_ms      # host time inside each Frontend.step
         # garbage collections in the timed region: [generation, step, pause ms]
         crit["gc_pauses"] = gc_log
+        if fe.wait_log is not None:
+            # waits on encoder batches that held the stream > 0.5 ms: [what, frame, ms]
+            crit["encoder_waits"] = [(w, i, round(e0.elapsed_time(e1), 3))
+                                     for w, i, e0, e1 in fe.wait_log
+                                     if e0.elapsed_time(e1) > 0.5]
+            fe.wait_log = None
         # device allocations (caching-allocator segments) made by the timed frames
         ms1 = torch.cuda.memory_stats(dev)
         crit["segments_allocated"] = {

@@ -282,6 +282,7 @@ class Frontend:
         self._kf_at_dist: dict[int, list[int]] = {}
         self._last_kf_i = 0
         self.spans = None          # list -> per-frame GPU events (encoder, main chain)
+        self.wait_log = None       # list -> device time of the waits on encoder batches (diagnostic)
         # main chain on a stream of its own priority (the encoder side stream
         # keeps the default one): the dispatcher then prefers the frame's
         # critical path and the encoder fills the CUs it leaves idle
@@ -361,15 +362,30 @@ class Frontend:
             if mode is None:
                 self.model.encoder.ahead_counts["declined"] += 1
                 return None
-            torch.cuda.current_stream(self.device).wait_event(q[1])
+            self._wait_enc(q[1], "ahead", i + 1)
             return q[0], (frame if mode == "new" else None)
         return ahead
+
+    def _wait_enc(self, done, what, i):
+        """The current stream waits for an encoder batch's completion event;
+        with `wait_log` set (diagnostic), timing events bracket the wait on
+        the device so the stall it causes can be read afterwards."""
+        st = torch.cuda.current_stream(self.device)
+        if self.wait_log is None:
+            st.wait_event(done)
+            return
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        st.wait_event(done)
+        e1.record(st)
+        self.wait_log.append((what, i, e0, e1))
 
     def _take_prefetched(self, i, T_WC):
         if i not in self._queue:
             return None
         frame, done = self._queue.pop(i)
-        torch.cuda.current_stream(self.device).wait_event(done)
+        self._wait_enc(done, "frame", i)
         frame.T_WC = T_WC
         return frame
 
