@@ -429,17 +429,24 @@ def _cpu_render(oracle, r1, r2, img, kimg, threads):
                   nthreads=threads)
 
 
-def bench_backend(model, dev, steps, rank, ws=1):
+def bench_backend(model, dev, steps, rank, ws=1, enc_batch=1, enc_ahead=None, decode_ahead=False,
+                  main_priority=None, warmup=5):
     """The frontend with the reference backend running concurrently
-    (single_thread: False, main.py:122-190): keyframe tasks (retrieval
-    update, add_factors over consecutive + retrieved keyframes, GN) on a
-    worker thread and its own HIP stream.  Timed from the first tracked
-    frame until the backend has drained the queue.  With ws > 1 the
+    (config/base.yaml single_thread: False, main.py:122-190): keyframe tasks
+    (retrieval update, add_factors over consecutive + retrieved keyframes,
+    GN) on a worker thread and its own lowest-priority HIP stream
+    (backend.worker_stream_priority).  The frontend runs the HEADLINE's
+    configuration (encoder lookahead batch, frames queued ahead, decode-ahead,
+    main-chain priority).  Two rates: `frames_per_s` over the frontend loop's
+    window with the backend running beside it -- the reference's FPS window
+    (main.py:363-535: FPS = i / (time - fps_timer), the backend process is
+    not waited for) -- and `frames_per_s_drained`, from the first timed frame
+    until the backend has also drained its queue.  With ws > 1 the
     backend's keyframe-pair batches are sharded (pairs.PairShard: keyframe
     features broadcast from rank 0's worker thread, each pair's two decode
     directions on ranks u mod ws, idx / valid / Q gathered back to rank 0);
     ranks > 0 serve the tasks (pairs.serve_backend) until rank 0 stops."""
-    from splatt3r_amd.backend import Backend
+    from splatt3r_amd.backend import Backend, worker_stream_priority
     from splatt3r_amd.frame import Keyframes
     from splatt3r_amd.pairs import PairShard, serve_backend
     from splatt3r_amd.slam import Frontend
@@ -449,23 +456,31 @@ def bench_backend(model, dev, steps, rank, ws=1):
     if rank > 0:
         sh = serve_backend(model, dev)
         return {"rank": rank, "served_units": sh.stats["units"]}
-    frames = tum_like_sequence(steps + 4, H, W, seed=100 + rank, step_px=2.0, device=dev)
+    kb = max(1, int(enc_batch))
+    look = kb + max(1, enc_ahead or 1)
+    n = warmup + 1 + steps
+    frames = tum_like_sequence(n + look + 1, H, W, seed=100 + rank, step_px=2.0, device=dev)
     shard = PairShard(model, dev) if ws > 1 else None
     be = Backend(model, Keyframes(), device=dev, shard=shard)
     be.start_worker()
-    fe = Frontend(model, device=dev, spatial_stride=4, render=True, backend=be)
-    nxt = lambda i: [frames[i + 1]]
+    fe = Frontend(model, device=dev, spatial_stride=4, render=True, backend=be, enc_batch=kb,
+                  enc_ahead=enc_ahead, decode_ahead=decode_ahead, main_priority=main_priority)
+    nxt = lambda i: [frames[j] for j in range(i + 1, min(i + 1 + look, frames.shape[0]))]
     try:
-        for i in range(3):
+        for i in range(warmup + 1):         # frame 0 = INIT, then warm-up frames
             fe.step(i, frames[i], next_img=nxt(i))
+        fe.drain()
         be.wait()
         torch.cuda.synchronize()
+        fe.reserve_memory()
         s0, b0 = dict(fe.stats), dict(be.stats)
         t0 = time.perf_counter()
-        for i in range(3, 3 + steps):
+        for i in range(warmup + 1, n):
             fe.step(i, frames[i], next_img=nxt(i))
+        fe.drain()
         torch.cuda.synchronize()
         t_front = time.perf_counter() - t0
+        opt_front = be.stats["optimized"] - b0.get("optimized", 0)
         be.wait()
         torch.cuda.synchronize()
         t = time.perf_counter() - t0
@@ -474,17 +489,100 @@ def bench_backend(model, dev, steps, rank, ws=1):
         fe.close()
     st = {k: fe.stats[k] - s0[k] for k in fe.stats}
     bs = {k: be.stats[k] - b0.get(k, 0) for k in be.stats if isinstance(be.stats[k], int)}
-    out = {"frames_per_s": steps / t, "frames_per_s_frontend_only_window": steps / t_front,
-           "steps": steps, "keyframes": st["keyframes"],
+    out = {"frames_per_s": steps / t_front, "frames_per_s_drained": steps / t,
+           "frames_per_s_definition": "frames_per_s: frames / the frontend loop's wall time "
+                                      "with the backend worker running beside it (the "
+                                      "reference's FPS window, main.py:363-535); "
+                                      "frames_per_s_drained: until the backend queue is empty too",
+           "steps": steps, "keyframes": st["keyframes"], "tracked": st["tracked"],
            "keyframe_rate": st["keyframes"] / steps, "backend_tasks": bs["optimized"],
+           "backend_tasks_done_in_frontend_window": opt_front,
            "factor_graph_edges": be.stats["edges"],
            "retrieval_candidates": bs["retrieval_candidates"],
-           "mode": "single_thread: False (worker thread + HIP stream, same GPU)"}
+           "worker_stream_priority": worker_stream_priority(),
+           "frontend_config": {"encoder_batch": kb, "encoder_ahead": enc_ahead,
+                               "decode_ahead": decode_ahead, "main_priority": main_priority},
+           "mode": "single_thread: False (worker thread + lowest-priority HIP stream, same GPU)"}
     if shard is not None:
         out["mode"] += (f"; keyframe-pair batches sharded over {ws} ranks (PairShard, directed "
                         f"units u -> rank u mod {ws})")
         out["rank0_units"] = shard.stats["units"]
     return out
+
+
+def _dry_match_dir(fa, pa, fb, pb, sa, sb):
+    """--dist-dry-run stand-in for splatt3r_match_directed: deterministic per
+    directed unit (keyframe ids carried in the features), whatever batch."""
+    hw = int(sa[0].reshape(-1)[0]) * int(sa[0].reshape(-1)[1])
+    ka, kb = fa[:, 0, 0].long(), fb[:, 0, 0].long()
+    ar = torch.arange(hw)
+    idx = (ar[None] * (ka[:, None] + 1) + kb[:, None]) % hw
+    q = (1.0 + (ar[None] % 5).float() + ka[:, None].float())[..., None]
+    return idx, ((ar[None] + kb[:, None]) % 3 != 0)[..., None], q, q + 1.0
+
+
+_DRY_CAP = 10
+
+
+def _dry_map(pairs, poses, hp):
+    """--dist-dry-run stand-in for PairShard._map_records: 3..9 records per
+    edge of _DRY_CAP rows, valued from the edge, its pose and the filters."""
+    buf = torch.full((len(pairs), _DRY_CAP, 13), -7.0)
+    cnt = torch.zeros(len(pairs), dtype=torch.int64)
+    for p, (i, j) in enumerate(pairs):
+        n = 3 + (5 * i + j) % 7
+        base = float(poses[i].sum()) + float(hp[1]) + 10 * i + j
+        buf[p, :n] = base + torch.arange(n * 13, dtype=torch.float32).reshape(n, 13) * 0.5
+        cnt[p] = n
+    return buf, cnt
+
+
+def _dry_frames(n_kf, H=32, W=48):
+    import lietorch
+    from splatt3r_amd.frame import Frame
+    from splatt3r_amd.net import positions
+    out = []
+    for k in range(n_kf):
+        f = Frame(k, torch.zeros(1, 3, H, W), torch.tensor([[H, W]]),
+                  torch.tensor([[H, W]]), T_WC=lietorch.Sim3.Identity(1))
+        f.feat = torch.full((1, 6, 8), float(k))
+        f.pos = positions(1, 2, 3, "cpu")
+        out.append(f)
+    return out
+
+
+def _dry_shard_check(ws, rank, n_kf=6):
+    """--dist-dry-run: the sharded-unit self-check of `bench.py --gpus N`
+    (pairs.bench_pairs shard_check / map_shard_check) on the CPU stand-ins:
+    rank 0 gathers a pair batch and a map refresh over the ranks, then
+    re-decodes units / edges other ranks produced and compares bit for bit."""
+    from splatt3r_amd.pairs import PairShard
+    sh = PairShard(None, "cpu", match_dir_fn=_dry_match_dir, map_fn=_dry_map,
+                   map_cap=lambda pairs, hp: _DRY_CAP)
+    if rank > 0:
+        sh.serve()
+        return None
+    for k, f in enumerate(_dry_frames(n_kf)):
+        if ws > 1:
+            sh.broadcast_keyframe(k, f)
+        else:
+            sh.register_local(k, f)
+    pairs = [(k - d, k) for k in range(1, n_kf) for d in (1, 2) if k - d >= 0]
+    ii, jj = [p[0] for p in pairs], [p[1] for p in pairs]
+    if ws == 1:
+        # one rank: the stand-in symmetric match is the two directed units
+        sh.match_fn = lambda fi, pi, fj, pj, si, sj: (
+            lambda a, b: (a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3]))(
+            _dry_match_dir(fi, pi, fj, pj, si, sj), _dry_match_dir(fj, pj, fi, pi, sj, si))
+    got = sh.match_pairs(ii, jj)
+    poses = torch.arange(n_kf * 8, dtype=torch.float32).reshape(n_kf, 8) * 0.1
+    mi = list(range(n_kf))
+    mj = [k + 1 if k + 1 < n_kf else k - 1 for k in mi]
+    recs = sh.refresh_map(mi, mj, poses, spatial_stride=4, opacity_threshold=0.0)
+    sh.stop()
+    u = sh.check_units(ii, jj, got, max_units=4)
+    m = sh.check_map(mi, mj, poses, (4.0, 0.98, 1.0, 1.5, 0.0), recs, max_pairs=2)
+    return {"pairs": u, "map": m, "equal": u["equal"] and m["equal"]}
 
 
 def _dry_backend(ws, rank, n_kf=9):
@@ -498,13 +596,7 @@ def _dry_backend(ws, rank, n_kf=9):
     from splatt3r_amd.net import positions
     from splatt3r_amd.pairs import PairShard, serve_backend
 
-    def match_dir(fa, pa, fb, pb, sa, sb):
-        hw = int(sa[0].reshape(-1)[0]) * int(sa[0].reshape(-1)[1])
-        ka, kb = fa[:, 0, 0].long(), fb[:, 0, 0].long()
-        ar = torch.arange(hw)
-        idx = (ar[None] * (ka[:, None] + 1) + kb[:, None]) % hw
-        q = (1.0 + (ar[None] % 5).float() + ka[:, None].float())[..., None]
-        return idx, ((ar[None] + kb[:, None]) % 3 != 0)[..., None], q, q + 1.0
+    match_dir = _dry_match_dir
 
     if rank > 0:
         sh = serve_backend(None, "cpu", match_dir_fn=match_dir)
@@ -770,11 +862,13 @@ def _dry_run(a, ws, rank):
                          dtype=torch.int64)
     if ws > 1:
         dist.all_reduce(units)
+    # the sharded-unit self-check the GPU run prints as shard_check
+    chk = _dry_shard_check(ws, rank)
     if rank == 0:
         line = {"metric": "dist-dry-run", "n_gpus": ws, "world_size": ws,
                 "dist_backend": dist.get_backend() if ws > 1 else None,
                 "pairs": len(pairs), "pairs_covered": int(tot[1]),
-                "checksum": int(tot[0]), "t_max_s": t}
+                "checksum": int(tot[0]), "t_max_s": t, "shard_check": chk}
         if be is not None:
             line["backend"] = dict(be, units_all_ranks=int(units[0]),
                                    mode="Backend worker thread + PairShard over the ranks "
@@ -1032,8 +1126,13 @@ def main(argv=None):
                 "(no dataset or checkpoint offline: keyframe rate and match fractions are "
                 "those of this sequence, not of fr1_desk)",
         "value_definition": "frames tracked / wall time with the frames resident in HBM (the "
-                            "bench contract); the reference's own FPS window (main.py:363-535, "
-                            "PNG read + resize_img + H2D + PNG write) is end_to_end_fps",
+                            "bench contract), frontend only (the headline's synthetic pan makes "
+                            "a keyframe of every other frame); the reference's own FPS window "
+                            "(main.py:363-535) adds the host I/O -- end_to_end_fps (PNG read + "
+                            "resize_img + H2D + PNG write) -- and runs the backend process "
+                            "beside the frontend -- fps_with_backend (same frontend "
+                            "configuration, backend worker on a lowest-priority stream; "
+                            "fps_with_backend_drained also waits for its queue to empty)",
         "world_size": ws, "dist_backend": backend,
         "config": {"workload": "C2 per-frame SLAM tracking, 512x384, config/base.yaml, --no-viz, "
                                "render on, spatial stride 4", "model": "Splatt3R (MASt3RGaussians)",
@@ -1148,11 +1247,26 @@ def main(argv=None):
         c4 = tum_like_sequence(12, 320, 512, seed=200 + rank, step_px=2.0, device=dev)
         result["pairs_c4"] = dict(bench_pairs(model, c4, ws, rank, dev, a.pairs_per_rank),
                                   image="512x320 (C4, EuRoC MH_01 shape)", scaling="weak")
+        if rank == 0:
+            # units / map edges decoded on other ranks, re-decoded on rank 0
+            # after the timed batches and compared bit for bit
+            legs = {k: {c: result[k].get(c) for c in ("shard_check", "map_shard_check")
+                        if result[k].get(c) is not None}
+                    for k in ("pairs", "pairs_strong", "pairs_c4")}
+            result["shard_check"] = {
+                "equal": all(v["equal"] for leg in legs.values() for v in leg.values()),
+                "world_size": ws, "dist_backend": backend, "legs": legs}
     if not a.no_backend:
         # ws > 1: rank 0's backend shards its pair batches over every rank
-        be = bench_backend(model, dev, a.backend_steps, rank, ws)
+        be = bench_backend(model, dev, a.backend_steps, rank, ws, enc_batch=kb,
+                           enc_ahead=a.enc_ahead, decode_ahead=a.decode_ahead,
+                           main_priority=a.main_priority)
         if rank == 0:
             result["backend"] = be
+            # beside `value`: the same frontend configuration with the
+            # reference's concurrent backend (base.yaml single_thread: False)
+            result["fps_with_backend"] = be["frames_per_s"]
+            result["fps_with_backend_drained"] = be["frames_per_s_drained"]
     if rank == 0 and not a.no_map:
         result["map_c5"] = bench_map(dev)
     if rank == 0 and not a.no_c3:

@@ -8,6 +8,7 @@
 // -ffp-contract=off so that the arithmetic is the strict evaluation of the
 // reference source text (see s3m.h).
 #include "common.hpp"
+#include "device_util.hpp"
 #include "s3m.h"
 
 #include <map>
@@ -642,8 +643,12 @@ extern "C" void s3m_refine_set_sort(int mode) {
 
 // Device scratch of the binning, one per (device, stream): tile counts
 // (kept zero between calls: the scan resets them), tile offsets, arrival
-// ranks and the visiting order.  Grown, never shrunk; outgrown buffers are
-// left allocated (work queued on the stream may still read them).
+// ranks and the visiting order.  Grown (to the next power of two), never
+// shrunk.  Growing is refused while the stream is being captured (an
+// allocation is not capturable); otherwise the stream is drained first, so
+// the outgrown buffers, which only work queued on this stream reads, are
+// freed, not leaked.  The first call at the largest batch size should come
+// before any capture (the binning is off by default, s3m_refine_set_sort).
 struct RefineScratch {
   int* cnt = nullptr;
   int* off = nullptr;
@@ -656,12 +661,26 @@ static std::map<std::pair<int, hipStream_t>, RefineScratch> g_scratch;
 
 static int refine_scratch(hipStream_t st, int64_t queries, int64_t tiles, RefineScratch* out) {
   int dev = 0;
-  S3_HIP(hipGetDevice(&dev));
+  S3_HIP(s3::stream_device(st, &dev));
+  s3::DeviceGuard guard(dev);   // allocations on the stream's device
   std::lock_guard<std::mutex> lk(g_scratch_mu);
   RefineScratch& s = g_scratch[{dev, st}];
+  if (s.tiles < tiles || s.queries < queries) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    S3_HIP(hipStreamIsCapturing(st, &cs));
+    S3_REQUIRE(cs == hipStreamCaptureStatusNone,
+               "s3m_refine_matches: the binning scratch must grow (%lld queries, %lld tiles) "
+               "while the stream is being captured; run one call at this size first",
+               (long long)queries, (long long)tiles);
+    S3_HIP(hipStreamSynchronize(st));   // queued reads of the old buffers are done
+  }
   if (s.tiles < tiles) {
     int64_t t = 4096;
     while (t < tiles) t *= 2;
+    if (s.cnt) S3_HIP(hipFree(s.cnt));
+    if (s.off) S3_HIP(hipFree(s.off));
+    s.cnt = s.off = nullptr;
+    s.tiles = 0;
     S3_HIP(hipMalloc(&s.cnt, t * sizeof(int)));
     S3_HIP(hipMalloc(&s.off, t * sizeof(int)));
     S3_HIP(hipMemsetAsync(s.cnt, 0, t * sizeof(int), st));
@@ -670,6 +689,10 @@ static int refine_scratch(hipStream_t st, int64_t queries, int64_t tiles, Refine
   if (s.queries < queries) {
     int64_t q = 1 << 16;
     while (q < queries) q *= 2;
+    if (s.rank) S3_HIP(hipFree(s.rank));
+    if (s.perm) S3_HIP(hipFree(s.perm));
+    s.rank = s.perm = nullptr;
+    s.queries = 0;
     S3_HIP(hipMalloc(&s.rank, q * sizeof(int)));
     S3_HIP(hipMalloc(&s.perm, q * sizeof(int)));
     s.queries = q;

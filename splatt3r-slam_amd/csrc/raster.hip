@@ -18,6 +18,7 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "device_util.hpp"
 #include "host_wait.hpp"
 #include "gsr.h"
 #include "raster_math.hpp"
@@ -916,7 +917,16 @@ k_red_finalize(const Reduce* __restrict__ red, uint32_t cap, int key_bits,
 // backward (and the two-call render) read it as before.
 constexpr int kBinThreads = 256, kBinPer = 4;     // Gaussians per thread
 constexpr int kTileLdsMax = 8192;                 // tiles counted in LDS (fill: 64 KiB)
-constexpr int kTSThreads = 1024, kTSWaves = kTSThreads / 64, kTSIpt = 16;
+// k_tile_sort's LDS image is sized for gfx950's 160 KiB (2 x 16384 x 4 B +
+// counts, ~145 KiB); a device pass for a 64-KiB-LDS target (S3_OFFLOAD_ARCH)
+// gets a quarter of the chunk so the library still builds there (the kernel
+// walks longer tiles in chunks either way).  Only device code reads kTSCap.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+constexpr int kTSIptArch = 4;
+#else
+constexpr int kTSIptArch = 16;
+#endif
+constexpr int kTSThreads = 1024, kTSWaves = kTSThreads / 64, kTSIpt = kTSIptArch;
 constexpr int kTSCap = kTSThreads * kTSIpt;        // instances sorted in LDS
 
 // the kept tiles of one duplication record, in k_duplicate's order
@@ -1879,13 +1889,28 @@ int gsr_preprocess(const gsr_settings* s, int64_t P, int M, const float* means3D
   tmark(2, st);
   // read-back into a pinned slot (a pageable destination takes a staged
   // copy) behind a polled event (a blocking wait adds its wake-up latency to
-  // every forward of the two-call API)
-  static thread_local Reduce* red_host = nullptr;
-  static thread_local hipEvent_t red_ev = nullptr;
-  if (!red_host) {
-    S3_HIP(hipHostMalloc(reinterpret_cast<void**>(&red_host), sizeof(Reduce), hipHostMallocDefault));
-    S3_HIP(hipEventCreateWithFlags(&red_ev, hipEventDisableTiming));
+  // every forward of the two-call API).  The slot and its event belong to
+  // the device of `st` (the caller's current device may be another one): one
+  // per (thread, device), the event created under that device.
+  constexpr int kMaxDev = 64;
+  static thread_local Reduce* red_hosts[kMaxDev] = {};
+  static thread_local hipEvent_t red_evs[kMaxDev] = {};
+  int sdev = -1;
+  S3_HIP(s3::stream_device(st, &sdev));
+  S3_REQUIRE(sdev >= 0 && sdev < kMaxDev, "gsr_preprocess: device %d out of range", sdev);
+  if (!red_hosts[sdev]) {
+    s3::DeviceGuard guard(sdev);
+    Reduce* h = nullptr;
+    hipEvent_t ev = nullptr;
+    S3_HIP(hipHostMalloc(reinterpret_cast<void**>(&h), sizeof(Reduce), hipHostMallocDefault));
+    const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) (void)hipHostFree(h);
+    S3_HIP(e);
+    red_hosts[sdev] = h;
+    red_evs[sdev] = ev;
   }
+  Reduce* red_host = red_hosts[sdev];
+  hipEvent_t red_ev = red_evs[sdev];
   S3_HIP(hipMemcpyAsync(red_host, g.red, sizeof(Reduce), hipMemcpyDeviceToHost, st));
   S3_HIP(hipEventRecord(red_ev, st));
   S3_HIP(s3::wait_event_spin(red_ev));

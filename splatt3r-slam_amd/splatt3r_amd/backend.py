@@ -37,6 +37,17 @@ from splatt3r_amd.config import config
 from splatt3r_amd.global_opt import FactorGraph
 
 
+def worker_stream_priority(priority_range=None) -> int:
+    """HIP stream priority of the backend worker: the LOWEST the device
+    offers (torch numbers priorities so that the range is (lowest, highest),
+    e.g. (0, -1)).  The frontend's main chain runs at high priority and its
+    encoder at normal; the keyframe tasks then fill what those leave and the
+    frontend keeps its frame rate while the queue drains (main.py:122-190
+    runs the backend as a separate process that shares the GPU)."""
+    lo, _hi = priority_range if priority_range is not None else torch.cuda.Stream.priority_range()
+    return int(lo)
+
+
 class Backend:
     def __init__(self, model, keyframes, K=None, device="cuda", retrieval=None, shard=None):
         from splatt3r_amd.retrieval_database import (RetrievalDatabase,
@@ -167,7 +178,8 @@ class Backend:
         frontend."""
         self._q = queue.Queue()
         if self.device.type == "cuda":
-            self._stream = torch.cuda.Stream(device=self.device)
+            self._stream = torch.cuda.Stream(device=self.device,
+                                             priority=worker_stream_priority())
         self._thread = threading.Thread(target=self._loop, daemon=True)
         self._thread.start()
 

@@ -45,11 +45,31 @@ class Frame:
     K: Optional[torch.Tensor] = None
     gaussian_pred: Optional[dict] = None
     gaussian_pred_cross: Optional[dict] = None
-    gs_world: Optional[list] = None   # [(records [n,13], device count)] (slam.py _to_world)
+    # [(records [n,13], device count)] (slam.py _to_world); read through the
+    # `gs_world` property, which orders the reader after the producing stream
+    _gs_world: Optional[list] = dataclasses.field(default=None, repr=False)
+    _gs_world_ready: Optional[object] = dataclasses.field(default=None, repr=False)
 
     def __post_init__(self):
         if self.T_WC is None:
             self.T_WC = lietorch.Sim3.Identity(1, device=self.img.device)
+
+    @property
+    def gs_world(self) -> Optional[list]:
+        """The no-viz world records.  They may be produced on the frontend's
+        aux stream after step() returns; reading them here makes the caller's
+        current stream wait for that producer first (stream-ordered, no host
+        sync)."""
+        ev = self._gs_world_ready
+        if ev is not None and self._gs_world is not None:
+            torch.cuda.current_stream(self.img.device).wait_event(ev)
+        return self._gs_world
+
+    def set_gs_world(self, recs: Optional[list], ready=None) -> None:
+        """Store the records; `ready` is the event recorded on the stream that
+        wrote them (None: written on the caller's stream)."""
+        self._gs_world = recs
+        self._gs_world_ready = ready
 
     def get_score(self, C):
         mode = config["tracking"]["filtering_score"]

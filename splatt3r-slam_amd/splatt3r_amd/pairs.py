@@ -306,6 +306,60 @@ class PairShard:
         return I[:, 0], I[:, 1], V[:, 0, :, None], V[:, 1, :, None], Qt[:, 0, :, None], \
             Qt[:, 1, :, None]
 
+    # ----------------------------------------------------------- checks ---
+    def check_units(self, ii, jj, gathered, max_units: int = 2) -> dict:
+        """Rank 0, after a sharded match_pairs(ii, jj) returned `gathered`:
+        re-decode up to `max_units` directed units that OTHER ranks decoded
+        (u mod W != 0; any unit when W == 1) here, alone, and compare idx,
+        valid and Q bit for bit with what came back through the collectives
+        (global_opt.py:56-66 weighting included).  The backend pair plans are
+        batch-invariant, so a unit decodes to the same bits alone or in its
+        rank's batch: any difference is a transport / ordering fault."""
+        pairs = list(zip((int(i) for i in ii), (int(j) for j in jj)))
+        units = self.units(pairs)
+        cand = [u for u in range(len(units)) if self.ws == 1 or u % self.ws != 0]
+        I_i2j, I_j2i, Vj, Vi, Qj, Qi = gathered
+        n_before = self.stats["units"]
+        checked, equal = [], True
+        for u in cand[:max_units]:
+            p, d = divmod(u, 2)
+            idx, val, q = self._run_units([units[u]])
+            gi = (I_i2j if d == 0 else I_j2i)[p].reshape(-1)
+            gv = (Vj if d == 0 else Vi)[p].reshape(-1)
+            gq = (Qj if d == 0 else Qi)[p].reshape(-1)
+            ok = (torch.equal(idx[0].reshape(-1).to(gi.device), gi)
+                  and torch.equal(val[0].reshape(-1).bool().to(gv.device), gv.bool())
+                  and torch.equal(q[0].reshape(-1).to(gq.device), gq))
+            checked.append({"unit": u, "pair": list(units[u]), "rank": u % self.ws,
+                            "equal": bool(ok)})
+            equal = equal and ok
+        self.stats["units"] = n_before        # the check is not shard work
+        return {"units": checked, "equal": bool(equal and checked),
+                "compared": "idx, valid, Q of units decoded on other ranks vs a local decode"}
+
+    def check_map(self, ii, jj, poses: torch.Tensor, hp, recs: "MapRecords",
+                  max_pairs: int = 1) -> dict:
+        """Rank 0, after refresh_map: recompute the record block of up to
+        `max_pairs` edges that other ranks produced (p mod W != 0; any edge
+        when W == 1) with this rank's map_fn and compare rows and count bit for
+        bit with the all-gathered block."""
+        pairs = list(zip((int(i) for i in ii), (int(j) for j in jj)))
+        poses = poses.reshape(-1, 8).float().contiguous()
+        cand = [p for p in range(len(pairs)) if self.ws == 1 or p % self.ws != 0]
+        checked, equal = [], True
+        for p in cand[:max_pairs]:
+            rec, c = self.map_fn([pairs[p]], poses, tuple(float(x) for x in hp))
+            n = int(c.reshape(-1)[0])
+            ng = int(recs.counts[p])
+            ok = n == ng and torch.equal(rec[0, :n].to(recs.buffers.device),
+                                         recs.buffers[p, :n])
+            checked.append({"edge": p, "pair": list(pairs[p]), "rank": p % self.ws,
+                            "records": n, "equal": bool(ok)})
+            equal = equal and ok
+        return {"edges": checked, "equal": bool(equal and checked),
+                "compared": "world-record block + count of edges re-inferred on other ranks "
+                            "vs a local re-inference"}
+
     # ------------------------------------------------------------- map ----
     def refresh_map(self, ii, jj, poses: torch.Tensor, spatial_stride: int = 1,
                     depth_max_percentile: float = 0.98, max_scale: float = 1.0,
@@ -531,8 +585,20 @@ def bench_pairs(model, frames, ws, rank, dev, pairs_per_rank=4, n_kf=8, reps=3, 
                ms_per_batch=t * 1e3,
                path="FactorGraph.add_factors -> PairShard (pair p on rank p mod W) -> "
                     "gather to rank 0")
+    # after the timed batches: one more sharded batch, whose units decoded on
+    # other ranks rank 0 re-decodes locally and compares bit for bit
+    if rank == 0:
+        got = sh.match_pairs(ii, jj)
+        if ws > 1:
+            sh.stop()
+        out["shard_check"] = sh.check_units(ii, jj, got)
+    else:
+        sh.serve()
     if with_map:
         t_map = timed(map_refresh)
+        if rank == 0:
+            out["map_shard_check"] = sh.check_map(map_i, map_j, poses,
+                                                  (4.0, 0.98, 1.0, 1.5, 0.0), sh.last_map)
         out["map_refresh"] = {"ms": t_map * 1e3, "keyframes": n_kf, "scaling": "strong",
                               "map_gaussians": sh.gmap.n_gaussians,
                               "path": "PairShard.refresh_map: keyframe k re-inferred on rank k "

@@ -710,12 +710,17 @@ class Frontend:
         if recs is None:
             return None
         # the running count on the stream that produced the records
-        ctx = (torch.cuda.stream(self.aux_stream) if self._aux_used and self.gmap is None
-               else contextlib.nullcontext())
+        on_aux = self._aux_used and self.gmap is None and self.aux_stream is not None
+        ctx = torch.cuda.stream(self.aux_stream) if on_aux else contextlib.nullcontext()
+        ready = None
         with ctx:
             for _, cnt in recs:
                 self._gw_count = cnt.clone() if self._gw_count is None else self._gw_count + cnt
-        frame.gs_world = recs
+            if on_aux:
+                # readers of frame.gs_world wait on this (Frame.gs_world)
+                ready = torch.cuda.Event()
+                ready.record(self.aux_stream)
+        frame.set_gs_world(recs, ready)
         return recs
 
     @property

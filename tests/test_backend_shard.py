@@ -226,16 +226,16 @@ def _gpu_rank(rank, ws, port, q):
     # static GEMM policy in both processes (batch-invariant, no per-process
     # timing choices)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), S3_GEMM_TUNE="0")
-    import datetime
-    dist.init_process_group("gloo", rank=rank, world_size=ws,
-                            timeout=datetime.timedelta(seconds=300))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from dist_util import init_gpu_group
+    dev = init_gpu_group(rank, ws, 300)
     try:
         from splatt3r_amd.gaussian_map import SharedGaussians
         from splatt3r_amd.pairs import PairShard, serve_backend
         from splatt3r_amd.splatt3r_utils import load_splatt3r
         from splatt3r_amd.synthetic import tum_like_sequence
         from splatt3r_amd.weights import FULL
-        dev = torch.device("cuda", 0)
         model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
         if rank > 0:
             sh = serve_backend(model, dev, gmap=SharedGaussians(max_gaussians=1 << 21, device=dev))
@@ -287,3 +287,34 @@ def test_slam_with_sharded_backend_equals_single_rank_on_gpu():
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     assert a["n"] == b["n"] == n1 > 0          # rank 1 holds the same map
     assert units1 > 0
+
+
+def test_backend_worker_stream_is_lowest_priority(monkeypatch):
+    """The backend worker's HIP stream takes the lowest priority the device
+    offers (torch's range is (lowest, highest)): the frontend's high-priority
+    main chain and its encoder keep their rate while keyframe tasks drain."""
+    from splatt3r_amd import backend as B
+    assert B.worker_stream_priority((0, -1)) == 0
+    assert B.worker_stream_priority((0, -5)) == 0
+    made = {}
+
+    class FakeStream:
+        def __init__(self, device=None, priority=0):
+            made.update(device=device, priority=priority)
+
+        @staticmethod
+        def priority_range():
+            return (0, -3)
+
+    monkeypatch.setattr(B.torch.cuda, "Stream", FakeStream)
+    monkeypatch.setattr(B.torch.cuda, "set_device", lambda d: None)
+    be = B.Backend.__new__(B.Backend)          # no retrieval database / factor graph needed
+    be.device = torch.device("cuda", 0)
+    be._q = be._thread = be._stream = be._err = None
+    be.start_worker()
+    try:
+        assert made == {"device": torch.device("cuda", 0), "priority": 0}
+    finally:
+        be._q.put(None)
+        be._thread.join(timeout=30)
+    assert not be._thread.is_alive()

@@ -83,6 +83,12 @@ def test_gpus_flag_spawns_ranks_without_a_launcher():
     be = d["backend"]
     assert be["keyframes"] == 9 and be["edges"] == be["pairs"] > 0
     assert be["units_all_ranks"] == 2 * be["pairs"] and 0 < be["rank0_units"] < 2 * be["pairs"]
+    # the sharded-unit self-check the GPU run prints (shard_check): units and
+    # map edges produced on rank 1, re-decoded on rank 0, equal bit for bit
+    sc = d["shard_check"]
+    assert sc["equal"] is True
+    assert sc["pairs"]["units"] and all(u["rank"] == 1 for u in sc["pairs"]["units"])
+    assert sc["map"]["edges"] and all(e["rank"] == 1 for e in sc["map"]["edges"])
 
 
 def test_world_size_must_match_gpus():

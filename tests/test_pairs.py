@@ -179,18 +179,18 @@ def _gpu_shard_worker(rank, ws, port, q):
     # static GEMM launch policy: the per-process tuner times candidates and
     # may pick other tiles in another process (same math, other rounding)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), S3_GEMM_TUNE="0")
-    import datetime
     _beat(rank, "init")
-    dist.init_process_group("gloo", rank=rank, world_size=ws,
-                            timeout=datetime.timedelta(seconds=240))
-    _beat(rank, "process group up")
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from dist_util import init_gpu_group
+    dev = init_gpu_group(rank, ws, 240)
+    _beat(rank, f"process group up ({dist.get_backend()})")
     try:
         from splatt3r_amd.frame import Keyframes, create_frame
         from splatt3r_amd.pairs import PairShard, q_weighted
         from splatt3r_amd.splatt3r_utils import load_splatt3r, splatt3r_match_symmetric
         from splatt3r_amd.synthetic import tum_like_sequence
         from splatt3r_amd.weights import FULL
-        dev = torch.device("cuda", 0)
         model = load_splatt3r(None, device=dev, cfg=FULL, seed=1234, symmetric=True)
         _beat(rank, "model loaded")
         sh = PairShard(model, dev)
@@ -372,3 +372,31 @@ def test_sharded_map_refresh_matches_single_rank_gloo(ws):
         assert len(res[r]) == len(MAP_EDGES)
         for got, w in zip(res[r], want):
             np.testing.assert_array_equal(got, w.numpy())
+
+
+def test_shard_check_detects_a_corrupted_unit():
+    """PairShard.check_units / check_map (bench.py --gpus N shard_check):
+    the local re-decode equals an intact gathered batch, and a single
+    flipped index, valid flag, Q bit or map record is reported unequal."""
+    from splatt3r_amd.pairs import PairShard
+    sh = PairShard(None, "cpu", match_fn=fake_match, match_dir_fn=fake_match_dir,
+                   map_fn=fake_map, map_cap=lambda pairs, hp: FAKE_CAP)
+    for k, f in enumerate(_kf_frames(5)):
+        sh.register_local(k, f)
+    ii, jj = [0, 1, 0, 2, 1], [1, 2, 2, 3, 3]
+    got = sh.match_pairs(ii, jj)
+    assert sh.check_units(ii, jj, got, max_units=10)["equal"] is True
+    assert sh.stats["units"] == 0                     # the check is not counted as work
+    for k, tamper in ((0, lambda t: t.view(-1)[17].add_(1)),
+                      (3, lambda t: t.view(-1)[5].logical_not_()),
+                      (5, lambda t: t.view(-1)[9].add_(1e-6))):
+        bad = [t.clone() for t in got]
+        tamper(bad[k])
+        assert sh.check_units(ii, jj, bad, max_units=10)["equal"] is False
+    poses = torch.arange(6 * 8, dtype=torch.float32).reshape(6, 8) * 0.1
+    mi, mj = [0, 1, 2, 3], [1, 2, 3, 2]
+    hp = (4.0, 0.98, 1.0, 1.5, 0.0)
+    recs = sh.refresh_map(mi, mj, poses, spatial_stride=4, opacity_threshold=0.0)
+    assert sh.check_map(mi, mj, poses, hp, recs, max_pairs=4)["equal"] is True
+    recs.buffers[2, 1, 4] += 1.0
+    assert sh.check_map(mi, mj, poses, hp, recs, max_pairs=4)["equal"] is False
