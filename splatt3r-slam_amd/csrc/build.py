@@ -51,6 +51,7 @@ SOURCES = {
     "net_ops.hip": STRICT,
     "gn_backend.hip": STRICT,
     "retrieval.hip": STRICT,
+    "gemm_bd.hip": FAST,
 }
 
 
