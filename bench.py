@@ -293,7 +293,9 @@ def _kernel_profile(units, reps=3):
     return agg
 
 
-_KFAM = re.compile(r"k_gemm<([^>]*)>")
+# k_gemm / k_gemm_pp: A mode = template argument 5; k_gemm_bd (B-direct
+# tiles) are dense only
+_KFAM = re.compile(r"k_gemm(?:_pp)?<([^>]*)>")
 
 
 def _algo_bytes(units, kind):
@@ -329,7 +331,9 @@ def _kernel_trace(units, reps=5):
             if "CUDA" not in str(e.device_type):
                 continue
             m = _KFAM.search(e.name)
-            if m:
+            if "k_gemm_bd<" in e.name:
+                k = "gemm.dense"
+            elif m:
                 k = "gemm.dense" if m.group(1).split(",")[4].strip() == "0" else "gemm.conv"
             elif "k_conv3_halo" in e.name:     # the halo-reuse conv tiles (net_gemm_t6.hip)
                 k = "gemm.conv"

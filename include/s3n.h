@@ -102,6 +102,12 @@ typedef struct {
   float* tail_out[S3N_MAX_GROUPS];
   int tail_n;
   int64_t ld_tail;
+  /* Optional fragment-packed copy of each group's B for the B-direct tiles
+   * (70-77): Bp[nb][ks][lane][8] fp16 with nb = n / 16 (N padded to a
+   * multiple of 16 with zeros), ks = k / 32, lane = 16 * ((k % 32) / 8) +
+   * n % 16, element k % 8; dense A only, K % 32 == 0.  NULL: those tiles
+   * are unavailable (the other tiles never read it). */
+  const void* Bp[S3N_MAX_GROUPS];
 } s3n_gemm_args;
 
 size_t s3n_gemm_workspace_bytes(const s3n_gemm_args* args);

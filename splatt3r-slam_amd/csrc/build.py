@@ -47,11 +47,11 @@ SOURCES = {
     "net_gemm_t6.hip": FAST,
     "net_gemm_t7.hip": FAST,
     "net_gemm_t8.hip": FAST,
+    "net_gemm_t9.hip": FAST,
     "net_attn.hip": FAST,
     "net_ops.hip": STRICT,
     "gn_backend.hip": STRICT,
     "retrieval.hip": STRICT,
-    "gemm_bd.hip": FAST,
 }
 
 

@@ -1,7 +1,7 @@
 // Grouped fp16 MFMA GEMM (include/s3n.h s3n_gemm): argument checks and the
 // C ABI.  The kernel template is net_gemm_kernel.hpp; its tile families are
-// instantiated in net_gemm_t1..t5.hip, the halo conv in net_gemm_t6.hip
-// (compiled in parallel).
+// instantiated in net_gemm_t1..t5.hip, the halo conv in net_gemm_t6.hip, the
+// B-direct tiles in net_gemm_t9.hip (compiled in parallel).
 #include "net_gemm_kernel.hpp"
 
 namespace s3gemm {
@@ -15,7 +15,7 @@ int s3n_ln_f16_saturations(int reset);   // net_ops.hip
 extern "C" int s3n_f16_saturations(int reset) {
   int any = 0;
   for (auto fn : {s3gemm::sat_t1, s3gemm::sat_t2, s3gemm::sat_t3, s3gemm::sat_t4, s3gemm::sat_t5,
-                  s3gemm::sat_t6, s3gemm::sat_t7, s3gemm::sat_t8}) {
+                  s3gemm::sat_t6, s3gemm::sat_t7, s3gemm::sat_t8, s3gemm::sat_t9}) {
     const int v = fn(reset);
     if (v < 0) return -1;
     any |= v;
@@ -63,6 +63,7 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
     p.R2[g] = on ? a->R2[g] : nullptr;
     p.C[g] = on ? a->C[g] : nullptr;
     p.C2[g] = on ? (f16*)a->C2[g] : nullptr;
+    p.Bp[g] = on ? (const f16*)a->Bp[g] : nullptr;
   }
   p.lda = a->lda; p.ldb = a->ldb; p.ldr1 = a->ldr1; p.r1_f16 = a->r1_f16;
   p.ldr2 = a->ldr2; p.r2_f16 = a->r2_f16; p.ldc = a->ldc; p.c_f16 = a->c_f16;
@@ -123,7 +124,7 @@ extern "C" int s3n_gemm(const s3n_gemm_args* a, void* stream) {
   // tile families live in their own translation units (net_gemm_t*.hip)
   for (auto fn : {s3gemm::launch_t1, s3gemm::launch_t2, s3gemm::launch_t3, s3gemm::launch_t4,
                   s3gemm::launch_t5, s3gemm::launch_t6, s3gemm::launch_t7,
-                  s3gemm::launch_t8}) {
+                  s3gemm::launch_t8, s3gemm::launch_t9}) {
     const int r = fn(a->tile, p, st);
     if (r != s3gemm::kNotMine) return r;
   }

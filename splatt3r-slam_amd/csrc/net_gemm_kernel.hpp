@@ -40,6 +40,7 @@ int launch_t5(int tile, const GemmP& p, hipStream_t st);
 int launch_t6(int tile, const GemmP& p, hipStream_t st);
 int launch_t7(int tile, const GemmP& p, hipStream_t st);
 int launch_t8(int tile, const GemmP& p, hipStream_t st);
+int launch_t9(int tile, const GemmP& p, hipStream_t st);
 // read (and optionally reset) one translation unit's fp16 saturation flag
 int sat_t1(int reset);
 int sat_t2(int reset);
@@ -49,6 +50,7 @@ int sat_t5(int reset);
 int sat_t6(int reset);
 int sat_t7(int reset);
 int sat_t8(int reset);
+int sat_t9(int reset);
 constexpr int kNotMine = -1000;
 }  // namespace s3gemm
 
@@ -91,6 +93,7 @@ struct GemmP {
   const float* rope_sin;
   int rope_ncols;
   const int64_t* rope_pos[S3N_MAX_GROUPS];
+  const f16* Bp[S3N_MAX_GROUPS];   // fragment-packed B (net_gemm_t9.hip), or null
 };
 }  // namespace s3gemm
 

@@ -4,7 +4,7 @@
 // row of the tile) keeps the LDS-DMA ring and XOR-swizzled fragment reads of
 // k_gemm (net_gemm_kernel.hpp).
 //
-// Packed layout (s3n_gemm_pack_b): Bp[nb][ks][lane][8] for nb = n / 16,
+// Packed layout (s3n_gemm_args.Bp, ops.packed_b): Bp[nb][ks][lane][8] for nb = n / 16,
 // ks = k / 32, lane = 16 * ((k % 32) / 8) + n % 16, element k % 8 -- one
 // v_mfma_f32_16x16x32_f16 B fragment is 1 KiB contiguous, so a wave loads
 // it with one fully coalesced 16-B-per-lane buffer load.  N is padded to a
@@ -30,10 +30,6 @@ namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-struct BpArr {
-  const f16* p[S3N_MAX_GROUPS];
-};
-
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < N) {
@@ -56,7 +52,7 @@ constexpr int bd_min_waves() {
 
 template <int BM, int BN, int NWM, int NWN, int S>
 __global__ void __launch_bounds__(64 * NWM * NWN, (bd_min_waves<BM, BN, NWM, NWN, S>()))
-k_gemm_bd(GemmP p, BpArr bpa) {
+k_gemm_bd(GemmP p) {
   typedef AccT<16> AT;
   constexpr int BK = 64;
   constexpr int NW = NWM * NWN;
@@ -98,7 +94,7 @@ k_gemm_bd(GemmP p, BpArr bpa) {
   const int wm = wave / NWN, wn = wave % NWN;
   const int M = p.M, N = p.N, K = p.K;
   const f16* __restrict__ A = p.A[g];
-  const f16* __restrict__ Bp = bpa.p[g];
+  const f16* __restrict__ Bp = p.Bp[g];
   const int KT = (K + BK - 1) / BK;
   const int KS = K / 32;            // packed K steps (host: K % 32 == 0)
   const int Npad = (N + 15) & ~15;
@@ -205,65 +201,36 @@ k_gemm_bd(GemmP p, BpArr bpa) {
 }
 
 template <int BM, int BN, int NWM, int NWN, int S>
-int launch_bd(const GemmP& p, const BpArr& bp, hipStream_t st) {
+int launch_bd(const GemmP& p, hipStream_t st) {
+  S3_REQUIRE(p.a_mode == S3N_A_DENSE && p.Bp[0] && p.vec_epi && p.split_k <= 1 && !p.tail_w[0] &&
+                 p.K % 32 == 0,
+             "s3n_gemm: B-direct tiles need dense A, the packed B (s3n_gemm_args.Bp), the vector "
+             "epilogue, split_k 1, no fused tail and K %% 32 == 0");
   const GemmP q = plan_grid(p, BM, BN, 64);
   dim3 grid(q.tiles_m * q.tiles_n, 1, p.groups);
-  k_gemm_bd<BM, BN, NWM, NWN, S><<<grid, 64 * NWM * NWN, 0, st>>>(q, bp);
+  k_gemm_bd<BM, BN, NWM, NWN, S><<<grid, 64 * NWM * NWN, 0, st>>>(q);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }
 
 }  // namespace
 
-extern "C" {
-
-// Experimental entry (tools/bench_gemm_bd.py): s3n_gemm's dense path with the
-// packed B of each group in bp[g] (host array of device pointers),
-// plain store, no split-K / RoPE / tail / scatter.
-int s3n_gemm_bd_exp(const s3n_gemm_args* a, const void* const* bp_host, int variant,
-                    void* stream) {
-  S3_REQUIRE(a && a->a_mode == S3N_A_DENSE && a->K % 32 == 0 && a->split_k <= 1 &&
-                 a->store_mode == S3N_STORE_PLAIN && !a->tail_w[0] && !a->rope_pos[0] &&
-                 a->N % 8 == 0 && a->ldc % 8 == 0 && a->lda % 8 == 0,
-             "s3n_gemm_bd_exp: dense plain GEMM only");
-  s3gemm::GemmP p{};
-  p.M = a->M; p.N = a->N; p.K = a->K; p.groups = a->groups;
-  for (int g = 0; g < S3N_MAX_GROUPS; ++g) {
-    const bool on = g < a->groups;
-    p.A[g] = on ? (const f16*)a->A[g] : nullptr;
-    p.B[g] = on ? (const f16*)a->B[g] : nullptr;
-    p.bias[g] = on ? a->bias[g] : nullptr;
-    p.R1[g] = on ? a->R1[g] : nullptr;
-    p.R2[g] = on ? a->R2[g] : nullptr;
-    p.C[g] = on ? a->C[g] : nullptr;
-    p.C2[g] = on ? (f16*)a->C2[g] : nullptr;
-    p.tail_w[g] = nullptr;
-    p.tail_b[g] = nullptr;
-    p.tail_out[g] = nullptr;
-    p.rope_pos[g] = nullptr;
+namespace s3gemm {
+// tiles 70-77 (ops._BDIRECT); launch configurations measured against the
+// LDS-staged tiles of the same reduction class on the network's dense shapes
+// (tools/bench_gemm_bd.py, profiles/r06b_gemm_bdirect.log)
+int launch_t9(int tile, const GemmP& p, hipStream_t st) {
+  switch (tile) {
+    case 70: return launch_bd<64, 128, 1, 4, 3>(p, st);    // wave 64 x 32
+    case 71: return launch_bd<64, 128, 1, 4, 2>(p, st);    // double-buffered
+    case 72: return launch_bd<64, 64, 1, 4, 3>(p, st);     // wave 64 x 16
+    case 73: return launch_bd<64, 64, 1, 4, 4>(p, st);
+    case 74: return launch_bd<128, 128, 1, 4, 4>(p, st);   // wave 128 x 32
+    case 75: return launch_bd<128, 128, 1, 4, 3>(p, st);
+    case 76: return launch_bd<128, 128, 2, 4, 3>(p, st);   // 8 waves, wave 64 x 32
+    case 77: return launch_bd<64, 128, 1, 4, 4>(p, st);
+    default: return kNotMine;
   }
-  p.lda = a->lda; p.ldb = a->ldb; p.ldr1 = a->ldr1; p.r1_f16 = a->r1_f16;
-  p.ldr2 = a->ldr2; p.r2_f16 = a->r2_f16; p.ldc = a->ldc; p.c_f16 = a->c_f16;
-  p.ldc2 = a->ldc2; p.act = a->act; p.store_mode = 0; p.a_mode = 0;
-  p.split_k = 1;
-  p.vec_epi = 1;
-  BpArr bp{};
-  for (int g = 0; g < a->groups; ++g) bp.p[g] = reinterpret_cast<const f16*>(bp_host[g]);
-  hipStream_t st = s3::as_stream(stream);
-  switch (variant) {
-    case 0: return launch_bd<128, 128, 2, 2, 3>(p, bp, st);   // wave 64 x 64
-    case 1: return launch_bd<128, 128, 1, 4, 3>(p, bp, st);   // wave 128 x 32, B unshared
-    case 2: return launch_bd<128, 128, 2, 4, 3>(p, bp, st);   // 8 waves, wave 64 x 32
-    case 3: return launch_bd<256, 128, 4, 2, 3>(p, bp, st);   // 8 waves, wave 64 x 64
-    case 4: return launch_bd<64, 128, 1, 4, 3>(p, bp, st);    // wave 64 x 32
-    case 5: return launch_bd<128, 64, 2, 2, 3>(p, bp, st);    // wave 64 x 32
-    case 6: return launch_bd<64, 64, 1, 4, 4>(p, bp, st);     // wave 64 x 16
-    case 7: return launch_bd<128, 256, 2, 4, 3>(p, bp, st);   // 8 waves, wave 64 x 64
-    case 8: return launch_bd<128, 128, 2, 2, 4>(p, bp, st);
-    case 9: return launch_bd<64, 128, 2, 2, 4>(p, bp, st);    // wave 32 x 64
-    default: break;
-  }
-  S3_REQUIRE(false, "s3n_gemm_bd_exp: unknown variant %d", variant);
 }
-
-}  // extern "C"
+int sat_t9(int reset) { return read_sat(reset); }
+}  // namespace s3gemm

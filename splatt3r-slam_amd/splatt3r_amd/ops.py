@@ -40,6 +40,7 @@ class GemmArgs(ctypes.Structure):
         ("rope_ncols", ctypes.c_int), ("rope_pos", P * G),
         ("tail_w", P * G), ("tail_b", P * G), ("tail_out", P * G), ("tail_n", ctypes.c_int),
         ("ld_tail", I64),
+        ("Bp", P * G),
     ]
 
 
@@ -242,7 +243,13 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
                 51: (128, 128), 52: (128, 128), 53: (256, 64),
                 # k_gemm_pp: fragment reads of half a K tile overlap the MFMAs
                 # of the other half (net_gemm_t8.hip)
-                63: (128, 128), 65: (128, 128), 68: (256, 128)}
+                63: (128, 128), 65: (128, 128), 68: (256, 128),
+                # B fragments straight from the packed weights into registers,
+                # A through the LDS ring (net_gemm_t9.hip)
+                70: (64, 128), 71: (64, 128), 72: (64, 64), 73: (64, 64), 74: (128, 128),
+                75: (128, 128), 76: (128, 128), 77: (64, 128)}
+# the B-direct tiles: dense A, a packed B (packed_b), split_k 1, no fused tail
+_BDIRECT = set(range(70, 78))
 _TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14, 40, 42, 43, 45, 46, 48, 49, 51, 52, 63, 65}
 # S3_GEMM_MF16=0: leave the 16x16x32 tile family out of the tuner (A/B)
 _EXCLUDED = set(range(21, 32)) if os.environ.get("S3_GEMM_MF16", "1") == "0" else set()
@@ -263,19 +270,23 @@ _TILE_RED = {1: (64, 1, 32), 2: (64, 1, 32), 3: (64, 1, 32), 4: (64, 1, 32), 5: 
              40: (64, 1, 16), 41: (64, 1, 16), 42: (64, 1, 32), 43: (64, 1, 16),
              45: (64, 1, 32), 46: (64, 1, 16), 47: (64, 1, 16), 48: (64, 1, 32), 49: (64, 1, 16),
              50: (64, 1, 16), 51: (64, 1, 16), 52: (64, 1, 32), 53: (64, 1, 16),
-             63: (64, 1, 16), 65: (64, 1, 32), 68: (64, 1, 16)}
+             63: (64, 1, 16), 65: (64, 1, 32), 68: (64, 1, 16),
+             **{t: (64, 1, 16) for t in range(70, 78)}}
 _REGS_EPILOGUE = {14, 34, 35}   # the fp32 tile does not fit the LDS ring
 # K tiles in (ky, channel chunk, kx) order instead of (ky, kx, channel chunk)
 _HALO = set(range(40, 54)) - {44}
 # S3_GEMM_HALO=0: leave the halo-reuse conv tiles out of the tuner (A/B)
 if os.environ.get("S3_GEMM_HALO", "1") == "0":
     _EXCLUDED |= _HALO
+# S3_GEMM_BDIRECT=0: leave the B-direct tiles out of the tuner (A/B)
+if os.environ.get("S3_GEMM_BDIRECT", "1") == "0":
+    _EXCLUDED |= _BDIRECT
 
 
 def _db_digest() -> str:
     import hashlib
     tables = (sorted(_TILE_SHAPES.items()), sorted(_TILE_RED.items()), sorted(_REGS_EPILOGUE),
-              sorted(_HALO), sorted(_TAIL_OK))
+              sorted(_HALO), sorted(_TAIL_OK), sorted(_BDIRECT))
     return hashlib.sha1(repr(tables).encode()).hexdigest()[:16]
 
 
@@ -371,7 +382,7 @@ def _tune_key(a):
          "ldr1", "ldr2", "ldc2", "store_mode", "sS", "sCout", "a_mode", "cH", "cW", "cC", "ksize",
          "stride", "pad", "oH", "oW", "relu_in", "rope_ncols", "tail_n", "ld_tail")
     return tuple(getattr(a, k) for k in f) + (bool(a.R1[0]), bool(a.R2[0]), bool(a.C2[0]),
-                                               bool(a.bias[0]), bool(a.C[0]))
+                                               bool(a.bias[0]), bool(a.C[0]), bool(a.Bp[0]))
 
 
 def _tune_candidates(a, split_ok, like=None):
@@ -385,9 +396,11 @@ def _tune_candidates(a, split_ok, like=None):
         if tile in _HALO and not (a.a_mode == 1 and a.ksize == 3 and a.stride == 1 and
                                   a.oW % bm == 0 and a.cC % 64 == 0):
             continue
+        if tile in _BDIRECT and not (a.Bp[0] and a.a_mode == 0 and not a.tail_n and a.K % 32 == 0):
+            continue
         tiles = a.groups * -(-a.M // bm) * -(-a.N // bn)
         for sk in (1, 2, 3, 4, 6, 8):
-            if sk > 1 and tile in _HALO:
+            if sk > 1 and (tile in _HALO or tile in _BDIRECT):
                 continue
             if like is not None:
                 # batch-invariant plan: only launches whose elements equal
@@ -501,6 +514,31 @@ def _tuned(a, A, B, bias, rope, rope_pos, split_ok, like=None):
     return best
 
 
+def packed_b(B) -> torch.Tensor | None:
+    """The fragment-packed copy of a weight matrix B [N, K] (fp16, rows
+    contiguous) that the B-direct tiles read (s3n.h s3n_gemm_args.Bp):
+    [ceil(N/16)][K/32][4][16][8], one v_mfma_f32_16x16x32_f16 B fragment per
+    KiB, N padded with zero rows.  Built once per weight and kept on the
+    tensor that owns the storage (a stacked group weight for its group
+    views), so it lives exactly as long as the weights.  None when B is not
+    such a tensor (raw pointer, other dtype / layout, K % 32 != 0)."""
+    if not isinstance(B, torch.Tensor) or B.dtype != torch.float16 or B.dim() != 2 or not B.is_cuda:
+        return None
+    N, K = B.shape
+    if K % 32 or B.stride() != (K, 1):
+        return None
+    owner = B._base if B._base is not None else B
+    cache = owner.__dict__.setdefault("_s3_packed", {})
+    key = (B.storage_offset(), N, K, B._version)
+    P_ = cache.get(key)
+    if P_ is None:
+        Np = -(-N // 16) * 16
+        Bz = B if Np == N else torch.cat([B, B.new_zeros(Np - N, K)])
+        P_ = Bz.reshape(Np // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+        cache[key] = P_
+    return P_
+
+
 def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1=None,
          ldr1=0, R2=None, ldr2=0, C2=None, ldc2=0, conv=None, store=None, split_k=None,
          tile=0, rope=None, rope_pos=None, rope_ncols=0, tail=None, batch=1,
@@ -526,6 +564,14 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
     a.C = _parr(C)
     a.lda = int(lda)
     a.ldb = int(ldb if ldb is not None else K)
+    # packed weights for the B-direct tiles (dense A only; every group or none)
+    bpk = None
+    if conv is None and tail is None and a.ldb == K:
+        bpk = [packed_b(b) for b in B]
+        if any(x is None for x in bpk):
+            bpk = None
+        else:
+            a.Bp = _parr(bpk)
     a.ldc = int(ldc if ldc is not None else N)
     a.bias = _parr(bias or [])
     a.act = ACT[act]
@@ -614,7 +660,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
     if tail is not None:
         per += 4 * M_ * int(tail[3]) + 2 * int(tail[3]) * N_
     return Call("s3n_gemm", ctypes.byref(a), keep=(a, A, B, C, bias, R1, R2, C2, ws, rope,
-                                                    rope_pos, tail),
+                                                    rope_pos, tail, bpk),
                 kind="gemm.conv" if conv is not None else "gemm.dense",
                 flops=2 * int(M) * int(N) * int(K) * groups, nbytes=per * groups,
                 desc=f"gemm{'.conv' if conv is not None else ''} {M}x{N}x{K} g{groups}"

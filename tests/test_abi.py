@@ -99,3 +99,26 @@ def test_error_path_reports_message():
     st = lib.s3lie_sim3_inv(None, None, -1, None)
     assert st == 1
     assert b"n < 0" in lib.s3_last_error()
+
+
+def test_gemm_args_layout_matches_the_c_header():
+    """ops.GemmArgs (ctypes) has the size and B-direct field offset of the C
+    s3n_gemm_args (include/s3n.h), compiled here with gcc."""
+    import ctypes
+    import os
+    import subprocess
+    import tempfile
+    from splatt3r_amd import ops
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    src = ('#include <stdio.h>\n#include <stddef.h>\n#include "s3n.h"\n'
+           'int main(void) { printf("%zu %zu %zu\\n", sizeof(s3n_gemm_args), '
+           'offsetof(s3n_gemm_args, Bp), offsetof(s3n_gemm_args, ld_tail)); return 0; }\n')
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "l.c"), os.path.join(d, "l")
+        with open(c, "w") as f:
+            f.write(src)
+        subprocess.run(["gcc", "-I", inc, c, "-o", exe], check=True)
+        size, bp, ldt = (int(x) for x in subprocess.run([exe], capture_output=True, text=True,
+                                                       check=True).stdout.split())
+    assert ctypes.sizeof(ops.GemmArgs) == size
+    assert ops.GemmArgs.Bp.offset == bp and ops.GemmArgs.ld_tail.offset == ldt

@@ -138,6 +138,81 @@ def test_gemm_pp_tiles_bitexact_vs_same_reduction_class(pp, ref, M, N, K, groups
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("bd,ref,M,N,K,groups", [
+    (70, 32, 1536, 3072, 768, 2), (71, 26, 6144, 1024, 1024, 1), (72, 22, 300, 200, 1056, 2),
+    (73, 26, 130, 296, 992, 1), (74, 32, 1536, 2304, 768, 2), (75, 28, 520, 296, 640, 1),
+    (76, 32, 300, 136, 544, 2), (77, 26, 768, 1024, 4096, 1), (70, 32, 64, 40, 96, 1),
+    (71, 32, 1, 24, 32, 1), (72, 26, 200, 1040, 2080, 3)])
+def test_gemm_bdirect_tiles_bitexact_vs_same_reduction_class(bd, ref, M, N, K, groups):
+    """The B-direct tiles (net_gemm_t9.hip: B fragments from the packed
+    weights, ops.packed_b, straight into registers) compute every element
+    in the reduction class of the LDS-staged 16x16x32 tiles: bit-identical
+    outputs with the full epilogue (bias, GELU, fp32 residual, fp16 out +
+    copy), ragged M, N % 16 != 0 (zero-padded packed rows), K % 64 == 32,
+    a single row and K tile; and correct against torch."""
+    from splatt3r_amd import ops, _lib
+    assert ops.reduction_class(K, bd, 1) == ops.reduction_class(K, ref, 1)
+    A = [_rand(M, K, seed=g) for g in range(groups)]
+    W = [_rand(N, K, scale=K ** -0.5, seed=10 + g) for g in range(groups)]
+    b = [_rand(N, dtype=torch.float32, seed=20 + g) for g in range(groups)]
+    R = [_rand(M, N, dtype=torch.float32, seed=30 + g) for g in range(groups)]
+    outs = []
+    for tile in (bd, ref):
+        C = [torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16)
+             for _ in range(groups)]
+        C2 = [torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16)
+              for _ in range(groups)]
+        ops.gemm(A, W, C, M, N, K, lda=K, bias=b, act="gelu", R1=R, ldr1=N, C2=C2, ldc2=N,
+                 split_k=1, tile=tile)(_lib.stream())
+        outs.append((C, C2))
+    for g in range(groups):
+        assert torch.equal(outs[0][0][g], outs[1][0][g])
+        assert torch.equal(outs[0][0][g], outs[0][1][g])
+        ref_ = F.gelu(A[g].float() @ W[g].float().T + b[g]) + R[g]
+        assert rel_err(outs[0][0][g], ref_) < 2e-3
+
+
+@pytest.mark.parametrize("tile", [70, 74])
+def test_gemm_bdirect_rope_and_scatter_epilogues(tile):
+    """The B-direct tiles share the LDS-staged epilogue: the fused RoPE2D
+    columns and the ConvTranspose scatter store equal tile 32's bits."""
+    from splatt3r_amd import ops, _lib
+    from splatt3r_amd.net import positions, rope_tables
+    B, ht, wt, K = 1, 24, 32, 128
+    M, Nout = B * ht * wt, 16 * 64
+    cos, sin = rope_tables(64, "cuda")
+    pos = [positions(B, ht, wt, "cuda")]
+    A, W = [_rand(M, K, seed=41)], [_rand(Nout, K, scale=K ** -0.5, seed=51)]
+    b = [_rand(Nout, dtype=torch.float32, seed=61)]
+    got = []
+    for t in (tile, 32):
+        C = [torch.empty(M, Nout, device="cuda")]
+        ops.gemm(A, W, C, M, Nout, K, lda=K, bias=b, rope=(cos, sin), rope_pos=pos,
+                 rope_ncols=1024, tile=t)(_lib.stream())
+        got.append(C[0])
+    assert torch.equal(got[0], got[1])
+    s, cout, K2 = 2, 64, 256
+    A2, W2 = [_rand(M, K2, seed=42)], [_rand(s * s * cout, K2, scale=K2 ** -0.5, seed=52)]
+    got = []
+    for t in (tile, 32):
+        C = [torch.empty(B, ht * s, wt * s, cout, device="cuda")]
+        ops.gemm(A2, W2, C, M, s * s * cout, K2, lda=K2, store=("convt", ht, wt, s, cout),
+                 tile=t)(_lib.stream())
+        got.append(C[0])
+    assert torch.equal(got[0], got[1])
+
+
+def test_gemm_bdirect_tiles_need_a_packed_b():
+    """Without a packed B (B given as a raw pointer) the B-direct tiles fail
+    instead of running another tile."""
+    from splatt3r_amd import ops, _lib
+    M, N, K = 256, 256, 256
+    A, W = [_rand(M, K)], _rand(N, K, scale=K ** -0.5, seed=1)
+    C = [torch.empty(M, N, device="cuda")]
+    with pytest.raises(RuntimeError, match="B-direct"):
+        ops.gemm(A, [W.data_ptr()], C, M, N, K, lda=K, split_k=1, tile=70)(_lib.stream())
+
+
 @pytest.mark.parametrize("tile", [21, 26, 32, 36, 63, 68])
 def test_gemm_mf16_tiles_reject_unaligned_n(tile):
     """A 16x16x32 tile stages its fp32 tile through LDS (vector epilogue:

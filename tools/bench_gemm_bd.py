@@ -1,17 +1,15 @@
-"""B-direct GEMM experiment (csrc/gemm_bd.hip): the weights read from a
-fragment-packed copy straight into registers, A through the LDS ring.
-Times each variant on the network's dense shapes next to the tiles the
-tuner picks today (same reduction class: 16x16x32, no split, vector
-epilogue) and hipBLASLt, and checks the outputs are bit-identical to the
-class's tile 32.
+"""B-direct GEMM tiles (csrc/net_gemm_t9.hip, tiles 70-77: the weights read
+from a fragment-packed copy straight into registers, A through the LDS
+ring) timed on the network's dense shapes next to the LDS-staged tiles of
+the same reduction class (16x16x32, no split, vector epilogue) and
+hipBLASLt; outputs checked bit-identical to the class's tile 32 ('!' marks
+a difference).
 
-  python -m tools.bench_gemm_bd [--variants 0,1,2] [--shapes MxNxKxG,...]
+  python -m tools.bench_gemm_bd [--tiles 70,71] [--shapes MxNxKxG,...]
 """
 from __future__ import annotations
 
 import argparse
-import ctypes
-
 import torch
 
 from splatt3r_amd import _lib, ops
@@ -22,26 +20,13 @@ SHAPES = ["1536x768x768x2", "1536x2304x768x2", "1536x1536x768x2", "1536x3072x768
           "6144x1024x4096x1", "1536x7168x1792x2", "1536x6400x7168x2"]
 
 
-def pack_b(B: torch.Tensor) -> torch.Tensor:
-    """[N, K] fp16 -> [ceil(N/16)][K/32][4][16][8] (gemm_bd.hip layout)."""
-    N, K = B.shape
-    Np = -(-N // 16) * 16
-    if Np != N:
-        B = torch.cat([B, B.new_zeros(Np - N, K)])
-    return B.view(Np // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
-
-
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,9")
-    ap.add_argument("--ref-tiles", default="32,26,22,28,63,68,29,24")
+    ap.add_argument("--tiles", default="70,71,72,73,74,75,76,77")
+    ap.add_argument("--ref-tiles", default="32,26,22,63")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--act", default="gelu")
     a = ap.parse_args()
-    L = _lib.lib()
-    fn = L.s3n_gemm_bd_exp
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
-    fn.restype = ctypes.c_int
     st = _lib.stream()
     for sh in a.shapes.split(","):
         M, N, K, G = (int(x) for x in sh.split("x"))
@@ -50,7 +35,6 @@ def main():
         B = [(torch.randn(N, K, device="cuda", generator=gen) * K ** -0.5).half() for _ in range(G)]
         bias = [torch.randn(N, device="cuda", generator=gen) * 0.1 for _ in range(G)]
         C = [torch.empty(M, N, device="cuda", dtype=torch.float16) for _ in range(G)]
-        Bp = [pack_b(b) for b in B]
         fl = 2 * M * N * K * G
         line = [f"{sh:>18}"]
         ref = ops.gemm(A, B, C, M, N, K, lda=K, split_k=1, tile=32, bias=bias, act=a.act)
@@ -65,22 +49,15 @@ def main():
                 line.append(f"t{t} --")
                 continue
             line.append(f"t{t} {us:6.1f}")
-        best_ref = None
-        call = ops.gemm(A, B, C, M, N, K, lda=K, split_k=1, tile=32, bias=bias, act=a.act)
-        args = call.keep[0]
-        bp_host = (ctypes.c_void_p * 4)(*[b.data_ptr() for b in Bp], *([None] * (4 - G)))
-        for v in (int(x) for x in a.variants.split(",") if x):
+        for t in (int(x) for x in a.tiles.split(",") if x):
             for c in C:
                 c.zero_()
-            rc = fn(ctypes.byref(args), ctypes.cast(bp_host, ctypes.c_void_p), v, st)
-            if rc != 0:
-                line.append(f"v{v} err")
-                continue
+            c = ops.gemm(A, B, C, M, N, K, lda=K, split_k=1, tile=t, bias=bias, act=a.act)
+            c(_lib.stream())
             torch.cuda.synchronize()
-            eq = all(torch.equal(c, w) for c, w in zip(C, want))
-            us = timeit(lambda: fn(ctypes.byref(args), ctypes.cast(bp_host, ctypes.c_void_p), v,
-                                   _lib.stream()), reps=20)
-            line.append(f"v{v} {us:6.1f}{'' if eq else '!'}")
+            eq = all(torch.equal(x, w) for x, w in zip(C, want))
+            us = timeit(lambda: c(_lib.stream()), reps=20)
+            line.append(f"t{t} {us:6.1f}{'' if eq else '!'}")
         # hipBLASLt calibration (no epilogue)
         Bt = [b.t() for b in B]
         us = timeit(lambda: [torch.matmul(x, y) for x, y in zip(A, Bt)], reps=20)
