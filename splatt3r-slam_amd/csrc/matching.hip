@@ -435,6 +435,135 @@ k_refine_lane(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21
   }
 }
 
+// Pixel-major refine: 3 lanes per candidate pixel, one 16-B chunk (8 of the
+// 24 fp16 descriptor values) each.  Radius 3, F = 24.  A query's 21 lanes
+// are 7 triplets, triplet t owning window column i = t (u = ub + t d); 3
+// queries per wave (lane 63 idles).  Per dilation level the wave moves the
+// window into LDS by LDS-DMA one window row at a time: row j's instruction
+// has triplet t read pixel (u_t, v_j) as 48 contiguous bytes, so a query's
+// row is 7 x 48 B of one image row (contiguous at d = 1) -- about a third of
+// the 64-B segments per load of the candidate-per-lane kernels, which the
+// texture addresser bounds (profiles/r05j).
+//
+// The reference's strict fp16 chain (matching_kernels.cu:55-64: every
+// product and every partial sum rounded to fp16, elements 0..23 in order)
+// runs systolically over the triplet: at step s member c scores chunk c of
+// window row j = s - c, starting from the partial sum member c - 1 produced
+// for the same pixel one step earlier (handed over by a wave_shr:1 DPP move;
+// member 0 starts from 0).  Member 2 finishes row s - 2 and keeps its
+// column's first strictly larger score (rows in scan order); the 7 columns
+// are then merged keeping the larger score and, on a tie, the smaller
+// column -- the sequential scan's first maximum (c = i 7 + j, i outer).
+// Same rule against the maximum carried in from the coarser levels.
+__global__ void __launch_bounds__(kBlock)
+k_refine_px(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
+            const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w, int n,
+            int dilation_max, const int* __restrict__ perm) {
+  constexpr int F = 24, R = 3, SIDE = 2 * R + 1, QPW = 3, LPQ = 3 * SIDE;
+  constexpr int WAVES = kBlock / 64;
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  typedef int i4 __attribute__((ext_vector_type(4)));
+  // window rows of every wave: [wave][row j][lane] 16 B (the LDS-DMA image)
+  __shared__ __attribute__((aligned(1024))) i4 win[WAVES][SIDE][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int qw = lane / LPQ;               // query of the wave (3: the idle lane)
+  const int r = lane - qw * LPQ;
+  const int t = r / 3, c = r - 3 * (r / 3);
+  const int64_t i = ((int64_t)blockIdx.x * WAVES + wave) * QPW + qw;
+  const int64_t b = blockIdx.y;
+  const bool live = qw < QPW && i < n;
+  const int64_t pi = b * (int64_t)n + (live ? (perm ? perm[b * (int64_t)n + i] : i) : 0);
+  // this member's 8 query values
+  h2 q[4];
+  {
+    const i4 x = *reinterpret_cast<const i4*>(D21 + pi * F + c * 8);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int xe = x[e];
+      q[e] = __builtin_bit_cast(h2, xe);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<_Float16*>(D11 + b * (int64_t)h * w * F), (short)0, (int)((int64_t)h * w * F * 2),
+      0x00020000);
+  constexpr uint32_t PIX = F * 2;
+  constexpr uint32_t kOff = 0x80000000u;   // out of range: the DMA writes zeros
+  // lane of the query's member-2 lane of column tt: qw * 21 + 3 tt + 2
+  const int base = qw * LPQ;
+  int64_t u0 = p1[pi * 2 + 0], v0 = p1[pi * 2 + 1];
+  _Float16 max_score = (_Float16)0.0f;      // Half() == 0, see k_refine
+  int64_t u_new = u0, v_new = v0;
+  for (int d = dilation_max; d > 0; --d) {
+    const int64_t ub = u0 - R * d, vb = v0 - R * d;
+    const int64_t u = ub + (int64_t)t * d;
+    const bool ou = live && u >= 0 && u < w;
+    uint32_t okr = 0;                       // bit j: pixel (u, v_j) inside the image
+#pragma unroll
+    for (int j = 0; j < SIDE; ++j) {
+      const int64_t v = vb + (int64_t)j * d;
+      const bool ok = ou && v >= 0 && v < h;
+      okr |= (uint32_t)ok << j;
+      const uint32_t off = ok ? (uint32_t)(v * w + u) * PIX + 16u * c : kOff;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)&win[wave][j][0], 16, (int)off, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's rows are in LDS
+    _Float16 best = max_score;
+    int best_j = -1;
+    _Float16 carry = (_Float16)0.0f;
+#pragma unroll
+    for (int s = 0; s < SIDE + 2; ++s) {
+      const int j = s - c;                  // this member's window row
+      const int jc = j < 0 ? 0 : (j >= SIDE ? SIDE - 1 : j);
+      const i4 x = win[wave][jc][lane];
+      _Float16 sc = c == 0 ? (_Float16)0.0f : carry;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int xe = x[e];
+        const h2 prod = q[e] * __builtin_bit_cast(h2, xe);
+        sc = sc + prod[0];
+        sc = sc + prod[1];
+      }
+      if (c == 2 && j >= 0 && j < SIDE && ((okr >> j) & 1u) && sc > best) {
+        best = sc;
+        best_j = j;
+      }
+      // hand the partial sum to the next member (lane + 1)
+      const int scb = (int)__builtin_bit_cast(unsigned short, sc);
+      const int nb = __builtin_amdgcn_update_dpp(0, scb, 0x138, 0xf, 0xf, false);   // wave_shr:1
+      carry = __builtin_bit_cast(_Float16, (unsigned short)nb);
+    }
+    // merge the 7 columns in column order: larger score, the smaller column
+    // on a tie (only a column that beat the carried maximum has best_j >= 0)
+    const int mine = ((int)__builtin_bit_cast(unsigned short, best) << 8) | (best_j & 0xff);
+    _Float16 lbest = max_score;
+    int lt = -1, lj = -1;
+#pragma unroll
+    for (int tt = 0; tt < SIDE; ++tt) {
+      const int o = __shfl(mine, base + 3 * tt + 2, 64);
+      const int oj = (int)(signed char)(o & 0xff);
+      const _Float16 os = __builtin_bit_cast(_Float16, (unsigned short)((o >> 8) & 0xffff));
+      if (oj >= 0 && os > lbest) {
+        lbest = os;
+        lt = tt;
+        lj = oj;
+      }
+    }
+    if (lt >= 0) {
+      max_score = lbest;
+      u_new = ub + (int64_t)lt * d;
+      v_new = vb + (int64_t)lj * d;
+    }
+    u0 = u_new;
+    v0 = v_new;
+  }
+  if (live && r == 0) {
+    p1_new[pi * 2 + 0] = u_new;
+    p1_new[pi * 2 + 1] = v_new;
+  }
+}
+
 // Window-centre binning ahead of the refine.  On the
 // tracking loop the queries' window centres scatter (pixel order puts 64
 // queries of one frame row on 64 columns and several rows of the keyframe),
@@ -627,8 +756,8 @@ static int g_refine_pf = 4;
 static int g_refine_sort = kRefineSortDefault;
 // (any other value, e.g. -1: the default)
 extern "C" void s3m_refine_set_lanes(int lanes) {
-  g_refine_lanes = (lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16 ||
-                    lanes == 32 || lanes == 64)
+  g_refine_lanes = (lanes == 1 || lanes == 2 || lanes == 3 || lanes == 4 || lanes == 8 ||
+                    lanes == 16 || lanes == 32 || lanes == 64)
                        ? lanes : kRefineLanesDefault;
 }
 extern "C" void s3m_refine_set_prefetch(int pf) {
@@ -768,14 +897,19 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* 
   auto d21 = reinterpret_cast<const _Float16*>(D21);
   auto st = s3::as_stream(stream);
   const int side = 2 * radius + 1;
-  const bool lane_k = g_refine_lanes <= 4 && refine_lane_ok(h, w, fdim, radius);
+  const bool px_k = g_refine_lanes == 3 && refine_lane_ok(h, w, fdim, radius);
+  const bool lane_k = !px_k && g_refine_lanes <= 4 && refine_lane_ok(h, w, fdim, radius);
   const bool coop_k = side * side <= 64 && (fdim == 24 || fdim == 16 || fdim == 32);
   const int* perm = nullptr;
-  if (lane_k || coop_k) {
+  if (px_k || lane_k || coop_k) {
     const int rc = refine_order(p1, b, h, w, n, st, &perm);
     if (rc != S3_OK) return rc;
   }
-  if (lane_k) {
+  if (px_k) {
+    // 3 queries per wave, 4 waves per workgroup
+    dim3 pg((unsigned)s3::cdiv(n, 3 * (kBlock / 64)), (unsigned)b);
+    k_refine_px<<<pg, kBlock, 0, st>>>(d11, d21, p1, p1_new, h, w, n, dilation_max, perm);
+  } else if (lane_k) {
     refine_lane(d11, d21, p1, p1_new, b, h, w, n, dilation_max, perm, st);
   } else if (coop_k) {
     const int lanes = g_refine_lanes <= 4 ? 16 : g_refine_lanes;   // other radius / fdim

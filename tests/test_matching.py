@@ -136,13 +136,14 @@ def test_hip_refine_bitexact_vs_oracle(f):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sort", [0, 0x33])
-@pytest.mark.parametrize("lanes,pf", [(1, 4), (1, 6), (2, 2), (2, 4), (4, 3), (16, 3)])
+@pytest.mark.parametrize("lanes,pf", [(1, 4), (1, 6), (2, 2), (2, 4), (3, 4), (4, 3), (16, 3)])
 @pytest.mark.parametrize("f,radius,dil", [(24, 3, 5), (24, 2, 3), (32, 1, 2), (24, 4, 2), (8, 3, 5)])
 def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil, lanes, pf, sort):
     """Quantised descriptors make many equal fp16 scores: every kernel must
     keep the first candidate in the reference's scan order.  lanes 1 / 2 / 4
     = k_refine_lane with 1 / 2 / 4 lanes per query (radius 3, f 24; pf its
-    load distance), 16 = k_refine_coop (the default); radius 4 (81
+    load distance), 3 = k_refine_px (3 lanes per pixel, the fp16 chain
+    handed lane to lane), 16 = k_refine_coop; radius 4 (81
     candidates) and fdim 8 take the generic per-lane kernel.  Query points
     up to 3 pixels off the image exercise the masked window slots.  sort:
     queries visited in window-centre tile order (8 x 8 tiles) or pixel order."""
@@ -169,7 +170,7 @@ def test_hip_refine_ties_and_windows_vs_oracle(f, radius, dil, lanes, pf, sort):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sort", [0x11, 0x60, 0x06, 0x42, 0x66])
-@pytest.mark.parametrize("lanes", [1, 4, 16])
+@pytest.mark.parametrize("lanes", [1, 3, 4, 16])
 def test_hip_refine_tile_orders_vs_oracle(sort, lanes):
     """Window-centre binning with lopsided tiles (2x2, 64x1, 1x64, 16x4,
     64x64: one tile per image), three batches of different query spread
@@ -227,7 +228,8 @@ def _tracker_like_init(h, w, rng, shift=(1, 2), jitter=2):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lanes,sort", [(None, None), (16, 0), (1, 0x33), (2, 0x42)])
+@pytest.mark.parametrize("lanes,sort", [(None, None), (16, 0), (3, 0), (3, 0x33), (1, 0x33),
+                                        (2, 0x42)])
 @pytest.mark.parametrize("h,w", [(384, 512), (320, 512)])
 def test_hip_refine_full_size_tracker_init_vs_oracle(h, w, lanes, sort):
     """refine_matches at the C2 / C4 frame sizes the tracker runs every

@@ -13,9 +13,8 @@ from splatt3r_amd.splatt3r_utils import load_splatt3r
 from splatt3r_amd.synthetic import tum_like_sequence
 from splatt3r_amd.weights import FULL
 
-VARIANTS = [(16, 0), (16, 0x33), (16, 0x42), (8, 0x33), (1, 0x33), (2, 0x33), (4, 0x33),
-            (1, 0x42), (2, 0x42), (4, 0x42), (1, 0x22), (2, 0x22), (4, 0x44), (16, 0x22),
-            (1, 0x43), (2, 0x43), (16, 0)]
+VARIANTS = [(16, 0), (3, 0), (3, 0x33), (3, 0x42), (3, 0x22), (16, 0x33), (1, 0x33), (4, 0x42),
+            (16, 0), (3, 0)]
 
 
 def timeit(fn, reps=20):
