@@ -80,6 +80,8 @@ def _args(argv=None):
     ap.add_argument("--pairs-per-rank", type=int, default=4)
     ap.add_argument("--no-kprof", action="store_true",
                     help="skip the per-launch network profile (roofline object)")
+    ap.add_argument("--no-in-window", action="store_true",
+                    help="skip the in-frame-loop kernel trace (roofline.in_window)")
     ap.add_argument("--enc-batch", type=int, default=8,
                     help="frames per encoder replay (lookahead over the sequence); the last "
                          "replay of the timed region is partial when --steps is not a multiple")
@@ -307,6 +309,75 @@ def _algo_bytes(units, kind):
                for wgt, plans in units for pl in plans)
 
 
+def _family(name: str):
+    """Roofline family of a network kernel name (None: not a network kernel)."""
+    m = _KFAM.search(name)
+    if "k_gemm_bd<" in name:
+        return "gemm.dense"
+    if m:
+        return "gemm.dense" if m.group(1).split(",")[4].strip() == "0" else "gemm.conv"
+    if "k_conv3_halo" in name:             # the halo-reuse conv tiles (net_gemm_t6.hip)
+        return "gemm.conv"
+    if "k_splitk_reduce" in name:
+        return "gemm.dense"
+    if "k_attn" in name:
+        return "s3n_attention"
+    if "k_layernorm" in name:
+        return "s3n_layernorm"
+    return None
+
+
+def bench_in_window(model, dev, steps, warmup, kb, enc_ahead, decode_ahead, main_priority):
+    """Kernel durations INSIDE a frame loop: a second
+    frontend with the headline's configuration runs `steps` frames of
+    another synthetic sequence under a torch.profiler (roctracer) kernel
+    trace, encoder side stream and main chain running concurrently as in the
+    timed region; per frame: {family: [launches, ms, executed GFLOP]}.
+    The trace slows the host a little, so this window is not the headline;
+    the kernels' own durations are what it measures."""
+    from torch.profiler import ProfilerActivity, profile
+    from splatt3r_amd.slam import Frontend
+    from splatt3r_amd.synthetic import tum_like_sequence
+    look = kb + max(1, enc_ahead or 1)
+    n = warmup + 1 + steps
+    frames = tum_like_sequence(n + look + 1, H, W, seed=300, step_px=2.0, device=dev)
+    fe = Frontend(model, device=dev, spatial_stride=4, render=True, enc_batch=kb,
+                  enc_ahead=enc_ahead, decode_ahead=decode_ahead, main_priority=main_priority)
+    nxt = lambda i: [frames[j] for j in range(i + 1, min(i + 1 + look, frames.shape[0]))]
+    try:
+        for i in range(warmup + 1):
+            fe.step(i, frames[i], next_img=nxt(i))
+        fe.drain()
+        torch.cuda.synchronize()
+        units0 = model.encoder.plan_units()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            for i in range(warmup + 1, n):
+                fe.step(i, frames[i], next_img=nxt(i))
+            fe.drain()
+            torch.cuda.synchronize()
+        units = _frame_units(model.encoder, units0, steps)
+    finally:
+        fe.close()
+    fam = {}
+    for e in prof.events():
+        if "CUDA" not in str(e.device_type):
+            continue
+        k = _family(e.name)
+        if k is None:
+            continue
+        f = fam.setdefault(k, [0.0, 0.0, 0.0])
+        if "k_splitk_reduce" not in e.name:
+            f[0] += 1.0 / steps
+        f[1] += e.device_time_total / 1e3 / steps
+    for wgt, plans in units:
+        for pl in plans:
+            for c in pl.calls:
+                k = getattr(c, "kind", None)
+                if k in fam:
+                    fam[k][2] += wgt * c.flops / 1e9
+    return fam
+
+
 def _kernel_trace(units, reps=5):
     """{family: [launches per frame, ms per frame]} of the network kernels:
     a torch.profiler (roctracer) kernel trace of `reps` serial replays of
@@ -330,20 +401,8 @@ def _kernel_trace(units, reps=5):
         for e in prof.events():
             if "CUDA" not in str(e.device_type):
                 continue
-            m = _KFAM.search(e.name)
-            if "k_gemm_bd<" in e.name:
-                k = "gemm.dense"
-            elif m:
-                k = "gemm.dense" if m.group(1).split(",")[4].strip() == "0" else "gemm.conv"
-            elif "k_conv3_halo" in e.name:     # the halo-reuse conv tiles (net_gemm_t6.hip)
-                k = "gemm.conv"
-            elif "k_splitk_reduce" in e.name:
-                k = "gemm.dense"
-            elif "k_attn" in e.name:
-                k = "s3n_attention"
-            elif "k_layernorm" in e.name:
-                k = "s3n_layernorm"
-            else:
+            k = _family(e.name)
+            if k is None:
                 continue
             f = fam.setdefault(k, [0.0, 0.0])
             if "k_splitk_reduce" not in e.name:
@@ -914,6 +973,10 @@ def main(argv=None):
         _prewarm(local)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    # the frame loop's dedicated streams first, before anything takes a
+    # stream from torch's pool: each gets a hardware queue of its own
+    from splatt3r_amd import _lib
+    _lib.reserve_frame_streams(dev)
     from splatt3r_amd.slam import Frontend
     from splatt3r_amd.splatt3r_utils import load_splatt3r
     from splatt3r_amd.synthetic import tum_like_sequence
@@ -1214,6 +1277,19 @@ def main(argv=None):
                              "speculative_gflop_per_frame and excluded from achieved"}
         if trace:
             result["roofline"]["trace_ms_per_frame"] = {k: v[1] for k, v in trace.items()}
+        if not a.no_in_window:
+            iw = bench_in_window(model, dev, 16, a.warmup, kb, a.enc_ahead, a.decode_ahead,
+                                 a.main_priority)
+            if dom in iw and iw[dom][1] > 0:
+                l_iw, ms_iw, gf_iw = iw[dom]
+                result["roofline"]["in_window"] = {
+                    "achieved": gf_iw / ms_iw, "frac": gf_iw / ms_iw / PEAK_F16_TFLOPS,
+                    "ms_per_frame": ms_iw, "launches_per_frame": l_iw,
+                    "executed_gflop_per_frame": gf_iw,
+                    "timing": "roctracer kernel timestamps (torch.profiler) of 16 frames of a "
+                              "frame loop with the headline's configuration (encoder side stream "
+                              "and main chain concurrent), executed FLOPs of the same window",
+                    "families_ms_per_frame": {k: v[1] for k, v in iw.items()}}
         if tr:
             result["roofline"]["traffic_detail"] = tr
         result["network"] = {"kernels": {k: {"launches": v[0], "gflop": v[1] / 1e9, "ms": v[2]}

@@ -40,6 +40,15 @@ int s3_abi_version(void);
 /* Name of the offload architecture the library was built for ("gfx950"). */
 const char* s3_arch(void);
 
+/* A non-blocking HIP stream of the given priority (HIP numbering: 0 =
+ * normal, negative = higher) on `device`, for the frame loop's dedicated
+ * streams (splatt3r_amd/_lib.py frame_stream): the runtime hands every new
+ * stream a hardware queue when it is created (GPU_MAX_HW_QUEUES per
+ * priority, then shared), so streams created first, in a fixed order, get
+ * queues of their own.  *out receives the hipStream_t. */
+int s3_stream_create(int device, int priority, void** out);
+int s3_stream_destroy(void* stream);
+
 #ifdef __cplusplus
 }
 #endif

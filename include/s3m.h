@@ -37,8 +37,10 @@ int s3m_refine_matches(const uint16_t* D11, const uint16_t* D21,
                        void* stream);
 
 /* Tuning hooks (not on the product path): lanes per query point of the
- * refine (1, 2, 4: per-lane kernel for radius 3 / fdim 24; 8, 16 = default,
- * 32, 64: cooperative kernel, also used for every other radius / fdim) and
+ * refine (1, 2, 4: per-lane kernel for radius 3 / fdim 24; 3 = default:
+ * pixel-major kernel for radius 3 / fdim 24, three lanes per window pixel;
+ * 8, 16, 32, 64: cooperative kernel, 16 of them also for every other
+ * radius / fdim) and
  * the per-lane kernel's load distance in candidates (2, 3, 4 = default, 6);
  * results identical for every setting.  s3m_refine_set_sort: visit the
  * queries in the order of the 2^sx x 2^sy pixel tile holding their window

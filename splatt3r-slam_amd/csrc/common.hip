@@ -1,5 +1,6 @@
 // ABI bookkeeping: last-error buffer, version and arch queries.
 #include "common.hpp"
+#include "device_util.hpp"
 #include "host_wait.hpp"
 
 #include <chrono>
@@ -40,3 +41,20 @@ hipError_t wait_event_spin(hipEvent_t ev) {
 extern "C" const char* s3_last_error(void) { return s3::g_err; }
 extern "C" int s3_abi_version(void) { return 1; }
 extern "C" const char* s3_arch(void) { return "gfx950"; }
+
+extern "C" int s3_stream_create(int device, int priority, void** out) {
+  S3_REQUIRE(out, "s3_stream_create: null out");
+  s3::DeviceGuard guard(device);
+  int least = 0, greatest = 0;
+  S3_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  const int pr = priority < greatest ? greatest : (priority > least ? least : priority);
+  hipStream_t s = nullptr;
+  S3_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pr));
+  *out = reinterpret_cast<void*>(s);
+  return S3_OK;
+}
+
+extern "C" int s3_stream_destroy(void* stream) {
+  if (stream) S3_HIP(hipStreamDestroy(s3::as_stream(stream)));
+  return S3_OK;
+}

@@ -469,6 +469,7 @@ k_refine_px(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
   const int wave = threadIdx.x >> 6;
   const int qw = lane / LPQ;               // query of the wave (3: the idle lane)
   const int r = lane - qw * LPQ;
+  const int base = qw * LPQ;               // the query's first lane
   const int t = r / 3, c = r - 3 * (r / 3);
   const int64_t i = ((int64_t)blockIdx.x * WAVES + wave) * QPW + qw;
   const int64_t b = blockIdx.y;
@@ -487,36 +488,49 @@ k_refine_px(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<_Float16*>(D11 + b * (int64_t)h * w * F), (short)0, (int)((int64_t)h * w * F * 2),
       0x00020000);
-  constexpr uint32_t PIX = F * 2;
+  constexpr int PIX = F * 2;
   constexpr uint32_t kOff = 0x80000000u;   // out of range: the DMA writes zeros
-  // lane of the query's member-2 lane of column tt: qw * 21 + 3 tt + 2
-  const int base = qw * LPQ;
-  int64_t u0 = p1[pi * 2 + 0], v0 = p1[pi * 2 + 1];
+  // image coordinates fit 32 bits (refine_lane_ok: h w F 2 < 2^31)
+  int u0 = (int)p1[pi * 2 + 0], v0 = (int)p1[pi * 2 + 1];
   _Float16 max_score = (_Float16)0.0f;      // Half() == 0, see k_refine
-  int64_t u_new = u0, v_new = v0;
+  int u_new = u0, v_new = v0;
+  // this lane's slot of window row 0 (row j is 64 slots further)
+  i4* const wl = &win[wave][0][lane];
   for (int d = dilation_max; d > 0; --d) {
-    const int64_t ub = u0 - R * d, vb = v0 - R * d;
-    const int64_t u = ub + (int64_t)t * d;
-    const bool ou = live && u >= 0 && u < w;
+    const int ub = u0 - R * d, vb = v0 - R * d;
+    const int u = ub + t * d;
+    const bool ou = live && (unsigned)u < (unsigned)w;
+    const int row_step = d * w * PIX;
+    int off = (vb * w + u) * PIX + 16 * c;  // pixel (u, v_0), chunk c (used when in range)
     uint32_t okr = 0;                       // bit j: pixel (u, v_j) inside the image
 #pragma unroll
     for (int j = 0; j < SIDE; ++j) {
-      const int64_t v = vb + (int64_t)j * d;
-      const bool ok = ou && v >= 0 && v < h;
+      const bool ok = ou && (unsigned)(vb + j * d) < (unsigned)h;
       okr |= (uint32_t)ok << j;
-      const uint32_t off = ok ? (uint32_t)(v * w + u) * PIX + 16u * c : kOff;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)&win[wave][j][0], 16, (int)off, 0, 0, 0);
+          rs, (__attribute__((address_space(3))) void*)&win[wave][j][0], 16,
+          ok ? off : (int)kOff, 0, 0, 0);
+      off += row_step;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's rows are in LDS
+    // bit s: member 2 compares at step s (its row s - 2 is inside the image)
+    const uint32_t cmpm = c == 2 ? okr << 2 : 0u;
     _Float16 best = max_score;
     int best_j = -1;
     _Float16 carry = (_Float16)0.0f;
 #pragma unroll
     for (int s = 0; s < SIDE + 2; ++s) {
+      // step s reads window rows <= s: this wave's DMA of row s has landed
+      // once at most 6 - s of its row instructions are outstanding (in order)
+      if (s == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (s == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else if (s == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (s == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if (s == 4) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (s == 5) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else if (s == 6) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int j = s - c;                  // this member's window row
       const int jc = j < 0 ? 0 : (j >= SIDE ? SIDE - 1 : j);
-      const i4 x = win[wave][jc][lane];
+      const i4 x = wl[jc * 64];
       _Float16 sc = c == 0 ? (_Float16)0.0f : carry;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -525,35 +539,37 @@ k_refine_px(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
         sc = sc + prod[0];
         sc = sc + prod[1];
       }
-      if (c == 2 && j >= 0 && j < SIDE && ((okr >> j) & 1u) && sc > best) {
+      if (s >= 2 && ((cmpm >> s) & 1u) && sc > best) {
         best = sc;
-        best_j = j;
+        best_j = s - 2;
       }
-      // hand the partial sum to the next member (lane + 1)
-      const int scb = (int)__builtin_bit_cast(unsigned short, sc);
-      const int nb = __builtin_amdgcn_update_dpp(0, scb, 0x138, 0xf, 0xf, false);   // wave_shr:1
-      carry = __builtin_bit_cast(_Float16, (unsigned short)nb);
+      if (s + 1 < SIDE + 2) {
+        // hand the partial sum to the next member (lane + 1)
+        const int scb = (int)__builtin_bit_cast(unsigned short, sc);
+        const int nb = __builtin_amdgcn_update_dpp(0, scb, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        carry = __builtin_bit_cast(_Float16, (unsigned short)nb);
+      }
     }
-    // merge the 7 columns in column order: larger score, the smaller column
-    // on a tie (only a column that beat the carried maximum has best_j >= 0)
-    const int mine = ((int)__builtin_bit_cast(unsigned short, best) << 8) | (best_j & 0xff);
-    _Float16 lbest = max_score;
-    int lt = -1, lj = -1;
+    // merge the 7 columns (member-2 lanes, 3 apart): larger score, the
+    // smaller column on a tie (a column with best_j >= 0 beat the carried
+    // maximum); a tree over columns t, t+1 | t+2 | t+4, then lane t = 0's
+    // result to the query's 21 lanes.  key = score bits << 16 | j << 8 | t
+    int key = ((int)__builtin_bit_cast(unsigned short, best) << 16) | ((best_j & 0xff) << 8) | t;
 #pragma unroll
-    for (int tt = 0; tt < SIDE; ++tt) {
-      const int o = __shfl(mine, base + 3 * tt + 2, 64);
-      const int oj = (int)(signed char)(o & 0xff);
-      const _Float16 os = __builtin_bit_cast(_Float16, (unsigned short)((o >> 8) & 0xffff));
-      if (oj >= 0 && os > lbest) {
-        lbest = os;
-        lt = tt;
-        lj = oj;
-      }
+    for (int k = 1; k < SIDE; k <<= 1) {
+      const int o = __shfl_down(key, 3 * k, 64);
+      const int oj = (int)(signed char)((o >> 8) & 0xff);
+      const int kj = (int)(signed char)((key >> 8) & 0xff);
+      const _Float16 os = __builtin_bit_cast(_Float16, (unsigned short)((o >> 16) & 0xffff));
+      const _Float16 ks = __builtin_bit_cast(_Float16, (unsigned short)((key >> 16) & 0xffff));
+      if (t + k < SIDE && oj >= 0 && (kj < 0 || os > ks)) key = o;
     }
-    if (lt >= 0) {
-      max_score = lbest;
-      u_new = ub + (int64_t)lt * d;
-      v_new = vb + (int64_t)lj * d;
+    key = __shfl(key, base + 2, 64);
+    const int lj = (int)(signed char)((key >> 8) & 0xff);
+    if (lj >= 0) {
+      max_score = __builtin_bit_cast(_Float16, (unsigned short)((key >> 16) & 0xffff));
+      u_new = ub + (key & 0xff) * d;
+      v_new = vb + lj * d;
     }
     u0 = u_new;
     v0 = v_new;
@@ -738,7 +754,8 @@ int s3m_iter_proj(const float* rays_img_with_grad, const float* pts_3d_norm,
 }
 
 // lanes per query point of the refine: 1, 2 or 4 (k_refine_lane, radius 3,
-// F = 24) or 8 / 16 / 32 / 64 (k_refine_coop; 16 is the default), and the
+// F = 24), 3 (k_refine_px, radius 3, F = 24: 3 lanes per window pixel, the
+// default) or 8 / 16 / 32 / 64 (k_refine_coop), and the
 // lane kernel's load distance in candidates (2, 3, 4 or 6); tuning hooks for
 // A/B runs.  The per-lane kernel wins when neighbouring query points have
 // neighbouring windows (129 vs 173 us at C2 on a clean 2-px shift,
@@ -747,7 +764,10 @@ int s3m_iter_proj(const float* rays_img_with_grad, const float* pts_3d_norm,
 // every other call: tools/refine_stats.py), its lanes touch one cache line
 // each and the 16-lane kernel is faster (185 vs 208 us per call,
 // profiles/r04g_summary.txt)
-constexpr int kRefineLanesDefault = 16;
+// round 6: the pixel-major kernel (3 lanes per pixel, k_refine_px) is the
+// default: 161-180 vs 176-197 us on the tracking loop's inputs
+// (profiles/r06e_refine_px.log)
+constexpr int kRefineLanesDefault = 3;
 // window-centre binning: 0 = off (pixel order), else 16 sx + sy for
 // 2^sx x 2^sy pixel tiles (k_refine_bin)
 constexpr int kRefineSortDefault = 0;

@@ -30,6 +30,8 @@ SIGNATURES: dict[str, tuple] = {
     "s3_last_error": (ctypes.c_char_p, []),
     "s3_abi_version": (I32, []),
     "s3_arch": (ctypes.c_char_p, []),
+    "s3_stream_create": (I32, [I32, I32, ctypes.POINTER(P)]),
+    "s3_stream_destroy": (I32, [P]),
     # s3lie.h
     "s3lie_sim3_mul": (I32, [P, I64, P, I64, P, I64, P]),
     "s3lie_sim3_inv": (I32, [P, P, I64, P]),
@@ -143,6 +145,64 @@ def wait_event(ev) -> None:
             return
         if _SPIN_YIELD:
             time.sleep(0)
+
+
+# The frame loop's streams.  HIP gives every new stream
+# a hardware queue when it is created -- its own while fewer than
+# GPU_MAX_HW_QUEUES (4 on the box) queues of that priority exist, a shared
+# one after -- and a queue runs the work of the streams on it in one order.
+# torch's pooled streams (torch.cuda.Stream) are created 32 at a time on
+# first use and handed out round-robin, so which frame-loop stream shared a
+# queue with which (the encoder's 13-ms batch replays with the aux stream or
+# the default stream behind the main chain's per-step wait) depended on how
+# many streams the process had taken before.  These streams are created by
+# the library instead, once per device, in this fixed order and ahead of
+# torch's pool when reserve_frame_streams() runs first (bench.py does): the
+# process's default stream, the encoder, the aux stream (world records,
+# read-backs) and the backend worker hold the 4 normal-priority queues, the
+# main chain the high-priority one.
+FRAME_STREAM_ROLES = (("encoder", 0), ("aux", 0), ("backend", 0), ("main", -1))
+_FRAME_STREAMS: dict = {}
+_FRAME_ORDER: list = []        # (device index, role, priority) in creation order
+
+
+def _make_stream(dev: torch.device, priority: int):
+    """A dedicated non-blocking HIP stream (s3_stream_create) as a torch stream."""
+    h = P()
+    check(lib().s3_stream_create(int(dev.index), int(priority), ctypes.byref(h)),
+          "s3_stream_create")
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
+def _dev(device) -> torch.device:
+    dev = torch.device(device if device is not None else "cuda")
+    return dev if dev.index is not None else torch.device("cuda", torch.cuda.current_device())
+
+
+def reserve_frame_streams(device=None) -> None:
+    """Create the frame loop's streams of `device` (FRAME_STREAM_ROLES order)
+    if they do not exist yet."""
+    dev = _dev(device)
+    for role, prio in FRAME_STREAM_ROLES:
+        frame_stream(dev, role, prio, _reserve=False)
+
+
+def frame_stream(device, role: str, priority: int = 0, _reserve: bool = True):
+    """The process's dedicated stream for (device, role, priority); the
+    standard set is created first (reserve_frame_streams) so its creation
+    order never depends on the caller's."""
+    dev = _dev(device)
+    if _reserve and not any(k[0] == dev.index for k in _FRAME_STREAMS):
+        reserve_frame_streams(dev)
+    key = (dev.index, role, int(priority))
+    s = _FRAME_STREAMS.get(key)
+    if s is None:
+        with _lock:
+            s = _FRAME_STREAMS.get(key)
+            if s is None:
+                s = _FRAME_STREAMS[key] = _make_stream(dev, int(priority))
+                _FRAME_ORDER.append(key)
+    return s
 
 
 def stream(device: torch.device | None = None) -> int:

@@ -178,8 +178,8 @@ class Backend:
         frontend."""
         self._q = queue.Queue()
         if self.device.type == "cuda":
-            self._stream = torch.cuda.Stream(device=self.device,
-                                             priority=worker_stream_priority())
+            from splatt3r_amd import _lib
+            self._stream = _lib.frame_stream(self.device, "backend", worker_stream_priority())
         self._thread = threading.Thread(target=self._loop, daemon=True)
         self._thread.start()
 

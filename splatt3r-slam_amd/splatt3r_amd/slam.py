@@ -38,6 +38,7 @@ import types
 import torch
 
 import lietorch
+from splatt3r_amd import _lib
 from splatt3r_amd.config import config
 from splatt3r_amd.frame import Frame, Keyframes, Mode, create_frame
 from splatt3r_amd.gaussian_map import SharedGaussians, should_append_gaussians
@@ -48,21 +49,16 @@ from splatt3r_amd.tracker import FrameTracker
 __all__ = ["Frontend", "should_append_gaussians", "lookahead_batches"]
 
 
-_STREAMS: dict = {}
-
-
 def _shared_stream(device, priority, role):
     """One HIP stream per (device, priority, role) for the whole process:
     Frontends created one after another (bench legs, tests) reuse the same
     streams instead of creating two or three more each; every new stream is
     mapped onto one of the process's few hardware queues (GPU_MAX_HW_QUEUES),
     and a frontend whose streams came late in that assignment ran its
-    frames ~1.6x slower (tools/live_ab.py, profiles/r04k_live_ab.log)."""
-    key = (str(torch.device(device)), int(priority), role)
-    s = _STREAMS.get(key)
-    if s is None:
-        s = _STREAMS[key] = torch.cuda.Stream(device=device, priority=int(priority))
-    return s
+    frames ~1.6x slower (tools/live_ab.py, profiles/r04k_live_ab.log).  The
+    streams are the library's dedicated ones (_lib.frame_stream: created in
+    a fixed order, each on a hardware queue of its own), not torch's pool."""
+    return _lib.frame_stream(device, role, int(priority))
 
 
 def _clear_ahead_slot(model):

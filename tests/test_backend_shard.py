@@ -292,28 +292,31 @@ def test_slam_with_sharded_backend_equals_single_rank_on_gpu():
 def test_backend_worker_stream_is_lowest_priority(monkeypatch):
     """The backend worker's HIP stream takes the lowest priority the device
     offers (torch's range is (lowest, highest)): the frontend's high-priority
-    main chain and its encoder keep their rate while keyframe tasks drain."""
+    main chain and its encoder keep their rate while keyframe tasks drain.
+    It is the library's dedicated "backend" stream (_lib.frame_stream)."""
+    from splatt3r_amd import _lib
     from splatt3r_amd import backend as B
     assert B.worker_stream_priority((0, -1)) == 0
     assert B.worker_stream_priority((0, -5)) == 0
-    made = {}
+    made = []
 
     class FakeStream:
-        def __init__(self, device=None, priority=0):
-            made.update(device=device, priority=priority)
-
         @staticmethod
         def priority_range():
             return (0, -3)
 
     monkeypatch.setattr(B.torch.cuda, "Stream", FakeStream)
     monkeypatch.setattr(B.torch.cuda, "set_device", lambda d: None)
+    monkeypatch.setattr(_lib, "_FRAME_STREAMS", {})
+    monkeypatch.setattr(_lib, "_FRAME_ORDER", [])
+    monkeypatch.setattr(_lib, "_make_stream", lambda dev, prio: made.append(prio) or object())
     be = B.Backend.__new__(B.Backend)          # no retrieval database / factor graph needed
     be.device = torch.device("cuda", 0)
     be._q = be._thread = be._stream = be._err = None
     be.start_worker()
     try:
-        assert made == {"device": torch.device("cuda", 0), "priority": 0}
+        assert be._stream is _lib._FRAME_STREAMS[(0, "backend", 0)]
+        assert (0, "backend", 0) in _lib._FRAME_ORDER
     finally:
         be._q.put(None)
         be._thread.join(timeout=30)

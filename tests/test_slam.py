@@ -642,3 +642,35 @@ def test_readback_copy_waits_on_the_render_event_on_the_aux_stream(monkeypatch):
     log.clear()
     fe._deliver_image(img, 1, "gs")
     assert log[0][:2] == ("main", "record") and log[1] == ("aux", "wait_event", log[0][2])
+
+
+def test_frame_streams_are_created_in_a_fixed_order(monkeypatch):
+    """The frame loop's streams come from the library
+    (_lib.frame_stream), created once per device in FRAME_STREAM_ROLES order
+    -- encoder, aux, backend at normal priority, then the main chain at high
+    priority -- whichever role a caller asks for first, so each holds a
+    hardware queue of its own (GPU_MAX_HW_QUEUES = 4 normal-priority queues:
+    the default stream + these three).  Frontend / Backend streams go
+    through it (slam._shared_stream)."""
+    import torch
+    from splatt3r_amd import _lib, slam
+    made = []
+    monkeypatch.setattr(_lib, "_FRAME_STREAMS", {})
+    monkeypatch.setattr(_lib, "_FRAME_ORDER", [])
+    monkeypatch.setattr(_lib, "_make_stream",
+                        lambda dev, prio: made.append((dev.index, prio)) or ("stream", dev.index,
+                                                                            len(made)))
+    dev = torch.device("cuda", 0)
+    s_main = slam._shared_stream(dev, -1, "main")            # asked for first
+    assert [k[1:] for k in _lib._FRAME_ORDER] == [("encoder", 0), ("aux", 0), ("backend", 0),
+                                                   ("main", -1)]
+    assert made == [(0, 0), (0, 0), (0, 0), (0, -1)]
+    assert s_main == ("stream", 0, 4)
+    assert slam._shared_stream(dev, 0, "encoder") == ("stream", 0, 1)   # cached, same object
+    assert slam._shared_stream(dev, 0, "aux") == ("stream", 0, 2)
+    # another priority for a role (--main-priority 0) is a new stream after the set
+    assert slam._shared_stream(dev, 0, "main") == ("stream", 0, 5)
+    # a second device gets its own set, in the same order
+    _lib.frame_stream(torch.device("cuda", 1), "aux")
+    assert [k for k in _lib._FRAME_ORDER if k[0] == 1] == [
+        (1, "encoder", 0), (1, "aux", 0), (1, "backend", 0), (1, "main", -1)]
