@@ -41,6 +41,18 @@ __device__ __forceinline__ float wave_reduce_scatter(const float (&acc)[N]) {
   return v[0];
 }
 
+// The barrier of an LDS-DMA ring (buffer_load ... lds into stages the waves
+// read with ds_read).  s_barrier alone does not wait for this wave's LDS
+// reads: one still in flight at the barrier could be overtaken by another
+// wave's DMA refill of the same stage issued just after it (a rare, timing-
+// dependent corruption of a few operands).  Drain them first.  One asm
+// statement with a memory clobber also keeps the compiler from moving LDS
+// reads across the barrier either way (__builtin_amdgcn_s_barrier is
+// modelled as touching no memory).
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 }  // namespace s3
 
 // Validate an argument; on failure record the message and return S3_ERR_INVALID.

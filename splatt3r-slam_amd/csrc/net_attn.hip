@@ -375,7 +375,7 @@ __global__ void __launch_bounds__(kThreads) k_attn_dma(AttnP p) {
     if (i < NT) issue(i, i);
   for (int t = 0; t < NT; ++t) {
     wait_tiles<4, AHEAD - 1>(NT - 1 - t);
-    __builtin_amdgcn_s_barrier();
+    s3::ring_barrier();
     if (t + AHEAD < NT) issue(t + AHEAD, (t + AHEAD) % kStages);
     const f16* Ks = smem + (t % kStages) * 2 * KT * D;
     const f16* Vs = Ks + KT * D;
@@ -555,7 +555,7 @@ __global__ void __launch_bounds__(64 * QW * SPLIT) k_attn_st(AttnP p) {
     if (i < NTs) issue(i, i);
   for (int i = 0; i < NTmax; ++i) {
     if (i < NTs) wait_tiles<2 * NJ, AHEAD - 1>(NTs - 1 - i);
-    __builtin_amdgcn_s_barrier();
+    s3::ring_barrier();
     if (i >= NTs) continue;
     if (i + AHEAD < NTs) issue(i + AHEAD, (i + AHEAD) % STAGES);
     const int t = i * SPLIT + sp;

@@ -834,7 +834,7 @@ k_gemm(GemmP p) {
     if (kt < KT) wait_tiles<PERW, AHEAD - 1>(KT - 1 - kt);
     // Everyone's DMA for tile kt is visible, and everyone finished reading
     // the stage that tile kt+AHEAD overwrites (read during iteration kt-1).
-    __builtin_amdgcn_s_barrier();
+    s3::ring_barrier();
     if (kt >= KT) continue;
     const f16* As = ring + (kt % kStages) * STAGE;
     const f16* Bs = As + BM * BK;

@@ -123,14 +123,14 @@ __global__ void __launch_bounds__(64 * NWM * NWN, S == 1 ? 2 : 1) k_conv3_halo(G
   for (int ss = 0; ss < SSn; ++ss) {
     if constexpr (S == 1) {
       if (ss > 0) {
-        __builtin_amdgcn_s_barrier();   // every wave is done reading the stage
+        s3::ring_barrier();   // every wave is done reading the stage
         issue(ss, 0);
       }
     }
     // this super-step's DMA (the only one outstanding) has landed, and every
     // wave is done reading the stage the next one overwrites
     wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
+    s3::ring_barrier();
     if constexpr (S == 2)
       if (ss + 1 < SSn) issue(ss + 1, (ss + 1) & 1);
     const f16* As = smem + (S == 2 ? (ss & 1) : 0) * STAGE;

@@ -19,8 +19,6 @@
 
 namespace {
 
-__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
 template <int BM, int BN, int NWM, int NWN, int AMODE, int S, int MF>
 __global__ void __launch_bounds__(64 * NWM * NWN, lds_waves_per_simd(BM, BN, NWM * NWN, S, 64))
 k_gemm_pp(GemmP p) {
@@ -201,7 +199,7 @@ k_gemm_pp(GemmP p) {
     if (i < KT) issue(kt_begin + i, i);
   if (KT > 0) {
     wait_tiles<PERW, S - 1>(KT - 1);
-    __builtin_amdgcn_s_barrier();
+    s3::ring_barrier();
     read_half(0, 0, ra0, rb0);
   }
   for (int kt = 0; kt < KT; ++kt) {
@@ -213,9 +211,7 @@ k_gemm_pp(GemmP p) {
       // flight), own reads of stage st retired; after the barrier everyone's
       // are, so stage st takes tile kt+S and tile kt+1 is readable
       wait_tiles<PERW, S - 2>(KT - 2 - kt);
-      lgkm_wait0();
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
+      s3::ring_barrier();
       if (kt + S < KT) issue(kt_begin + kt + S, st);
       read_half((kt + 1) % S, 0, ra0, rb0);
     }

@@ -162,7 +162,7 @@ k_gemm_bd(GemmP p) {
     // stay in flight); after the barrier every wave's A of tile kt is
     // visible and the stage tile kt + AHEAD refills is no longer read
     wait_vmcnt<PERW * (AHEAD - 1)>();
-    __builtin_amdgcn_s_barrier();
+    s3::ring_barrier();
     const bool live = kt < KT;
     f16x8 af[NKS][FM];
     if (live) {

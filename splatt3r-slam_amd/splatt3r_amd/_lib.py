@@ -164,10 +164,19 @@ def wait_event(ev) -> None:
 FRAME_STREAM_ROLES = (("encoder", 0), ("aux", 0), ("backend", 0), ("main", -1))
 _FRAME_STREAMS: dict = {}
 _FRAME_ORDER: list = []        # (device index, role, priority) in creation order
+# guards the stream table (not _lock: creating a stream may load the library,
+# which takes _lock)
+_STREAM_LOCK = threading.Lock()
+
+
+# S3_FRAME_STREAMS=0: torch's pooled streams instead (A/B diagnostic)
+FRAME_STREAMS_DEDICATED = os.environ.get("S3_FRAME_STREAMS", "1") != "0"
 
 
 def _make_stream(dev: torch.device, priority: int):
     """A dedicated non-blocking HIP stream (s3_stream_create) as a torch stream."""
+    if not FRAME_STREAMS_DEDICATED:
+        return torch.cuda.Stream(device=dev, priority=int(priority))
     h = P()
     check(lib().s3_stream_create(int(dev.index), int(priority), ctypes.byref(h)),
           "s3_stream_create")
@@ -197,7 +206,7 @@ def frame_stream(device, role: str, priority: int = 0, _reserve: bool = True):
     key = (dev.index, role, int(priority))
     s = _FRAME_STREAMS.get(key)
     if s is None:
-        with _lock:
+        with _STREAM_LOCK:
             s = _FRAME_STREAMS.get(key)
             if s is None:
                 s = _FRAME_STREAMS[key] = _make_stream(dev, int(priority))

@@ -615,7 +615,7 @@ class Splatt3RNet:
             # plan buffers are ordinary tensors even when the first call
             # comes from inside torch.inference_mode (they are re-filled
             # in place by later calls made outside it)
-            with torch.inference_mode(False):
+            with torch.inference_mode(False), ops.plan_scope("enc"):
                 ep = EncoderPlan(self, B, H, W)
             if self._capture_here():
                 ep.plan.capture()
@@ -632,7 +632,7 @@ class Splatt3RNet:
         tracker would."""
         key = (Bp, H, W, keep_tokens, tag)
         if key not in self._pair:
-            with torch.inference_mode(False):
+            with torch.inference_mode(False), ops.plan_scope("pair"):
                 pp = PairPlan(self, Bp, H, W, keep_tokens,
                               batch_invariant=tag in (None, "backend"))
             if self._capture_here() and not keep_tokens:

@@ -7,6 +7,7 @@ into a HIP graph.  No op has a torch fallback.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import Sequence
@@ -281,6 +282,20 @@ if os.environ.get("S3_GEMM_HALO", "1") == "0":
 # S3_GEMM_BDIRECT=0: leave the B-direct tiles out of the tuner (A/B)
 if os.environ.get("S3_GEMM_BDIRECT", "1") == "0":
     _EXCLUDED |= _BDIRECT
+# S3_GEMM_BDIRECT_OFF=enc,pair: no packed B (so no B-direct tile) for the
+# GEMMs of the plans built in those scopes (plan_scope; diagnostic A/B)
+_BD_OFF = set(filter(None, os.environ.get("S3_GEMM_BDIRECT_OFF", "").split(",")))
+_SCOPE = [None]
+
+
+@contextlib.contextmanager
+def plan_scope(name):
+    """Name the plan being built (net.py: "enc" / "pair") for S3_GEMM_BDIRECT_OFF."""
+    prev, _SCOPE[0] = _SCOPE[0], name
+    try:
+        yield
+    finally:
+        _SCOPE[0] = prev
 
 
 def _db_digest() -> str:
@@ -521,7 +536,14 @@ def packed_b(B) -> torch.Tensor | None:
     KiB, N padded with zero rows.  Built once per weight and kept on the
     tensor that owns the storage (a stacked group weight for its group
     views), so it lives exactly as long as the weights.  None when B is not
-    such a tensor (raw pointer, other dtype / layout, K % 32 != 0)."""
+    such a tensor (raw pointer, other dtype / layout, K % 32 != 0).
+
+    The copy is written on the stream current at plan-build time while the
+    plan may launch on any other (the decode-ahead pair replay is built on
+    one frame-loop stream and replayed on another), so the build waits for
+    its stream once: the packed weights are then complete before any
+    launch, whatever stream it is on.  Never built during graph capture
+    (the copy would become a graph node over the graph pool): None then."""
     if not isinstance(B, torch.Tensor) or B.dtype != torch.float16 or B.dim() != 2 or not B.is_cuda:
         return None
     N, K = B.shape
@@ -532,9 +554,12 @@ def packed_b(B) -> torch.Tensor | None:
     key = (B.storage_offset(), N, K, B._version)
     P_ = cache.get(key)
     if P_ is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
         Np = -(-N // 16) * 16
         Bz = B if Np == N else torch.cat([B, B.new_zeros(Np - N, K)])
         P_ = Bz.reshape(Np // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+        torch.cuda.current_stream(B.device).synchronize()
         cache[key] = P_
     return P_
 
@@ -566,7 +591,7 @@ def gemm(A, B, C, M, N, K, *, lda, ldb=None, ldc=None, bias=None, act="none", R1
     a.ldb = int(ldb if ldb is not None else K)
     # packed weights for the B-direct tiles (dense A only; every group or none)
     bpk = None
-    if conv is None and tail is None and a.ldb == K:
+    if conv is None and tail is None and a.ldb == K and _SCOPE[0] not in _BD_OFF:
         bpk = [packed_b(b) for b in B]
         if any(x is None for x in bpk):
             bpk = None

@@ -368,3 +368,70 @@ def test_portrait_true_shape_vs_reference_golden(parity):
         _check(parity, f"portrait_res2_{k}", r2[k], g["res2_" + k], TOL["head"])
     with pytest.raises(AssertionError, match="landscape"):
         net._encode_image(torch.zeros(1, 3, 64, 48, device="cuda"), None)
+
+
+def _class_equality(plans, max_calls=None):
+    """Every launch configuration of a GEMM call's reduction class computes
+    the same bits as the configuration the plan chose, on the call's own
+    operands and epilogue (bias, activation, in-place residual, RoPE, fused
+    tail, scatter store).  Returns [(call desc, tile, split)] mismatches and
+    the number of (call, candidate) pairs compared."""
+    import ctypes
+    from splatt3r_amd import _lib, ops
+    L = _lib.lib()
+    st = _lib.stream()
+    bad, n = [], 0
+    calls = [c for pl in plans for c in pl.calls if getattr(c, "kind", "").startswith("gemm")]
+    seen = set()
+    for c in calls[:max_calls]:
+        a = c.keep[0]
+        if a.split_k > 1 or (a.tile, ops._tune_key(a)) in seen:
+            continue
+        seen.add((a.tile, ops._tune_key(a)))
+        outs = [t for t in c.keep[3] if isinstance(t, torch.Tensor)]
+        if a.C2[0]:
+            outs += [t for t in c.keep[7] if isinstance(t, torch.Tensor)]
+        if c.keep[11] is not None:
+            outs += [t for t in c.keep[11][2] if isinstance(t, torch.Tensor)]
+        snap = [t.clone() for t in outs]
+
+        def run(tile):
+            for t, s in zip(outs, snap):
+                t.copy_(s)
+            x = ops.GemmArgs.from_buffer_copy(a)
+            x.tile, x.split_k = tile, 1
+            if L.s3n_gemm(ctypes.byref(x), st) != 0:
+                return None
+            torch.cuda.synchronize()
+            return [t.clone() for t in outs]
+
+        want = run(a.tile)
+        for tile, sk in ops._tune_candidates(a, False, like=(a.tile, 1)):
+            if tile == a.tile or sk != 1:
+                continue
+            got = run(tile)
+            if got is None:
+                continue
+            n += 1
+            if not all(torch.equal(x, y) for x, y in zip(got, want)):
+                bad.append((c.desc, tile, sk))
+        for t, s in zip(outs, snap):
+            t.copy_(s)
+    return bad, n
+
+
+@pytest.mark.gpu
+def test_every_tile_of_a_reduction_class_gives_the_same_bits_on_the_network_gemms():
+    """The premise of the batch-invariant plans (ops.reduction_class): on the
+    network's own GEMM calls -- the encoder, decoder and head plans at full
+    size, with their real epilogues -- every tile of the class the plan chose
+    (the B-direct tiles 70-77 included) reproduces the chosen tile's output
+    bit for bit."""
+    from splatt3r_amd import weights as W
+    from splatt3r_amd.net import Splatt3RNet
+    net = Splatt3RNet(W.FULL, seed=1234)
+    ep = net.encoder_plan(1, 384, 512)
+    pp = net.pair_plan(1, 384, 512)
+    bad, n = _class_equality([ep.plan, pp.decoder_plan, pp.head_plan])
+    assert n > 50, n
+    assert not bad, bad[:20]

@@ -172,7 +172,7 @@ def test_gemm_bdirect_tiles_bitexact_vs_same_reduction_class(bd, ref, M, N, K, g
         assert rel_err(outs[0][0][g], ref_) < 2e-3
 
 
-@pytest.mark.parametrize("tile", [70, 74])
+@pytest.mark.parametrize("tile", [70, 71, 72, 73, 74, 75, 76, 77])
 def test_gemm_bdirect_rope_and_scatter_epilogues(tile):
     """The B-direct tiles share the LDS-staged epilogue: the fused RoPE2D
     columns and the ConvTranspose scatter store equal tile 32's bits."""

@@ -674,3 +674,25 @@ def test_frame_streams_are_created_in_a_fixed_order(monkeypatch):
     _lib.frame_stream(torch.device("cuda", 1), "aux")
     assert [k for k in _lib._FRAME_ORDER if k[0] == 1] == [
         (1, "encoder", 0), (1, "aux", 0), (1, "backend", 0), (1, "main", -1)]
+
+
+def test_first_frame_stream_loads_the_library_without_deadlock(monkeypatch):
+    """bench.py reserves the frame streams before anything else has loaded
+    the native library: creating the first stream then loads it from inside
+    the stream table's critical section.  The table has its own lock (the
+    library loader's is not reentrant), so this returns instead of hanging
+    (the r06 bench sat silent in reserve_frame_streams until killed)."""
+    import threading
+    import torch
+    from splatt3r_amd import _lib
+    monkeypatch.setattr(_lib, "_FRAME_STREAMS", {})
+    monkeypatch.setattr(_lib, "_FRAME_ORDER", [])
+    monkeypatch.setattr(_lib, "_lib", None)        # not loaded yet
+    monkeypatch.setattr(_lib, "_make_stream", lambda dev, prio: (_lib.lib(), ("stream", prio))[1])
+    t = threading.Thread(target=_lib.reserve_frame_streams, args=(torch.device("cuda", 0),),
+                         daemon=True)
+    t.start()
+    t.join(timeout=30)
+    assert not t.is_alive(), "reserve_frame_streams deadlocked loading the library"
+    assert len(_lib._FRAME_ORDER) == len(_lib.FRAME_STREAM_ROLES)
+    assert _lib._lib is not None
