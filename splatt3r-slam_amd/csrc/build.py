@@ -28,6 +28,23 @@ ARCH = os.environ.get("S3_OFFLOAD_ARCH", "gfx950")
 
 STRICT = ["-ffp-contract=off"]
 FAST = ["-ffp-contract=fast"]
+# No packed-FP32 VALU instructions (v_pk_{mul,add,fma}_f32) in any kernel.
+# On the MI355X boxes they return wrong values while MFMA instructions of
+# another kernel run on the same CU: a concurrent GEMM on another stream --
+# ours or hipBLASLt's -- corrupted 30-93 % of the matching kernels' launches
+# (tools/stress_bd_concurrency.py, profiles/r06_packed_fp32_mfma.log); built
+# without them, 0 of ~160k.  The results are the same IEEE values (each
+# packed op is two scalar ops; contraction is set per file above).
+# S3_PACKED_FP32=1 builds the packed variant beside it (_pk suffix, A/B only).
+NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+_VARIANT = "_pk" if os.environ.get("S3_PACKED_FP32", "0") == "1" else ""
+OBJ_DIR += _VARIANT
+LIB_NAME = LIB_NAME.replace(".so", _VARIANT + ".so")
+
+
+def device_flags(src: str) -> list[str]:
+    """Every compile flag of `src` beyond the common ones (tests use it)."""
+    return SOURCES[src] + ([] if _VARIANT else NO_PACKED_FP32)
 
 # source file -> extra flags
 SOURCES = {
@@ -74,15 +91,20 @@ def _headers_mtime() -> float:
 def _compile(src: str, flags: list[str], force: bool, hdr_mtime: float) -> str:
     path = os.path.join(HERE, src)
     obj = os.path.join(OBJ_DIR, src.replace(".hip", ".o"))
-    if (not force and os.path.exists(obj)
-            and os.path.getmtime(obj) >= max(os.path.getmtime(path), hdr_mtime)):
-        return obj
     cmd = [hipcc(), "-c", path, "-o", obj, "-fPIC", "-O3", "-std=c++17",
            f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", HERE,
-           "-Wno-unused-result", "-munsafe-fp-atomics"] + flags
+           "-Wno-unused-result", "-munsafe-fp-atomics"] + flags + ([] if _VARIANT else NO_PACKED_FP32)
+    # the command is stamped beside the object: a flag change rebuilds it
+    stamp = obj + ".cmd"
+    same_cmd = os.path.exists(stamp) and open(stamp).read() == " ".join(cmd[1:])
+    if (not force and same_cmd and os.path.exists(obj)
+            and os.path.getmtime(obj) >= max(os.path.getmtime(path), hdr_mtime)):
+        return obj
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    with open(stamp, "w") as f:
+        f.write(" ".join(cmd[1:]))
     return obj
 
 

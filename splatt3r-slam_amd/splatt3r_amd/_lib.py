@@ -17,6 +17,10 @@ import torch  # noqa: F401  (must be loaded before the HIP library, see above)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_native", "libsplatt3r_hip.so")
+# S3_LIB_VARIANT=_pk: the library built with S3_PACKED_FP32=1 (packed-FP32
+# instructions allowed; A/B runs only, see csrc/build.py)
+if os.environ.get("S3_LIB_VARIANT"):
+    LIB_PATH = LIB_PATH.replace(".so", os.environ["S3_LIB_VARIANT"] + ".so")
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int

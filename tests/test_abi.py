@@ -122,3 +122,43 @@ def test_gemm_args_layout_matches_the_c_header():
                                                        check=True).stdout.split())
     assert ctypes.sizeof(ops.GemmArgs) == size
     assert ops.GemmArgs.Bp.offset == bp and ops.GemmArgs.ld_tail.offset == ldt
+
+
+def test_shipped_library_has_no_packed_fp32_instructions(tmp_path):
+    """Every kernel is built without v_pk_{mul,add,fma}_f32 (csrc/build.py
+    NO_PACKED_FP32): on the MI355X boxes those return wrong values while
+    MFMAs of another kernel run on the same CU (a GEMM on another stream
+    corrupted 30-93 % of the matching kernels' launches,
+    tools/stress_bd_concurrency.py).  Checked on the library that ships:
+    every device bundle of its .hip_fatbin section is disassembled."""
+    import shutil
+    import subprocess
+    import pytest
+    llvm = "/opt/rocm/lib/llvm/bin"
+    tools = [os.path.join(llvm, t) for t in ("llvm-objcopy", "clang-offload-bundler",
+                                              "llvm-objdump")]
+    if not all(os.path.exists(t) for t in tools):
+        pytest.skip("ROCm LLVM tools not found")
+    lib = os.path.join(REPO, "splatt3r-slam_amd", "splatt3r_amd", "_native", "libsplatt3r_hip.so")
+    fat = tmp_path / "fatbin.bin"
+    subprocess.run([tools[0], f"--dump-section=.hip_fatbin={fat}", lib, str(tmp_path / "copy.so")],
+                   check=True, capture_output=True)
+    blob = fat.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    offs = [m.start() for m in re.finditer(re.escape(magic), blob)]
+    assert len(offs) >= 10, offs
+    packed, disassembled = 0, 0
+    for k, o in enumerate(offs):
+        part = tmp_path / f"b{k}.bin"
+        part.write_bytes(blob[o:offs[k + 1] if k + 1 < len(offs) else len(blob)])
+        co = tmp_path / f"d{k}.co"
+        r = subprocess.run([tools[1], "--unbundle", "--type=o",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={part}",
+                            f"--output={co}"], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        d = subprocess.run([tools[2], "-d", str(co)], capture_output=True, text=True).stdout
+        disassembled += d.count("\n")
+        packed += len(re.findall(r"\bv_pk_(?:mul|add|fma)_f32", d))
+    shutil.rmtree(tmp_path, ignore_errors=True)
+    assert disassembled > 100000
+    assert packed == 0

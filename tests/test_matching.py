@@ -289,3 +289,54 @@ def test_backends_reject_non_contiguous():
     pts = torch.zeros(1, 3, 64, device="cuda").transpose(1, 2)
     with pytest.raises(RuntimeError, match="contiguous"):
         be.iter_proj(rays, pts, torch.zeros(1, 64, 2, device="cuda"), 10, 1e-8, 1e-6)
+
+
+@pytest.mark.gpu
+def test_matching_is_exact_while_a_gemm_runs_on_another_stream():
+    """The frame loop overlaps the encoder's GEMMs (side stream) with the
+    tracker's matching (main stream).  Packed-FP32 VALU instructions return
+    wrong values while MFMAs of another kernel share the CU (csrc/build.py
+    NO_PACKED_FP32): with them, 30-93 % of the matching launches overlapped
+    by a GEMM came out different (tools/stress_bd_concurrency.py).  Here a
+    library GEMM replays on a side stream while the dense matching runs
+    again and again on the main stream: every result must equal the result
+    on an idle device, bit for bit."""
+    import time
+    from splatt3r_amd import _lib, ops
+    from splatt3r_amd.matching import match
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    h, w = 384, 512
+    yy, xx = torch.meshgrid(torch.arange(h, device=dev, dtype=torch.float32),
+                            torch.arange(w, device=dev, dtype=torch.float32), indexing="ij")
+    X11 = torch.stack((xx / w - 0.5, yy / h - 0.5, torch.ones_like(xx)), -1)[None]
+    X21 = X11 + 0.002 * torch.randn(X11.shape, device=dev, generator=g)
+    D11 = torch.randn(1, h, w, 24, device=dev, generator=g).half()
+    D21 = D11 + 0.05 * torch.randn(D11.shape, device=dev, generator=g).half()
+    M, N, K = 1536, 4096, 1024
+    A = torch.randn(M, K, device=dev, generator=g).half()
+    Bw = torch.randn(N, K, device=dev, generator=g).half() * 0.03
+    C = torch.empty(M, N, device=dev).half()
+    gemm = ops.gemm([A], [Bw], [C], M, N, K, lda=K, bias=[torch.zeros(N, device=dev)],
+                    act="gelu", tile=25, split_k=1)
+    torch.cuda.synchronize()
+    ref = match(X11, X21, D11, D21)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream(device=dev)
+    outs = []
+    t_end = time.time() + 3.0
+    while time.time() < t_end:
+        with torch.cuda.stream(side):
+            for _ in range(16):
+                gemm(_lib.stream(dev))
+        for _ in range(8):
+            outs.append(match(X11, X21, D11, D21))
+        if len(outs) >= 64:
+            torch.cuda.synchronize()
+            bad = sum(not (torch.equal(i, ref[0]) and torch.equal(v, ref[1])) for i, v in outs)
+            assert bad == 0, f"{bad} of {len(outs)} overlapped matching calls differ"
+            outs = []
+    torch.cuda.synchronize()
+    bad = sum(not (torch.equal(i, ref[0]) and torch.equal(v, ref[1])) for i, v in outs)
+    assert bad == 0, f"{bad} of {len(outs)} overlapped matching calls differ"

@@ -38,6 +38,14 @@ def make_side(dev, g):
             c = a @ b
             (c * 0.5 + 1.0).relu_()
         return kind, run
+    if kind == "torchs":
+        a = torch.randn(1536, 1024, device=dev, generator=g).half()
+        b = torch.randn(1024, 4096, device=dev, generator=g).half() * 0.03
+
+        def run():
+            for _ in range(8):
+                torch.nn.functional.gelu(a @ b)
+        return kind, run
     if kind.startswith("gemm"):
         from splatt3r_amd import _lib, ops
         tile = int(kind[4:])
@@ -78,9 +86,58 @@ def main():
     victim = os.environ.get("STRESS_VICTIM", "match")
     xv = torch.randn(1 << 23, device=dev, generator=g)
 
+    # fixed inputs of each matching stage (victim = stage_<name>)
+    from splatt3r_amd import _lib
+    from splatt3r_amd.config import config
+    cfg = config["matching"]
+    npx = h * w
+    rays0, pts0, pinit0 = matching.prep_for_iter_proj(X11, X21, None)
+    p0 = torch.empty(1, npx, 2, device=dev)
+    conv0 = torch.empty(1, npx, device=dev, dtype=torch.bool)
+    _lib.call("s3m_iter_proj", rays0.data_ptr(), pts0.data_ptr(), pinit0.data_ptr(),
+              p0.data_ptr(), conv0.data_ptr(), 1, h, w, npx, int(cfg["max_iter"]),
+              float(cfg["lambda_init"]), float(cfg["convergence_thresh"]), _lib.stream(dev))
+    p1_0 = torch.empty(1, npx, 2, device=dev, dtype=torch.int64)
+    valid0 = torch.empty(1, npx, device=dev, dtype=torch.bool)
+    _lib.call("s3m_occlusion", p0.data_ptr(), conv0.data_ptr(), X11.data_ptr(),
+              X21.data_ptr(), p1_0.data_ptr(), valid0.data_ptr(), 1, h, w,
+              float(cfg["dist_thresh"]), _lib.stream(dev))
+    D21r = D21.reshape(1, npx, -1).contiguous()
+
+    def stage(name):
+        st = _lib.stream(dev)
+        if name == "prep":
+            r, q, pi = matching.prep_for_iter_proj(X11, X21, None)
+            return torch.cat((r.reshape(-1), q.reshape(-1), pi.reshape(-1))), None
+        if name == "iter":
+            p = torch.empty(1, npx, 2, device=dev)
+            c = torch.empty(1, npx, device=dev, dtype=torch.bool)
+            _lib.call("s3m_iter_proj", rays0.data_ptr(), pts0.data_ptr(), pinit0.data_ptr(),
+                      p.data_ptr(), c.data_ptr(), 1, h, w, npx, int(cfg["max_iter"]),
+                      float(cfg["lambda_init"]), float(cfg["convergence_thresh"]), st)
+            return p, c
+        if name == "occl":
+            q = torch.empty(1, npx, 2, device=dev, dtype=torch.int64)
+            v = torch.empty(1, npx, device=dev, dtype=torch.bool)
+            _lib.call("s3m_occlusion", p0.data_ptr(), conv0.data_ptr(), X11.data_ptr(),
+                      X21.data_ptr(), q.data_ptr(), v.data_ptr(), 1, h, w,
+                      float(cfg["dist_thresh"]), st)
+            return q, v
+        if name == "refine":
+            return matching.refine_matches(D11, D21r, p1_0, int(cfg["radius"]),
+                                           int(cfg["dilation_max"])), None
+        raise ValueError(name)
+
     def victim_run():
+        if victim.startswith("stage_"):
+            a, b = stage(victim[6:])
+            return a, (b if b is not None else a[:1])
         if victim == "torch":
             y = torch.sin(xv) * 1.5 + xv * xv
+            return y, (y > 0.5)
+        if victim == "torch64":
+            xd = xv.double()
+            y = (1.0 / (xd + 4.0)) * 1.5 + xd * xd
             return y, (y > 0.5)
         return matching.match(X11, X21, D11, D21)
 
@@ -104,7 +161,7 @@ def main():
             torch.cuda.synchronize()
             for idx, valid in outs:
                 calls += 1
-                n = int(((idx != ref_idx).reshape(-1) | (valid != ref_valid).reshape(-1)).sum())
+                n = int((idx != ref_idx).sum()) + int((valid != ref_valid).sum())
                 if n:
                     bad_calls += 1
                     bad_px += n
@@ -114,7 +171,7 @@ def main():
     torch.cuda.synchronize()
     for idx, valid in outs:
         calls += 1
-        n = int(((idx != ref_idx).reshape(-1) | (valid != ref_valid).reshape(-1)).sum())
+        n = int((idx != ref_idx).sum()) + int((valid != ref_valid).sum())
         if n:
             bad_calls += 1
             bad_px += n
