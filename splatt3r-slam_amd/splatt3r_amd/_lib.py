@@ -159,12 +159,13 @@ def wait_event(ev) -> None:
 # first use and handed out round-robin, so which frame-loop stream shared a
 # queue with which (the encoder's 13-ms batch replays with the aux stream or
 # the default stream behind the main chain's per-step wait) depended on how
-# many streams the process had taken before.  These streams are created by
-# the library instead, once per device, in this fixed order and ahead of
-# torch's pool when reserve_frame_streams() runs first (bench.py does): the
-# process's default stream, the encoder, the aux stream (world records,
-# read-backs) and the backend worker hold the 4 normal-priority queues, the
-# main chain the high-priority one.
+# many streams the process had taken before.  Every role therefore takes
+# one stream per (device, role, priority), once, in this fixed order, when
+# reserve_frame_streams() runs first (bench.py does).  The streams come from
+# torch's pool by default; S3_FRAME_STREAMS=1 creates dedicated library
+# streams instead (then the default stream, the encoder, the aux stream and
+# the backend worker hold the 4 normal-priority queues and the main chain
+# the high-priority one) -- measured slower, see below.
 FRAME_STREAM_ROLES = (("encoder", 0), ("aux", 0), ("backend", 0), ("main", -1))
 _FRAME_STREAMS: dict = {}
 _FRAME_ORDER: list = []        # (device index, role, priority) in creation order
@@ -173,12 +174,18 @@ _FRAME_ORDER: list = []        # (device index, role, priority) in creation orde
 _STREAM_LOCK = threading.Lock()
 
 
-# S3_FRAME_STREAMS=0: torch's pooled streams instead (A/B diagnostic)
-FRAME_STREAMS_DEDICATED = os.environ.get("S3_FRAME_STREAMS", "1") != "0"
+# S3_FRAME_STREAMS=1: dedicated library streams (s3_stream_create) instead
+# of torch's pooled streams.  Measured against each other in driver-command
+# benches on one box (profiles/r06y_frame_streams_ab.log): pooled 203.4 /
+# 202.6 frames/s, no main-queue gap; dedicated 191.5 (one 5.5 ms gap at
+# frame 16) / 197.7, and both r06x runs on the dedicated streams had a
+# 6-7 ms gap at frame 16.  The pooled streams are the default.
+FRAME_STREAMS_DEDICATED = os.environ.get("S3_FRAME_STREAMS", "0") == "1"
 
 
 def _make_stream(dev: torch.device, priority: int):
-    """A dedicated non-blocking HIP stream (s3_stream_create) as a torch stream."""
+    """A stream of torch's pool, or with S3_FRAME_STREAMS=1 a dedicated
+    non-blocking HIP stream (s3_stream_create) wrapped as a torch stream."""
     if not FRAME_STREAMS_DEDICATED:
         return torch.cuda.Stream(device=dev, priority=int(priority))
     h = P()

@@ -35,6 +35,8 @@ from collections import defaultdict
 
 
 def _family(name: str) -> str:
+    if "k_gemm_bd<" in name:          # B-direct tiles: dense A only
+        return "gemm_dense"
     # k_gemm / k_gemm_pp <BM, BN, NWM, NWN, AMODE, ...>: AMODE 0 = dense
     m = re.search(r"k_gemm(?:_pp)?<(\d+), (\d+), \d+, \d+, (\d+),", name)
     if m:
@@ -71,10 +73,15 @@ def run_raster(reps: int) -> None:
     print("pmc_traffic run: done", reps, "raster forward+backward")
 
 
-def run(reps: int, kb: int = 1, bp: int = 1) -> None:
+def run(reps: int, kb: int = 1, bp: int = 1, mix=None) -> None:
     """One rep = kb frames: one encoder replay of kb images and kb / bp
     replays of the Bp = bp pair plan (the bench's frame composition with
-    --enc-batch kb and, for bp = 2, --decode-ahead with every slot used)."""
+    --enc-batch kb and, for bp = 2, --decode-ahead with every slot used).
+    mix = (frames, encoder replays, Bp=2 replays, Bp=1 replays) per rep
+    instead: the bench's timed composition (frame_breakdown.decode_ahead:
+    paired frames share a Bp = 2 replay, the others decode alone)."""
+    if mix is not None:
+        return _run_mix(reps, kb, mix)
     import torch
     from splatt3r_amd import weights as W
     from splatt3r_amd.net import Splatt3RNet
@@ -100,6 +107,35 @@ def run(reps: int, kb: int = 1, bp: int = 1) -> None:
     torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     print("pmc_traffic run: done", reps, "reps of", kb, "frames")
+
+
+def _run_mix(reps: int, kb: int, mix) -> None:
+    import torch
+    from splatt3r_amd import weights as W
+    from splatt3r_amd.net import Splatt3RNet
+    frames, n_enc, n_p2, n_p1 = mix
+    H, Wd = 384, 512
+    net = Splatt3RNet(W.FULL, seed=1234, graphs=False)
+    img = torch.rand(kb, 3, H, Wd, device="cuda") * 2 - 1
+    f, p, _ = net._encode_image(img)
+    for bp in (1, 2):
+        fb, pb = f[:1].expand(bp, -1, -1), p[:1].expand(bp, -1, -1)
+        net.infer_pair(fb, pb, fb, pb, (H, Wd))
+    enc = net.encoder_plan(kb, H, Wd).plan
+    p2, p1 = net.pair_plan(2, H, Wd), net.pair_plan(1, H, Wd)
+    plans = ([enc] * n_enc + [p2.decoder_plan, p2.head_plan] * n_p2
+             + [p1.decoder_plan, p1.head_plan] * n_p1)
+    torch.cuda.synchronize()
+    for plan in plans:
+        plan.run()
+    torch.cuda.synchronize()
+    for _ in range(reps):
+        torch.cuda._sleep(1000)
+        for plan in plans:
+            plan.run()
+    torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
+    print("pmc_traffic run: done", reps, "reps of", frames, "frames (mix)")
 
 
 def _load(d: str, counter: str):
@@ -128,7 +164,7 @@ def _frames(rows, reps: int, marker: str):
 
 
 def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str, workload: str = "network",
-              kb: int = 1, bp: int = 1):
+              kb: int = 1, bp: int = 1, mix=None):
     out = {}
     for counter, d, scale in (("FETCH_SIZE", fetch_dir, 2.0), ("WRITE_SIZE", write_dir, 1.0)):
         frames = _frames(_load(d, counter), reps, marker)
@@ -138,7 +174,7 @@ def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str, workload: 
                 a = agg[_family(name)]
                 a[0] += 1
                 a[1] += kib * 1024.0 * scale
-        nf = reps * kb     # frames
+        nf = reps * (mix[0] if mix else kb)     # frames
         for fam, (n, b) in agg.items():
             o = out.setdefault(fam, {"launches_per_frame": n / nf})
             o[("read" if counter == "FETCH_SIZE" else "write") + "_bytes_per_frame"] = b / nf
@@ -147,13 +183,21 @@ def summarize(fetch_dir: str, write_dir: str, reps: int, marker: str, workload: 
         o["bytes_per_launch"] = o["bytes_per_frame"] / max(1e-9, o["launches_per_frame"])
     return {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                       "FETCH_SIZE x2 (gfx950 correction), KiB -> bytes",
-            "workload": (f"512x384 frames of the network (encoder + decoder + 2 heads), eager; "
-                         f"encoder batch {kb}, pair plan Bp={bp} ({kb // bp} pair replays per "
-                         f"encoder replay), per frame"
+            "workload": ((f"512x384 frames of the network (encoder + decoder + 2 heads), eager; "
+                          f"the bench's timed composition: per {mix[0]} frames {mix[1]} encoder "
+                          f"replays of batch {kb}, {mix[2]} Bp=2 and {mix[3]} Bp=1 pair replays; "
+                          f"per frame") if mix else
+                         (f"512x384 frames of the network (encoder + decoder + 2 heads), eager; "
+                          f"encoder batch {kb}, pair plan Bp={bp} ({kb // bp} pair replays per "
+                          f"encoder replay), per frame")
                          if workload == "network" else
                          "C3 rasterizer: 4,194,304 splats at 960x540, forward + backward "
                          "(GaussianRasterizer, torch elementwise kernels included)"),
             "frames": reps, "families": dict(sorted(out.items(), key=lambda kv: -kv[1]["bytes_per_frame"]))}
+
+
+def _mix(v):
+    return tuple(int(x) for x in v.split(",")) if v else None
 
 
 def main():
@@ -164,9 +208,12 @@ def main():
     r.add_argument("--workload", choices=("network", "raster"), default="network")
     r.add_argument("--kb", type=int, default=1, help="encoder batch (frames per rep)")
     r.add_argument("--bp", type=int, default=1, help="pairs per pair-plan replay")
+    r.add_argument("--mix", default=None,
+                   help="frames,encoder replays,Bp=2 replays,Bp=1 replays per rep")
     s = sub.add_parser("summarize")
     s.add_argument("--kb", type=int, default=1)
     s.add_argument("--bp", type=int, default=1)
+    s.add_argument("--mix", default=None)
     s.add_argument("fetch_dir")
     s.add_argument("write_dir")
     s.add_argument("--reps", type=int, default=3)
@@ -178,9 +225,10 @@ def main():
         if a.workload == "raster":
             run_raster(a.reps)
         else:
-            run(a.reps, a.kb, a.bp)
+            run(a.reps, a.kb, a.bp, _mix(a.mix))
         return
-    res = summarize(a.fetch_dir, a.write_dir, a.reps, a.marker, a.workload, a.kb, a.bp)
+    res = summarize(a.fetch_dir, a.write_dir, a.reps, a.marker, a.workload, a.kb, a.bp,
+                    _mix(a.mix))
     txt = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as fh:
