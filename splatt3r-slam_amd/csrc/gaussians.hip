@@ -1,20 +1,30 @@
 // gaussians_to_world for one predicted view (include/s3w.h).
 //
-// k_prep    strided gather of z, "z > depth_min" keys (+inf otherwise) and
-//           the valid count
-// sort      hipcub radix sort of the keys (the quantile's order statistic)
-// k_flags   torch.quantile (linear) bound + scale / confidence filters
-// scan      hipcub exclusive sum of the flags (stable compaction order)
-// k_emit    world transform, covariance, colour, opacity -> 13-float records
+// Multi-pass path (n > kSelMax: the stride-1 views, 196,608 Gaussians at
+// 512x384), hand-written, no library sort or scan:
+// k_prep       strided gather of z -> order-preserving uint32 keys
+//              ("z > depth_min", 0xffffffff otherwise) and the valid count
+// k_sel_hist / k_sel_pick
+//              the two order statistics torch.quantile (linear) needs, by a
+//              radix select: 4 passes of 8-bit digits, per-block LDS
+//              histograms of the keys still matching each rank's prefix,
+//              one workgroup picks the digit (integer counts: exact)
+// k_flags      quantile bound + scale / confidence filters, per-block kept
+//              counts
+// k_scan_blocks  exclusive scan of the block counts (one workgroup) and
+//              the total
+// k_emit       block-local scan of the flags + the block's offset (stable
+//              compaction order): world transform, covariance, colour,
+//              opacity -> 13-float records
 // All stream-ordered; the only host-visible result is *count_dev.
 //
 // Map buffer (SharedGaussians, frame.py:357-463):
-// k_map_flags  opacity > threshold over the valid records
-// scan         hipcub exclusive sum (record-order compaction)
+// k_map_flags  opacity > threshold over the valid records, block counts
+// k_scan_blocks  (record-order compaction)
 // k_map_evict  if full: newest half -> front (one grid-stride copy), and the
 //              post-eviction count for the append
 // k_map_emit   scatter kept records into the SoA map, update the count
-#include <hipcub/hipcub.hpp>
+#include <algorithm>
 
 #include "common.hpp"
 #include "s3w.h"
@@ -25,43 +35,30 @@ constexpr int kThreads = 256;
 constexpr float kC0 = 0.28209479177387814f;
 
 struct Ws {
-  float* keys_in;
-  float* keys_out;
-  uint32_t* flags;
-  uint32_t* offsets;
-  uint32_t* n_valid0;
-  void* sort_tmp;
-  size_t sort_bytes;
-  void* scan_tmp;
-  size_t scan_bytes;
+  uint32_t* keys;     // fkey(z) / 0xffffffff, per Gaussian
+  uint32_t* flags;    // kept, per Gaussian
+  uint32_t* bsum;     // per-block kept counts -> exclusive block offsets; [nblk] = total
+  uint32_t* hist;     // [2][256] select histograms
+  uint32_t* sel;      // [0..3] (prefix, remaining rank) of the two ranks, [4] n0
 };
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-size_t sort_bytes(int64_t n) {
-  size_t b = 0;
-  hipcub::DeviceRadixSort::SortKeys(nullptr, b, (float*)nullptr, (float*)nullptr, (int)n);
-  return b;
-}
+int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
-size_t scan_bytes(int64_t n) {
-  size_t b = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-  return b;
+size_t ws_bytes(int64_t n) {
+  return 2 * align256(sizeof(uint32_t) * n) + align256(sizeof(uint32_t) * (nblocks(n) + 1)) +
+         align256(sizeof(uint32_t) * 512) + 256;
 }
 
 Ws carve(void* base, int64_t n) {
   char* p = static_cast<char*>(base);
   Ws w;
-  w.keys_in = (float*)p;  p += align256(sizeof(float) * n);
-  w.keys_out = (float*)p; p += align256(sizeof(float) * n);
+  w.keys = (uint32_t*)p;  p += align256(sizeof(uint32_t) * n);
   w.flags = (uint32_t*)p; p += align256(sizeof(uint32_t) * n);
-  w.offsets = (uint32_t*)p; p += align256(sizeof(uint32_t) * n);
-  w.n_valid0 = (uint32_t*)p; p += 256;
-  w.sort_bytes = sort_bytes(n);
-  w.sort_tmp = p; p += align256(w.sort_bytes);
-  w.scan_bytes = scan_bytes(n);
-  w.scan_tmp = p;
+  w.bsum = (uint32_t*)p;  p += align256(sizeof(uint32_t) * (nblocks(n) + 1));
+  w.hist = (uint32_t*)p;  p += align256(sizeof(uint32_t) * 512);
+  w.sel = (uint32_t*)p;
   return w;
 }
 
@@ -72,29 +69,6 @@ struct Grid {
     return y * W + x;
   }
 };
-
-__global__ void __launch_bounds__(kThreads)
-k_prep(int64_t n, Grid g, const float* __restrict__ means, float depth_min,
-       float* __restrict__ keys, uint32_t* __restrict__ n_valid0) {
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
-  const float z = means[g.pix(i) * 3 + 2];
-  const bool v = z > depth_min;
-  keys[i] = v ? z : INFINITY;
-  if (v) atomicAdd(n_valid0, 1u);
-}
-
-// torch.quantile(sorted[:n], q), interpolation='linear' (aten Sorting.cpp:
-// ranks = q * (n - 1); below = long(ranks); above = ceil(ranks);
-// lerp(v_below, v_above, ranks - below) with torch's two-sided lerp).
-__device__ float quantile_linear(const float* sorted, uint32_t n, float q) {
-  const float ranks = q * (float)(n - 1);
-  const int64_t lo = (int64_t)ranks;
-  const int64_t hi = (int64_t)ceilf(ranks);
-  const float w = ranks - (float)lo;
-  const float a = sorted[lo], b = sorted[hi];
-  return fabsf(w) < 0.5f ? a + w * (b - a) : b - (b - a) * (1.0f - w);
-}
 
 // The three splash filters of one Gaussian (splatt3r_utils.py:296-312).
 __device__ __forceinline__ bool keep(int64_t p, const float* __restrict__ means,
@@ -112,20 +86,6 @@ __device__ __forceinline__ bool keep(int64_t p, const float* __restrict__ means,
   v = v && (m < max_scale);
   if (conf && min_conf > 0.0f) v = v && (conf[p] >= min_conf);
   return v;
-}
-
-__global__ void __launch_bounds__(kThreads)
-k_flags(int64_t n, Grid g, const float* __restrict__ means, const float* __restrict__ scales,
-        const float* __restrict__ conf, float depth_min, float q, float max_scale, float min_conf,
-        const float* __restrict__ sorted, const uint32_t* __restrict__ n_valid0,
-        uint32_t* __restrict__ flags) {
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
-  const int64_t p = g.pix(i);
-  const uint32_t n0 = *n_valid0;
-  const bool use_q = n0 > 0 && q < 1.0f;
-  flags[i] = keep(p, means, scales, conf, depth_min, use_q,
-                  use_q ? quantile_linear(sorted, n0, q) : 0.0f, max_scale, min_conf) ? 1u : 0u;
 }
 
 // One world record (13 floats) of the Gaussian at pixel p: world transform,
@@ -176,16 +136,6 @@ __device__ __forceinline__ void emit_record(const s3w_view& v, const Grid& g,
     o[9 + c] = fminf(fmaxf(sh0 * kC0 + 0.5f, 0.0f), 1.0f);
   }
   o[12] = v.opacities[p];
-}
-
-__global__ void __launch_bounds__(kThreads)
-k_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44, const uint32_t* __restrict__ flags,
-       const uint32_t* __restrict__ offsets, float* __restrict__ out, int64_t* __restrict__ count) {
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
-  if (i == n - 1) *count = (int64_t)offsets[i] + flags[i];
-  if (!flags[i]) return;
-  emit_record(v, g, T44, g.pix(i), out + (int64_t)offsets[i] * 13);
 }
 
 // ---- two-launch path (n <= kSelMax): k_g2w_select, one workgroup, holds
@@ -334,6 +284,165 @@ k_g2w_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44,
   emit_record(v, g, T44, g.pix(i), out + (int64_t)o * 13);
 }
 
+// ---- multi-pass path (n > kSelMax) ---------------------------------------
+
+// block-wide exclusive scan of one value per thread (kThreads threads)
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int NW = kThreads / 64;
+  const uint32_t incl = wave_incl_scan(x, lane);
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    if (w < wave) base += s_w[w];
+    tot += s_w[w];
+  }
+  __syncthreads();
+  if (total) *total = tot;
+  return base + incl - x;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_prep(int64_t n, Grid g, const float* __restrict__ means, float depth_min,
+       uint32_t* __restrict__ keys, uint32_t* __restrict__ sel) {
+  __shared__ uint32_t s_w[kThreads / 64];
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  bool ok = false;
+  if (i < n) {
+    const float z = means[g.pix(i) * 3 + 2];
+    ok = z > depth_min;
+    keys[i] = ok ? fkey(z) : 0xFFFFFFFFu;
+  }
+  uint32_t tot = 0;
+  block_excl_scan(ok ? 1u : 0u, s_w, &tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&sel[4], tot);   // n0 (integer: order-free)
+}
+
+// one select pass: histograms of digit (key >> shift) & 255 over the keys
+// whose higher digits equal each rank's prefix so far
+__global__ void __launch_bounds__(kThreads)
+k_sel_hist(int64_t n, const uint32_t* __restrict__ keys, const uint32_t* __restrict__ sel,
+           uint32_t mask, int shift, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t lh[2][256];
+  for (int b = threadIdx.x; b < 512; b += kThreads) (&lh[0][0])[b] = 0u;
+  __syncthreads();
+  const uint32_t p0 = sel[0], p1 = sel[2];
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kThreads) {
+    const uint32_t k = keys[i], d = (k >> shift) & 255u;
+    if ((k & mask) == p0) atomicAdd(&lh[0][d], 1u);
+    if ((k & mask) == p1) atomicAdd(&lh[1][d], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < 512; b += kThreads)
+    if ((&lh[0][0])[b]) atomicAdd(&hist[b], (&lh[0][0])[b]);
+}
+
+// one workgroup of two waves: wave t finds the digit holding its rank's
+// remaining rank (ranks floor / ceil of q (n0 - 1), set on the first pass),
+// then the histograms are cleared for the next pass
+__global__ void __launch_bounds__(128)
+k_sel_pick(uint32_t* __restrict__ hist, uint32_t* __restrict__ sel, int shift, float q) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t n0 = sel[4];
+  if (shift == 24 && threadIdx.x < 2) {
+    const float ranks = q * (float)(n0 > 0 ? n0 - 1 : 0);
+    sel[2 * threadIdx.x + 1] = threadIdx.x == 0 ? (uint32_t)(int64_t)ranks
+                                                : (uint32_t)(int64_t)ceilf(ranks);
+  }
+  __syncthreads();
+  const uint32_t rem = sel[2 * wave + 1];
+  uint32_t h[4], sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { h[j] = hist[wave * 256 + 4 * lane + j]; sum += h[j]; }
+  const uint32_t incl = wave_incl_scan(sum, lane);
+  const uint64_t hit = __ballot(rem < incl);
+  const int L = hit ? __ffsll((unsigned long long)hit) - 1 : -1;
+  if (lane == L) {
+    uint32_t c = incl - sum;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (rem < c + h[j]) {
+        sel[2 * wave] |= (uint32_t)(4 * lane + j) << shift;
+        sel[2 * wave + 1] = rem - c;
+        break;
+      }
+      c += h[j];
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < 512; b += 128) hist[b] = 0u;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_flags(int64_t n, Grid g, const float* __restrict__ means, const float* __restrict__ scales,
+        const float* __restrict__ conf, float depth_min, float q, float max_scale, float min_conf,
+        const uint32_t* __restrict__ sel, uint32_t* __restrict__ flags,
+        uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t s_w[kThreads / 64];
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const uint32_t n0 = sel[4];
+  const bool use_q = n0 > 0 && q < 1.0f;
+  float zq = 0.0f;
+  if (use_q) {
+    // torch.quantile linear between the two order statistics (as k_g2w_select)
+    const float ranks = q * (float)(n0 - 1);
+    const float a = fval(sel[0]), b = fval(sel[2]);
+    const float w = ranks - (float)(int64_t)ranks;
+    zq = fabsf(w) < 0.5f ? a + w * (b - a) : b - (b - a) * (1.0f - w);
+  }
+  uint32_t f = 0;
+  if (i < n) {
+    f = keep(g.pix(i), means, scales, conf, depth_min, use_q, zq, max_scale, min_conf) ? 1u : 0u;
+    flags[i] = f;
+  }
+  uint32_t tot = 0;
+  block_excl_scan(f, s_w, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// exclusive scan of the nblk block counts in place, total in bsum[nblk]
+// (and, when given, in *count)
+__global__ void __launch_bounds__(1024)
+k_scan_blocks(uint32_t* __restrict__ bsum, int64_t nblk, int64_t* __restrict__ count) {
+  __shared__ uint32_t s_w[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (int64_t c0 = 0; c0 < nblk; c0 += 1024) {
+    const int64_t c = c0 + threadIdx.x;
+    const uint32_t v = c < nblk ? bsum[c] : 0u;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      if (w < wave) base += s_w[w];
+      tot += s_w[w];
+    }
+    if (c < nblk) bsum[c] = carry + base + incl - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    bsum[nblk] = carry;
+    if (count) *count = (int64_t)carry;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_emit(int64_t n, Grid g, s3w_view v, const float* __restrict__ T44,
+       const uint32_t* __restrict__ flags, const uint32_t* __restrict__ bsum,
+       float* __restrict__ out) {
+  __shared__ uint32_t s_w[kThreads / 64];
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const uint32_t f = i < n ? flags[i] : 0u;
+  const uint32_t off = bsum[blockIdx.x] + block_excl_scan(f, s_w, nullptr);
+  if (f) emit_record(v, g, T44, g.pix(i), out + (int64_t)off * 13);
+}
+
 int64_t count_for(const s3w_view* v) {
   return s3::cdiv(v->H, v->stride) * s3::cdiv(v->W, v->stride);
 }
@@ -344,7 +453,7 @@ extern "C" void s3w_set_path(int path) { g_g2w_path = path; }
 
 extern "C" size_t s3w_workspace_bytes(int64_t n) {
   if (n <= 0) return 256;
-  return 4 * align256(sizeof(float) * n) + 256 + align256(sort_bytes(n)) + scan_bytes(n);
+  return ws_bytes(n);   // >= the two-launch path's slot array (n x 4 B)
 }
 
 extern "C" int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, float depth_min,
@@ -373,23 +482,29 @@ extern "C" int s3w_gaussians_to_world(const s3w_view* v, const float* T_WC, floa
     return S3_OK;
   }
   Ws w = carve(workspace, n);
-  const int blocks = (int)s3::cdiv(n, kThreads);
-  S3_HIP(hipMemsetAsync(w.n_valid0, 0, sizeof(uint32_t), st));
-  k_prep<<<blocks, kThreads, 0, st>>>(n, g, v->means, depth_min, w.keys_in, w.n_valid0);
-  S3_LAUNCH_CHECK();
+  const int64_t blocks = nblocks(n);
   const bool use_q = depth_max_percentile < 1.0f;
-  if (use_q) {
-    size_t tb = w.sort_bytes;
-    S3_HIP(hipcub::DeviceRadixSort::SortKeys(w.sort_tmp, tb, w.keys_in, w.keys_out, (int)n, 0,
-                                             32, st));
-  }
-  k_flags<<<blocks, kThreads, 0, st>>>(n, g, v->means, v->scales, v->conf, depth_min,
-                                       use_q ? depth_max_percentile : 1.0f, max_scale,
-                                       min_confidence, w.keys_out, w.n_valid0, w.flags);
+  S3_HIP(hipMemsetAsync(w.hist, 0, sizeof(uint32_t) * 512 + 256, st));   // hist, sel, n0
+  k_prep<<<(unsigned)blocks, kThreads, 0, st>>>(n, g, v->means, depth_min, w.keys, w.sel);
   S3_LAUNCH_CHECK();
-  size_t sb = w.scan_bytes;
-  S3_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, sb, w.flags, w.offsets, (int)n, st));
-  k_emit<<<blocks, kThreads, 0, st>>>(n, g, *v, T_WC, w.flags, w.offsets, out, count_dev);
+  if (use_q) {
+    const unsigned hb = (unsigned)std::min<int64_t>(blocks, 1024);
+    uint32_t mask = 0u;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      k_sel_hist<<<hb, kThreads, 0, st>>>(n, w.keys, w.sel, mask, shift, w.hist);
+      S3_LAUNCH_CHECK();
+      k_sel_pick<<<1, 128, 0, st>>>(w.hist, w.sel, shift, depth_max_percentile);
+      S3_LAUNCH_CHECK();
+      mask |= 255u << shift;
+    }
+  }
+  k_flags<<<(unsigned)blocks, kThreads, 0, st>>>(n, g, v->means, v->scales, v->conf, depth_min,
+                                                 use_q ? depth_max_percentile : 1.0f, max_scale,
+                                                 min_confidence, w.sel, w.flags, w.bsum);
+  S3_LAUNCH_CHECK();
+  k_scan_blocks<<<1, 1024, 0, st>>>(w.bsum, blocks, count_dev);
+  S3_LAUNCH_CHECK();
+  k_emit<<<(unsigned)blocks, kThreads, 0, st>>>(n, g, *v, T_WC, w.flags, w.bsum, out);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }
@@ -399,10 +514,8 @@ namespace {
 
 struct MapWs {
   uint32_t* flags;
-  uint32_t* offsets;
-  int64_t* n0;  // count after eviction (read by k_map_emit)
-  void* scan_tmp;
-  size_t scan_bytes;
+  uint32_t* bsum;  // per-block kept counts -> exclusive block offsets; [nblk] = total
+  int64_t* n0;     // count after eviction (read by k_map_emit)
 };
 
 MapWs carve_map(void* base, int64_t n, size_t* total = nullptr) {
@@ -410,20 +523,25 @@ MapWs carve_map(void* base, int64_t n, size_t* total = nullptr) {
   char* p0 = p;
   MapWs w;
   w.flags = (uint32_t*)p; p += align256(sizeof(uint32_t) * n);
-  w.offsets = (uint32_t*)p; p += align256(sizeof(uint32_t) * n);
+  w.bsum = (uint32_t*)p; p += align256(sizeof(uint32_t) * (nblocks(n) + 1));
   w.n0 = (int64_t*)p; p += 256;
-  w.scan_bytes = scan_bytes(n);
-  w.scan_tmp = p; p += align256(w.scan_bytes);
   if (total) *total = (size_t)(p - p0);
   return w;
 }
 
 __global__ void __launch_bounds__(kThreads)
 k_map_flags(int64_t n_max, const float* __restrict__ rec, const int64_t* __restrict__ count,
-            float thr, uint32_t* __restrict__ flags) {
+            float thr, uint32_t* __restrict__ flags, uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t s_w[kThreads / 64];
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n_max) return;
-  flags[i] = (i < *count && rec[i * 13 + 12] > thr) ? 1u : 0u;
+  uint32_t f = 0;
+  if (i < n_max) {
+    f = (i < *count && rec[i * 13 + 12] > thr) ? 1u : 0u;
+    flags[i] = f;
+  }
+  uint32_t tot = 0;
+  block_excl_scan(f, s_w, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
 // grid-stride: every block copies a slice of the newest half when full.
@@ -431,11 +549,10 @@ k_map_flags(int64_t n_max, const float* __restrict__ rec, const int64_t* __restr
 // of 0) leaves the map untouched: frame.py:414-416 returns before the
 // eviction when n_new == 0.
 __global__ void __launch_bounds__(kThreads)
-k_map_evict(s3w_map m, int64_t n_max, const uint32_t* __restrict__ flags,
-            const uint32_t* __restrict__ offsets, int64_t* __restrict__ n0) {
+k_map_evict(s3w_map m, const uint32_t* __restrict__ kept_total, int64_t* __restrict__ n0) {
   const int64_t n = *m.n;
   const int64_t half = m.cap / 2;
-  const int64_t kept = (int64_t)offsets[n_max - 1] + flags[n_max - 1];
+  const int64_t kept = (int64_t)*kept_total;
   const bool full = n >= m.cap && kept > 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *n0 = full ? half : n;
   if (!full) return;
@@ -455,18 +572,20 @@ k_map_evict(s3w_map m, int64_t n_max, const uint32_t* __restrict__ flags,
 
 __global__ void __launch_bounds__(kThreads)
 k_map_emit(int64_t n_max, s3w_map m, const float* __restrict__ rec,
-           const uint32_t* __restrict__ flags, const uint32_t* __restrict__ offsets,
+           const uint32_t* __restrict__ flags, const uint32_t* __restrict__ bsum, int64_t nblk,
            const int64_t* __restrict__ n0p, int32_t kf) {
+  __shared__ uint32_t s_w[kThreads / 64];
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n_max) return;
+  const uint32_t f = i < n_max ? flags[i] : 0u;
+  const int64_t off = (int64_t)bsum[blockIdx.x] + block_excl_scan(f, s_w, nullptr);
   const int64_t n0 = *n0p;
   const int64_t space = m.cap - n0;
   if (i == n_max - 1) {
-    const int64_t kept = (int64_t)offsets[i] + flags[i];
+    const int64_t kept = (int64_t)bsum[nblk];
     *m.n = n0 + (kept < space ? kept : space);
   }
-  if (!flags[i] || (int64_t)offsets[i] >= space) return;
-  const int64_t j = n0 + offsets[i];
+  if (!f || off >= space) return;
+  const int64_t j = n0 + off;
   const float* r = rec + i * 13;
 #pragma unroll
   for (int k = 0; k < 3; ++k) m.means[j * 3 + k] = r[k];
@@ -509,18 +628,18 @@ extern "C" int s3w_map_append(const s3w_map* map, const float* records, const in
   S3_REQUIRE(records && count_dev && workspace, "s3w_map_append: null argument");
   hipStream_t st = s3::as_stream(stream);
   MapWs w = carve_map(workspace, n_max);
-  const int blocks = (int)s3::cdiv(n_max, kThreads);
-  k_map_flags<<<blocks, kThreads, 0, st>>>(n_max, records, count_dev, opacity_threshold,
-                                           w.flags);
+  const int64_t blocks = nblocks(n_max);
+  k_map_flags<<<(unsigned)blocks, kThreads, 0, st>>>(n_max, records, count_dev,
+                                                     opacity_threshold, w.flags, w.bsum);
   S3_LAUNCH_CHECK();
-  size_t sb = w.scan_bytes;
-  S3_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, sb, w.flags, w.offsets, (int)n_max, st));
+  k_scan_blocks<<<1, 1024, 0, st>>>(w.bsum, blocks, nullptr);
+  S3_LAUNCH_CHECK();
   const int64_t half = map->cap / 2;
   const int eb = (int)std::max<int64_t>(1, std::min<int64_t>(s3::cdiv(half, kThreads), 2048));
-  k_map_evict<<<eb, kThreads, 0, st>>>(*map, n_max, w.flags, w.offsets, w.n0);
+  k_map_evict<<<eb, kThreads, 0, st>>>(*map, w.bsum + blocks, w.n0);
   S3_LAUNCH_CHECK();
-  k_map_emit<<<blocks, kThreads, 0, st>>>(n_max, *map, records, w.flags, w.offsets, w.n0,
-                                          kf_idx);
+  k_map_emit<<<(unsigned)blocks, kThreads, 0, st>>>(n_max, *map, records, w.flags, w.bsum,
+                                                    blocks, w.n0, kf_idx);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }
