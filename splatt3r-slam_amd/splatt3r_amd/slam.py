@@ -827,7 +827,8 @@ class Frontend:
                 else None
             add_new_kf, _, try_reloc = self.tracker.track(
                 frame, before_sync=hook,
-                ahead=self._ahead_source(i, frame) if self.decode_ahead else None)
+                ahead=self._ahead_source(i, frame) if self.decode_ahead else None,
+                keep_info=False)
             # states.set_frame(frame) (main.py:455): the next frame starts from
             # the tracked pose, not from what the backend later writes into
             # the keyframe (the same object here, a shared-memory copy there)

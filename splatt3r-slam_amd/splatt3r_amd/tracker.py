@@ -219,7 +219,7 @@ class FrameTracker:
     def reset_idx_f2k(self):
         self.idx_f2k = None
 
-    def track(self, frame, before_sync=None, ahead=None):
+    def track(self, frame, before_sync=None, ahead=None, keep_info=True):
         """tracker.py:28-127; returns (new_kf, match_info, try_reloc).
 
         before_sync(T_WC): called with the device-side pose after the first
@@ -228,7 +228,9 @@ class FrameTracker:
         Its result is kept in self.spec; self.spec_valid says whether that
         pose is the final one (GN stopped inside the first chunk).
         ahead(): the next frame for a shared decode (splatt3r_utils
-        _decode_ahead), or None."""
+        _decode_ahead), or None.  keep_info=False: the match info list is not
+        built (None; the frontend drops it: no Q copies, no average-conf
+        passes per frame)."""
         self.spec, self.spec_valid = None, False
         from splatt3r_amd.splatt3r_utils import splatt3r_match_asymmetric
         mark = getattr(self, "mark", None)       # host-phase recorder (diagnostic)
@@ -321,6 +323,8 @@ class FrameTracker:
         new_kf = min(match_frac_k, unique_frac_f) < self.cfg["match_frac_thresh"]
         if new_kf:
             self.reset_idx_f2k()
+        if not keep_info:
+            return new_kf, None, False
         # Qkf / Qff are views of the pair plan's outputs (splatt3r_match_asymmetric):
         # copies for a caller that keeps the match info past this frame
         return (new_kf, [keyframe.X_canon, keyframe.get_average_conf(), frame.X_canon,
