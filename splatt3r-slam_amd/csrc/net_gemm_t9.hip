@@ -10,11 +10,13 @@
 // it with one fully coalesced 16-B-per-lane buffer load.  N is padded to a
 // multiple of 16 with zeros; K must be a multiple of 32.
 //
-// Reduction order: the K tiles run in order, each as two 16x16x32 steps in
-// k order, into one accumulator chain per element -- the order of every
-// other 16x16x32 tile without K-groups or split-K (ops.reduction_class
-// (16, 1, 0, 0, ...)), and the same LDS-staged vector epilogue, so these
-// tiles compute the same bits as those.
+// Reduction order: the K tiles of the workgroup's split run in order, each
+// as two 16x16x32 steps in k order, into one accumulator chain per element
+// -- the order of every other 16x16x32 tile without K-groups
+// (ops.reduction_class (16, 1, 0, bound, ...)); with split-K each split's
+// fp32 plane goes through the shared k_splitk_reduce, which adds the planes
+// in split order, and without it the same LDS-staged vector epilogue: these
+// tiles compute the same bits as the LDS-staged tiles of their class.
 //
 // The A tile and the B fragments of K tile kt are issued together (one
 // "tile" of AW + 2 FN vector-memory operations per wave), S - 1 tiles ahead,
@@ -95,7 +97,10 @@ k_gemm_bd(GemmP p) {
   const int M = p.M, N = p.N, K = p.K;
   const f16* __restrict__ A = p.A[g];
   const f16* __restrict__ Bp = p.Bp[g];
-  const int KT = (K + BK - 1) / BK;
+  // this workgroup's K tiles: split blockIdx.y of plan_grid's partition
+  const int KT_all = (K + BK - 1) / BK;
+  const int kt_begin = blockIdx.y * p.kt_per_split;
+  const int KT = min(KT_all, kt_begin + p.kt_per_split) - kt_begin;
   const int KS = K / 32;            // packed K steps (host: K % 32 == 0)
   const int Npad = (N + 15) & ~15;
 
@@ -135,7 +140,7 @@ k_gemm_bd(GemmP p) {
   auto issue = [&](int kt, auto stc) {
     constexpr int st = decltype(stc)::value;
     f16* As = ring + st * STAGE;
-    const int k0 = kt * BK;
+    const int k0 = (kt_begin + kt) * BK;
     const bool live = kt < KT;
 #pragma unroll
     for (int j = 0; j < AW; ++j) {
@@ -145,8 +150,8 @@ k_gemm_bd(GemmP p) {
     }
 #pragma unroll
     for (int q = 0; q < NKS; ++q) {
-      const int ks = 2 * kt + q;
-      const bool ok = ks < KS;
+      const int ks = 2 * (kt_begin + kt) + q;
+      const bool ok = live && ks < KS;
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
@@ -202,15 +207,14 @@ k_gemm_bd(GemmP p) {
 
 template <int BM, int BN, int NWM, int NWN, int S>
 int launch_bd(const GemmP& p, hipStream_t st) {
-  S3_REQUIRE(p.a_mode == S3N_A_DENSE && p.Bp[0] && p.vec_epi && p.split_k <= 1 && !p.tail_w[0] &&
-                 p.K % 32 == 0,
+  S3_REQUIRE(p.a_mode == S3N_A_DENSE && p.Bp[0] && p.vec_epi && !p.tail_w[0] && p.K % 32 == 0,
              "s3n_gemm: B-direct tiles need dense A, the packed B (s3n_gemm_args.Bp), the vector "
-             "epilogue, split_k 1, no fused tail and K %% 32 == 0");
+             "epilogue, no fused tail and K %% 32 == 0");
   const GemmP q = plan_grid(p, BM, BN, 64);
-  dim3 grid(q.tiles_m * q.tiles_n, 1, p.groups);
+  dim3 grid(q.tiles_m * q.tiles_n, q.split_k, p.groups);
   k_gemm_bd<BM, BN, NWM, NWN, S><<<grid, 64 * NWM * NWN, 0, st>>>(q);
   S3_LAUNCH_CHECK();
-  return S3_OK;
+  return launch_splitk_reduce(q, st);
 }
 
 }  // namespace

@@ -249,7 +249,7 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
                 # A through the LDS ring (net_gemm_t9.hip)
                 70: (64, 128), 71: (64, 128), 72: (64, 64), 73: (64, 64), 74: (128, 128),
                 75: (128, 128), 76: (128, 128), 77: (64, 128)}
-# the B-direct tiles: dense A, a packed B (packed_b), split_k 1, no fused tail
+# the B-direct tiles: dense A, a packed B (packed_b), no fused tail
 _BDIRECT = set(range(70, 78))
 _TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14, 40, 42, 43, 45, 46, 48, 49, 51, 52, 63, 65}
 # S3_GEMM_MF16=0: leave the 16x16x32 tile family out of the tuner (A/B)
@@ -415,7 +415,7 @@ def _tune_candidates(a, split_ok, like=None):
             continue
         tiles = a.groups * -(-a.M // bm) * -(-a.N // bn)
         for sk in (1, 2, 3, 4, 6, 8):
-            if sk > 1 and (tile in _HALO or tile in _BDIRECT):
+            if sk > 1 and tile in _HALO:
                 continue
             if like is not None:
                 # batch-invariant plan: only launches whose elements equal

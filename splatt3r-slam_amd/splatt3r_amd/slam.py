@@ -549,7 +549,10 @@ class Frontend:
         profiles/r04p_host_steps.log).  A freed large segment is split for
         later large allocations of its stream, and `small_blocks` freed 1 MiB
         blocks keep the small pool (<= 1 MiB requests) from growing."""
-        streams = [s for s in (self.enc_stream, self.main_stream) if s is not None]
+        # the aux stream too: the world records and read-backs allocate there
+        # (3 small-pool segments grew inside every timed window without it)
+        streams = [s for s in (self.enc_stream, self.main_stream, self.aux_stream)
+                   if s is not None]
         streams.append(torch.cuda.current_stream(self.device))
         seen = set()
         for st in streams:

@@ -172,6 +172,35 @@ def test_gemm_bdirect_tiles_bitexact_vs_same_reduction_class(bd, ref, M, N, K, g
         assert rel_err(outs[0][0][g], ref_) < 2e-3
 
 
+@pytest.mark.parametrize("bd,ref,M,N,K,groups,split", [
+    (73, 26, 1536, 768, 3072, 2, 3), (72, 22, 1536, 768, 3072, 2, 2),
+    (74, 32, 6144, 1024, 4096, 1, 2), (77, 26, 300, 136, 2080, 1, 4),
+    (70, 32, 520, 296, 1056, 3, 3), (75, 28, 1, 24, 640, 1, 2)])
+def test_gemm_bdirect_split_k_bitexact_vs_same_reduction_class(bd, ref, M, N, K, groups, split):
+    """Split-K on the B-direct tiles: each split's K tiles in order into an
+    fp32 plane, the planes added in split order by k_splitk_reduce -- the
+    same bits as an LDS-staged tile of the class with the same split
+    (ragged M and N, K % 64 == 32 at the last split, three groups), and
+    correct against torch."""
+    from splatt3r_amd import ops, _lib
+    assert ops.reduction_class(K, bd, split) == ops.reduction_class(K, ref, split)
+    A = [_rand(M, K, seed=g) for g in range(groups)]
+    W = [_rand(N, K, scale=K ** -0.5, seed=10 + g) for g in range(groups)]
+    b = [_rand(N, dtype=torch.float32, seed=20 + g) for g in range(groups)]
+    R = [_rand(M, N, dtype=torch.float32, seed=30 + g) for g in range(groups)]
+    outs = []
+    for tile in (bd, ref):
+        C = [torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16)
+             for _ in range(groups)]
+        ops.gemm(A, W, C, M, N, K, lda=K, bias=b, act="gelu", R1=R, ldr1=N, split_k=split,
+                 tile=tile)(_lib.stream())
+        outs.append(C)
+    for g in range(groups):
+        assert torch.equal(outs[0][g], outs[1][g])
+        ref_ = F.gelu(A[g].float() @ W[g].float().T + b[g]) + R[g]
+        assert rel_err(outs[0][g], ref_) < 2e-3
+
+
 @pytest.mark.parametrize("tile", [70, 71, 72, 73, 74, 75, 76, 77])
 def test_gemm_bdirect_rope_and_scatter_epilogues(tile):
     """The B-direct tiles share the LDS-staged epilogue: the fused RoPE2D

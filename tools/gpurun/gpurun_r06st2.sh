@@ -1,0 +1,16 @@
+#!/bin/bash
+# the driver's order (full GPU suite, smoke, bench) with the stall watchdog on the benches
+set -o pipefail
+O=gpurun_out/r06st2
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+for i in 1 2 3; do
+S3_STALL_TRACE=4 timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench$i.log 2> $O/bench$i.err || { tail -20 $O/bench$i.err; exit 1; }
+grep '^{' $O/bench$i.log | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); c=d['critical_path']
+print('run $i', round(d['value'],1), 'gaps', c['big_gaps'], 'host', [round(x,1) for x in c['host_step_ms']][5:10])"
+echo "dumps: $(grep -c 'most recent call first' $O/bench$i.err)"
+done
