@@ -9,14 +9,16 @@ arguments and return values), with every stage on HIP kernels:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from splatt3r_amd import _lib
 from splatt3r_amd.config import config
 
 # S3_REFINE_LANES=<n>: refine kernel variant for A/B runs (s3m_refine_set_lanes)
-if "S3_REFINE_LANES" in __import__("os").environ:
-    _lib.lib().s3m_refine_set_lanes(int(__import__("os").environ["S3_REFINE_LANES"]))
+if "S3_REFINE_LANES" in os.environ:
+    _lib.lib().s3m_refine_set_lanes(int(os.environ["S3_REFINE_LANES"]))
 
 
 def pixel_to_lin(p1, w):
