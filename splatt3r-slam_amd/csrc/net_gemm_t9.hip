@@ -220,7 +220,7 @@ int launch_bd(const GemmP& p, hipStream_t st) {
 }  // namespace
 
 namespace s3gemm {
-// tiles 70-77 (ops._BDIRECT); launch configurations measured against the
+// tiles 70-79 (ops._BDIRECT); launch configurations measured against the
 // LDS-staged tiles of the same reduction class on the network's dense shapes
 // (tools/bench_gemm_bd.py, profiles/r06b_gemm_bdirect.log)
 int launch_t9(int tile, const GemmP& p, hipStream_t st) {
@@ -233,6 +233,10 @@ int launch_t9(int tile, const GemmP& p, hipStream_t st) {
     case 75: return launch_bd<128, 128, 1, 4, 3>(p, st);
     case 76: return launch_bd<128, 128, 2, 4, 3>(p, st);   // 8 waves, wave 64 x 32
     case 77: return launch_bd<64, 128, 1, 4, 4>(p, st);
+    // 6-stage rings (5 K tiles in flight) for the latency-bound decoder
+    // launches: B needs no LDS, so a stage is only the A tile (8 KiB at BM 64)
+    case 78: return launch_bd<64, 64, 1, 4, 6>(p, st);
+    case 79: return launch_bd<64, 128, 1, 4, 6>(p, st);
     default: return kNotMine;
   }
 }

@@ -248,9 +248,9 @@ _TILE_SHAPES = {1: (64, 64), 2: (64, 128), 3: (128, 128), 4: (256, 128), 5: (128
                 # B fragments straight from the packed weights into registers,
                 # A through the LDS ring (net_gemm_t9.hip)
                 70: (64, 128), 71: (64, 128), 72: (64, 64), 73: (64, 64), 74: (128, 128),
-                75: (128, 128), 76: (128, 128), 77: (64, 128)}
+                75: (128, 128), 76: (128, 128), 77: (64, 128), 78: (64, 64), 79: (64, 128)}
 # the B-direct tiles: dense A, a packed B (packed_b), no fused tail
-_BDIRECT = set(range(70, 78))
+_BDIRECT = set(range(70, 80))
 _TAIL_OK = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 14, 40, 42, 43, 45, 46, 48, 49, 51, 52, 63, 65}
 # S3_GEMM_MF16=0: leave the 16x16x32 tile family out of the tuner (A/B)
 _EXCLUDED = set(range(21, 32)) if os.environ.get("S3_GEMM_MF16", "1") == "0" else set()
@@ -272,7 +272,7 @@ _TILE_RED = {1: (64, 1, 32), 2: (64, 1, 32), 3: (64, 1, 32), 4: (64, 1, 32), 5: 
              45: (64, 1, 32), 46: (64, 1, 16), 47: (64, 1, 16), 48: (64, 1, 32), 49: (64, 1, 16),
              50: (64, 1, 16), 51: (64, 1, 16), 52: (64, 1, 32), 53: (64, 1, 16),
              63: (64, 1, 16), 65: (64, 1, 32), 68: (64, 1, 16),
-             **{t: (64, 1, 16) for t in range(70, 78)}}
+             **{t: (64, 1, 16) for t in range(70, 80)}}
 _REGS_EPILOGUE = {14, 34, 35}   # the fp32 tile does not fit the LDS ring
 # K tiles in (ky, channel chunk, kx) order instead of (ky, kx, channel chunk)
 _HALO = set(range(40, 54)) - {44}

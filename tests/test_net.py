@@ -425,7 +425,7 @@ def test_every_tile_of_a_reduction_class_gives_the_same_bits_on_the_network_gemm
     """The premise of the batch-invariant plans (ops.reduction_class): on the
     network's own GEMM calls -- the encoder, decoder and head plans at full
     size, with their real epilogues -- every tile of the class the plan chose
-    (the B-direct tiles 70-77 included) reproduces the chosen tile's output
+    (the B-direct tiles 70-79 included) reproduces the chosen tile's output
     bit for bit.  The plans run once on real images first, so every GEMM's
     operands hold activations (plan buffers are reused across layers: the
     last layer's values), not the zeros of fresh buffers."""

@@ -142,7 +142,8 @@ def test_gemm_pp_tiles_bitexact_vs_same_reduction_class(pp, ref, M, N, K, groups
     (70, 32, 1536, 3072, 768, 2), (71, 26, 6144, 1024, 1024, 1), (72, 22, 300, 200, 1056, 2),
     (73, 26, 130, 296, 992, 1), (74, 32, 1536, 2304, 768, 2), (75, 28, 520, 296, 640, 1),
     (76, 32, 300, 136, 544, 2), (77, 26, 768, 1024, 4096, 1), (70, 32, 64, 40, 96, 1),
-    (71, 32, 1, 24, 32, 1), (72, 26, 200, 1040, 2080, 3)])
+    (71, 32, 1, 24, 32, 1), (72, 26, 200, 1040, 2080, 3), (78, 22, 1536, 768, 768, 2),
+    (79, 32, 130, 296, 992, 1), (78, 26, 64, 40, 96, 1)])
 def test_gemm_bdirect_tiles_bitexact_vs_same_reduction_class(bd, ref, M, N, K, groups):
     """The B-direct tiles (net_gemm_t9.hip: B fragments from the packed
     weights, ops.packed_b, straight into registers) compute every element
@@ -175,7 +176,7 @@ def test_gemm_bdirect_tiles_bitexact_vs_same_reduction_class(bd, ref, M, N, K, g
 @pytest.mark.parametrize("bd,ref,M,N,K,groups,split", [
     (73, 26, 1536, 768, 3072, 2, 3), (72, 22, 1536, 768, 3072, 2, 2),
     (74, 32, 6144, 1024, 4096, 1, 2), (77, 26, 300, 136, 2080, 1, 4),
-    (70, 32, 520, 296, 1056, 3, 3), (75, 28, 1, 24, 640, 1, 2)])
+    (70, 32, 520, 296, 1056, 3, 3), (75, 28, 1, 24, 640, 1, 2), (78, 26, 1536, 768, 3072, 2, 2)])
 def test_gemm_bdirect_split_k_bitexact_vs_same_reduction_class(bd, ref, M, N, K, groups, split):
     """Split-K on the B-direct tiles: each split's K tiles in order into an
     fp32 plane, the planes added in split order by k_splitk_reduce -- the
@@ -201,7 +202,7 @@ def test_gemm_bdirect_split_k_bitexact_vs_same_reduction_class(bd, ref, M, N, K,
         assert rel_err(outs[0][g], ref_) < 2e-3
 
 
-@pytest.mark.parametrize("tile", [70, 71, 72, 73, 74, 75, 76, 77])
+@pytest.mark.parametrize("tile", [70, 71, 72, 73, 74, 75, 76, 77, 78, 79])
 def test_gemm_bdirect_rope_and_scatter_epilogues(tile):
     """The B-direct tiles share the LDS-staged epilogue: the fused RoPE2D
     columns and the ConvTranspose scatter store equal tile 32's bits."""
