@@ -85,6 +85,10 @@ def main():
     D21 = D11 + 0.05 * torch.randn(D11.shape, device=dev, generator=g).half()
     victim = os.environ.get("STRESS_VICTIM", "match")
     xv = torch.randn(1 << 23, device=dev, generator=g)
+    q = torch.nn.functional.normalize(torch.randn(2, 4, device=dev, generator=g), dim=-1)
+    Tv = torch.cat([torch.randn(2, 3, device=dev, generator=g), q,
+                    torch.rand(2, 1, device=dev, generator=g) + 0.5], -1)
+    Pts = torch.randn(1, h * w, 3, device=dev, generator=g)
 
     # fixed inputs of each matching stage (victim = stage_<name>)
     from splatt3r_amd import _lib
@@ -135,6 +139,15 @@ def main():
         if victim == "torch":
             y = torch.sin(xv) * 1.5 + xv * xv
             return y, (y > 0.5)
+        if victim == "lie":
+            # the frame loop's pose algebra (lietorch Sim3 compose / inverse /
+            # act on a pointmap) and small torch glue, as on the main chain
+            import lietorch
+            Ta = lietorch.Sim3(Tv[0:1])
+            Tb = lietorch.Sim3(Tv[1:2])
+            Tc = Ta.inv() * Tb
+            Xw = Tc.act(Pts)
+            return Xw.contiguous(), (Tc.data * 1.0)
         if victim == "torch64":
             xd = xv.double()
             y = (1.0 / (xd + 4.0)) * 1.5 + xd * xd
