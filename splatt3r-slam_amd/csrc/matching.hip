@@ -443,7 +443,7 @@ k_refine_lane(const _Float16* __restrict__ D11, const _Float16* __restrict__ D21
 // has triplet t read pixel (u_t, v_j) as 48 contiguous bytes, so a query's
 // row is 7 x 48 B of one image row (contiguous at d = 1) -- about a third of
 // the 64-B segments per load of the candidate-per-lane kernels, which the
-// texture addresser bounds (profiles/r05j).
+// texture addresser bounds (profiles/r05j_refine_counters.txt).
 //
 // The reference's strict fp16 chain (matching_kernels.cu:55-64: every
 // product and every partial sum rounded to fp16, elements 0..23 in order)

@@ -55,7 +55,7 @@ def _shared_stream(device, priority, role):
     streams instead of creating two or three more each; every new stream is
     mapped onto one of the process's few hardware queues (GPU_MAX_HW_QUEUES),
     and a frontend whose streams came late in that assignment ran its
-    frames ~1.6x slower (tools/live_ab.py, profiles/r04k_live_ab.log).  The
+    frames ~1.6x slower (tools/live_ab.py, profiles/r04k_live_ab_before.log / _after.log).  The
     streams are the library's dedicated ones (_lib.frame_stream: created in
     a fixed order, each on a hardware queue of its own), not torch's pool."""
     return _lib.frame_stream(device, role, int(priority))
