@@ -290,6 +290,10 @@ class Frontend:
         # their consumers (stats, drain) wait for it
         self.aux_stream = _shared_stream(device, 0, "aux") if self.enc_stream is not None else None
         self._aux_used = False
+        # the tracked frame's speculative sync-free render on the aux stream
+        # too (S3_RENDER_AUX=0: on the main stream, behind the GN chunk)
+        self.render_on_aux = (self.aux_stream is not None and self.sizing is not None
+                              and os.environ.get("S3_RENDER_AUX", "1") != "0")
 
     def _prefetch(self, i, imgs):
         """Create frames i, i+1, ... for `imgs` and queue their encoder on
@@ -491,6 +495,8 @@ class Frontend:
                     img = None
                 elif self._rworker is not None:
                     img = self._render_task(frame, ref, T_WC)      # a ticket
+                elif self.render_on_aux and self.sizing.capacity is not None:
+                    img = self._render_aux(frame, ref, T_WC)
                 else:
                     img = splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=T_WC,
                                           sizing=self.sizing)
@@ -505,9 +511,34 @@ class Frontend:
             return recs, img
         return hook
 
+    def _render_aux(self, frame, ref, T_WC):
+        """The sync-free splatt3r_render on the aux stream, ordered after the
+        calling stream's work so far (the pose of the GN chunk, the
+        predictions), its inputs kept alive for the aux stream.  The image
+        carries its stream (`_s3_stream`): the flag copy, the read-back and
+        the PNG writer's copy are ordered after it there."""
+        cur = torch.cuda.current_stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        ins = [frame.img, ref.img, frame.T_WC.data, T_WC.data]
+        for g in (frame.gaussian_pred, frame.gaussian_pred_cross):
+            if g is not None:
+                ins += [v for v in g.values() if torch.is_tensor(v)]
+        with torch.cuda.stream(self.aux_stream):
+            self.aux_stream.wait_event(ready)
+            img = splatt3r_render(self.model, frame, ref, K=self.K, target_T_WC=T_WC,
+                                  sizing=self.sizing)
+        for t in ins:
+            if t.is_cuda:
+                t.record_stream(self.aux_stream)
+        if img is not None:
+            img._s3_stream = self.aux_stream
+        return img
+
     def _finish_render(self, img, index=0, prefix="gs_track", count=True):
         if img is not None and count:
             self._stats["rendered"] += 1
+        src = getattr(img, "_s3_stream", None)   # the aux stream (_render_aux) or None
         chk = getattr(img, "_gsr_check", None)
         if chk is not None:
             # pinned flag mirrors from a fixed ring (a pinned allocation in
@@ -522,14 +553,18 @@ class Frontend:
             self._info_i = (self._info_i + 1) % self._INFO_RING
             # the copy and the event on the frontend device's stream (the
             # Frontend's device need not be the current device)
-            st = torch.cuda.current_stream(self.device)
+            st = src if src is not None else torch.cuda.current_stream(self.device)
             with torch.cuda.stream(st):
                 info.copy_(chk.info, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(st)
             self._pending.append((img, chk, info, ev, index, prefix))
             return
-        self._deliver_image(img, index, prefix)
+        ready = None
+        if src is not None:
+            ready = torch.cuda.Event()
+            ready.record(src)
+        self._deliver_image(img, index, prefix, ready)
 
     def _deliver(self, block: bool):
         """Hand the validated sync-free renders to the writer / read-back in
@@ -596,6 +631,9 @@ class Frontend:
         stream (None: recorded here, on the current stream)."""
         if img is not None:
             if self.render_writer is not None:
+                if ready is not None:
+                    # the writer copies on the current stream
+                    torch.cuda.current_stream(self.device).wait_event(ready)
                 self.render_writer.submit(index, img, prefix)
                 self._last_render, self._rb_event = None, None
                 return

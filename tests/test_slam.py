@@ -516,7 +516,8 @@ def test_sync_free_render_matches_two_call_render():
     and delivers each image once its validity flag has landed: the renders,
     poses and counters equal the two-call path bit for bit, also when every
     frame overflows the binning capacity or the depth-key width and is
-    re-rendered."""
+    re-rendered; and with the speculative render on the aux stream (the
+    default) or on the main stream."""
     from splatt3r_amd.slam import Frontend
     from splatt3r_amd.splatt3r_utils import load_splatt3r
     from splatt3r_amd.synthetic import tum_like_sequence
@@ -527,9 +528,11 @@ def test_sync_free_render_matches_two_call_render():
     n = 8
     frames = tum_like_sequence(n + 1, 384, 512, seed=3, step_px=2.0, device=dev)
 
-    def run(deferred, force=None, per_frame=True):
+    def run(deferred, force=None, per_frame=True, aux=True):
         fe = Frontend(model, device=dev, spatial_stride=4, render=True, main_priority=-1,
                       deferred_render=deferred)
+        assert fe.render_on_aux == deferred       # the default with the aux stream
+        fe.render_on_aux = fe.render_on_aux and aux
         if force is not None:
             cap, bits = force
             fe.sizing.update = lambda *a, **k: None
@@ -559,20 +562,19 @@ def test_sync_free_render_matches_two_call_render():
             assert torch.equal(a, b)
         for a, b in zip(r0, r1):
             assert torch.equal(a, b), force
+    p3, r3, s3 = run(True, aux=False)
+    assert s3.pop("rerendered") == 0
+    assert s3 == {k: v for k, v in s0.items() if k != "rerendered"}
+    assert all(torch.equal(a, b) for a, b in zip(p0, p3))
+    assert all(torch.equal(a, b) for a, b in zip(r0, r3))
     # delivery lagging behind the loop (no read between frames): same last image
     _, r2, s2 = run(True, per_frame=False)
     assert torch.equal(r2[-1], r0[-1]) and s2["rendered"] == n
 
 
-def test_readback_copy_waits_on_the_render_event_on_the_aux_stream(monkeypatch):
-    """VERDICT r04 item 3 (the 6 ms host stall): the render read-back's
-    device-to-host copy, issued at the next step's start on the main stream
-    behind the queued decode-ahead replay, held the host until the stream
-    reached it (profiles/r05h_stall_trace.log).  _deliver_image issues it on
-    the aux stream, ordered after the render's own event only (never a
-    wait_stream on the main stream), and the ring slot's event is recorded
-    on that stream.  CPU stand-ins for the streams and events."""
-    from splatt3r_amd.slam import Frontend
+def _stand_in_streams(monkeypatch):
+    """CPU stand-ins for torch.cuda streams / events / stream contexts and
+    for record_stream and copy_, logging (stream, op, arg)."""
     log = []
 
     class _Stream:
@@ -623,6 +625,19 @@ def test_readback_copy_waits_on_the_render_event_on_the_aux_stream(monkeypatch):
         return real_copy(self, src)
 
     monkeypatch.setattr(torch.Tensor, "copy_", copy)
+    return log, main, aux, cur, _Event
+
+
+def test_readback_copy_waits_on_the_render_event_on_the_aux_stream(monkeypatch):
+    """VERDICT r04 item 3 (the 6 ms host stall): the render read-back's
+    device-to-host copy, issued at the next step's start on the main stream
+    behind the queued decode-ahead replay, held the host until the stream
+    reached it (profiles/r05h_stall_trace.log).  _deliver_image issues it on
+    the aux stream, ordered after the render's own event only (never a
+    wait_stream on the main stream), and the ring slot's event is recorded
+    on that stream.  CPU stand-ins for the streams and events."""
+    from splatt3r_amd.slam import Frontend
+    log, main, aux, cur, _Event = _stand_in_streams(monkeypatch)
     fe = Frontend.__new__(Frontend)
     fe.render_writer, fe.readback, fe.device = None, True, torch.device("cpu")
     fe.aux_stream, fe._RB_RING, fe._rb_i = aux, 2, 0
@@ -696,3 +711,49 @@ def test_first_frame_stream_loads_the_library_without_deadlock(monkeypatch):
     assert not t.is_alive(), "reserve_frame_streams deadlocked loading the library"
     assert len(_lib._FRAME_ORDER) == len(_lib.FRAME_STREAM_ROLES)
     assert _lib._lib is not None
+
+
+def test_speculative_render_runs_on_the_aux_stream(monkeypatch):
+    """The tracked frame's speculative sync-free render (Frontend._render_aux,
+    the default when the aux stream exists): issued on the aux stream after
+    it waits on an event recorded on the calling (main) stream, every input
+    kept alive for the aux stream, and the image's validity-flag copy and
+    delivery event on the aux stream too -- the main chain carries none of
+    it (headline A/B: profiles/r06ra_render_aux_ab.log).  CPU stand-ins."""
+    import types
+
+    import splatt3r_amd.slam as slam
+    from splatt3r_amd.slam import Frontend
+    from splatt3r_amd.splatt3r_utils import RasterSizing, RenderCheck
+    log, main, aux, cur, _Event = _stand_in_streams(monkeypatch)
+    sizing = RasterSizing()
+
+    def fake_render(model, frame, ref, K=None, target_T_WC=None, sizing=None):
+        log.append((cur[-1].name, "render", None))
+        out = torch.zeros(1, 1, 3, 4, 4)
+        out._gsr_check = RenderCheck(torch.zeros(3, dtype=torch.int64), None, sizing)
+        return out
+
+    monkeypatch.setattr(slam, "splatt3r_render", fake_render)
+    fe = Frontend.__new__(Frontend)
+    fe.device, fe.aux_stream, fe.model, fe.K, fe.sizing = torch.device("cpu"), aux, None, None, sizing
+    fe._stats = {"rendered": 0}
+    fe._info_ring, fe._info_i, fe._INFO_RING, fe._pending = None, 0, 4, []
+    pose = types.SimpleNamespace(data=torch.zeros(1, 8))
+    pred = {"means": torch.zeros(2, 3)}
+    frame = types.SimpleNamespace(img=torch.zeros(1, 3, 4, 4), T_WC=pose, gaussian_pred=pred,
+                                  gaussian_pred_cross=pred, frame_id=3)
+    ref = types.SimpleNamespace(img=torch.zeros(1, 3, 4, 4))
+    monkeypatch.setattr(torch.Tensor, "is_cuda", property(lambda self: True))
+    monkeypatch.setattr(torch, "empty", lambda *a, **k: torch.zeros(*a, dtype=k.get("dtype")))
+    img = fe._render_aux(frame, ref, pose)
+    i_rec = log.index(("main", "record", log[0][2]))
+    assert log[i_rec + 1] == ("aux", "wait_event", log[0][2])
+    assert log[i_rec + 2] == ("aux", "render", None)
+    assert [e for e in log if e[1] == "record_stream"] and \
+        all(s == "aux" for s, op, _ in log if op == "record_stream")
+    assert img._s3_stream is aux
+    log.clear()
+    fe._finish_render(img, 3, "gs_track")
+    assert [s for s, op, _ in log if op in ("copy", "record")] == ["aux", "aux"]
+    assert fe._pending and fe._stats["rendered"] == 1
