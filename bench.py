@@ -1213,6 +1213,7 @@ def main(argv=None):
                    "parallelism": f"replicas x{ws} (tracker path does not shard)",
                    "encoder_batch": kb, "encoder_ahead": a.enc_ahead,
                    "decode_ahead": a.decode_ahead, "render_async": a.render_async,
+                   "render_stream": "aux" if getattr(fe, "render_on_aux", False) else "main",
                    "timed_encodes": encodes, "planned_encodes": plan["timed_encodes"]},
         "msplats_per_s": P_frame * st["rendered"] * ws / t_max / 1e6,
         "critical_path": crit,
