@@ -1,6 +1,8 @@
 // Memory-bound network ops (include/s3n.h): LayerNorm, patch im2col,
 // bilinear x2 upsample, Gaussian-head postprocess, portable PRNG fill, cast.
 // All vectorised to 16 B per lane where the layout allows (guide G13).
+#include <cstdlib>
+
 #include "common.hpp"
 #include "s3n.h"
 
@@ -120,37 +122,52 @@ struct UpP {
 
 // Idx = uint32_t when B * oh * ow * C/8 < 2^31 (every frame-loop shape):
 // the per-thread index split is then 32-bit division, not the ~4x longer
-// 64-bit sequences.
-template <typename Idx>
+// 64-bit sequences.  PX output pixels along x per thread (2: one index
+// split and the row offsets for both; the same per-pixel arithmetic).
+template <typename Idx, int PX>
 __global__ void __launch_bounds__(kThreads) k_upsample2x(UpP p) {
   const int g = blockIdx.y;
   const int OH = 2 * p.H, OW = 2 * p.W, C8 = p.C / 8;
-  const Idx total = (Idx)p.B * p.oh * p.ow * C8;
+  const int owp = (p.ow + PX - 1) / PX;
+  const Idx total = (Idx)p.B * p.oh * owp * C8;
   const Idx i = (Idx)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c8 = (int)(i % (Idx)C8);
   Idx t = i / (Idx)C8;
-  const int ox = (int)(t % (Idx)p.ow);
-  t /= (Idx)p.ow;
+  const int ox0 = (int)(t % (Idx)owp) * PX;
+  t /= (Idx)owp;
   const int oy = (int)(t % (Idx)p.oh);
   const int b = (int)(t / (Idx)p.oh);
   const float sh = OH > 1 ? (float)(p.H - 1) / (float)(OH - 1) : 0.f;
   const float sw = OW > 1 ? (float)(p.W - 1) / (float)(OW - 1) : 0.f;
-  const float fy = sh * oy, fx = sw * ox;
-  const int y0 = (int)fy, x0 = (int)fx;
-  const int y1 = min(y0 + 1, p.H - 1), x1 = min(x0 + 1, p.W - 1);
-  const float ly = fy - y0, lx = fx - x0;
-  const float hy = 1.f - ly, hx = 1.f - lx;
+  const float fy = sh * oy;
+  const int y0 = (int)fy;
+  const int y1 = min(y0 + 1, p.H - 1);
+  const float ly = fy - y0;
+  const float hy = 1.f - ly;
   const f16* src = p.in[g] + (int64_t)b * p.H * p.W * p.C + c8 * 8;
-  const f16x8 a = *reinterpret_cast<const f16x8*>(src + ((int64_t)y0 * p.W + x0) * p.C);
-  const f16x8 bq = *reinterpret_cast<const f16x8*>(src + ((int64_t)y0 * p.W + x1) * p.C);
-  const f16x8 cq = *reinterpret_cast<const f16x8*>(src + ((int64_t)y1 * p.W + x0) * p.C);
-  const f16x8 d = *reinterpret_cast<const f16x8*>(src + ((int64_t)y1 * p.W + x1) * p.C);
-  f16x8 o;
+  const f16* r0 = src + (int64_t)y0 * p.W * p.C;
+  const f16* r1 = src + (int64_t)y1 * p.W * p.C;
+  f16* dst = p.out[g] + (((int64_t)b * p.oh + oy) * p.ow) * p.C + c8 * 8;
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    o[j] = (f16)(hy * (hx * (float)a[j] + lx * (float)bq[j]) + ly * (hx * (float)cq[j] + lx * (float)d[j]));
-  *reinterpret_cast<f16x8*>(p.out[g] + (((int64_t)b * p.oh + oy) * p.ow + ox) * p.C + c8 * 8) = o;
+  for (int k = 0; k < PX; ++k) {
+    const int ox = ox0 + k;
+    if (PX > 1 && ox >= p.ow) break;
+    const float fx = sw * ox;
+    const int x0 = (int)fx;
+    const int x1 = min(x0 + 1, p.W - 1);
+    const float lx = fx - x0;
+    const float hx = 1.f - lx;
+    const f16x8 a = *reinterpret_cast<const f16x8*>(r0 + (int64_t)x0 * p.C);
+    const f16x8 bq = *reinterpret_cast<const f16x8*>(r0 + (int64_t)x1 * p.C);
+    const f16x8 cq = *reinterpret_cast<const f16x8*>(r1 + (int64_t)x0 * p.C);
+    const f16x8 d = *reinterpret_cast<const f16x8*>(r1 + (int64_t)x1 * p.C);
+    f16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      o[j] = (f16)(hy * (hx * (float)a[j] + lx * (float)bq[j]) + ly * (hx * (float)cq[j] + lx * (float)d[j]));
+    *reinterpret_cast<f16x8*>(dst + (int64_t)ox * p.C) = o;
+  }
 }
 
 // ------------------------------------------------------ postprocess -------
@@ -314,12 +331,21 @@ int s3n_upsample2x(int groups, const void* const* in, void* const* out, int B, i
     p.in[g] = g < groups ? (const f16*)in[g] : nullptr;
     p.out[g] = g < groups ? (f16*)out[g] : nullptr;
   }
-  const int64_t total = (int64_t)B * oh * ow * (C / 8);
+  // S3_UPSAMPLE_PX=1 / 4: output pixels per thread (A/B)
+  static const int px = [] {
+    const char* e = std::getenv("S3_UPSAMPLE_PX");
+    return e && e[0] == '1' ? 1 : (e && e[0] == '4' ? 4 : 2);
+  }();
+  const int64_t total = (int64_t)B * oh * ((ow + px - 1) / px) * (C / 8);
   dim3 grid((unsigned)s3::cdiv(total, kThreads), (unsigned)groups);
-  if (total < ((int64_t)1 << 31))
-    k_upsample2x<uint32_t><<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
-  else
-    k_upsample2x<int64_t><<<grid, kThreads, 0, s3::as_stream(stream)>>>(p);
+  hipStream_t st = s3::as_stream(stream);
+  const bool small = (int64_t)B * oh * ow * (C / 8) < ((int64_t)1 << 31);
+  if (px == 4 && small) k_upsample2x<uint32_t, 4><<<grid, kThreads, 0, st>>>(p);
+  else if (px == 4) k_upsample2x<int64_t, 4><<<grid, kThreads, 0, st>>>(p);
+  else if (px == 2 && small) k_upsample2x<uint32_t, 2><<<grid, kThreads, 0, st>>>(p);
+  else if (px == 2) k_upsample2x<int64_t, 2><<<grid, kThreads, 0, st>>>(p);
+  else if (small) k_upsample2x<uint32_t, 1><<<grid, kThreads, 0, st>>>(p);
+  else k_upsample2x<int64_t, 1><<<grid, kThreads, 0, st>>>(p);
   S3_LAUNCH_CHECK();
   return S3_OK;
 }
